@@ -1,0 +1,272 @@
+"""Generate the golden vectors that pin the oracle and the HIP path to the reference.
+
+Run in the build container only (the GPU box has no /root/reference):
+
+    python tests/golden/make_golden.py
+
+What it does
+  1. ``make -C oracle ref`` compiles the reference's own C++ core from its sources where they lie
+     (/root/reference/openke/base/Base.cpp) into ``oracle/_ref/Base.so`` (git-ignored).
+  2. Copies the reference *Python* package to a throw-away temp dir (never into this repo), drops
+     the freshly built Base.so into ``<tmp>/openke/release/`` (where its ctypes loaders look,
+     TrainDataLoader.py:30-31) and imports it on CPU.
+  3. Writes the synthetic datasets ``tests/golden/kg_small`` and ``kg_tiny`` (headerless format)
+     and, one subprocess per case (the reference keeps process-global C state, Base.cpp:16-168),
+     records inputs and outputs as compressed ``.npz`` fixtures next to this script.
+
+The fixtures are data: inputs (seeds, configs, initial tables, batches) and the reference's
+outputs (batches, losses, updated tables, universe maps, link-prediction metrics).
+"""
+import ctypes
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(REPO, "openke-putranse_amd", "tools"))
+import synth_kg  # noqa: E402
+
+DATASETS = {"small": os.path.join(HERE, "kg_small") + os.sep, "tiny": os.path.join(HERE, "kg_tiny") + os.sep}
+
+SAMPLER_CASES = [
+    # name, dataset, threads, batch_size, neg_ent, bern, filter, seed
+    ("s1", "small", 8, 375, 1, 0, 0, 7),
+    ("s2", "small", 8, 123, 3, 1, 1, 11),
+    ("s3", "small", 3, 50, 25, 1, 1, 4),
+    ("s4", "small", 1, 64, 2, 0, 1, 0),
+    ("s5", "small", 8, 5, 1, 1, 0, 3),
+    ("s6", "tiny", 8, 37, 4, 1, 1, 9),
+    ("s7", "tiny", 8, 16, 1, 0, 0, 2),
+]
+
+TRAIN_CASES = [
+    # name, model, dim, p_norm, norm_flag, opt, lr, margin, threads, bs, neg, bern, filter, seed, torch_seed, steps
+    ("t1", "TransE", 16, 1, True, "sgd", 0.5, 5.0, 8, 375, 1, 0, 0, 7, 1, 5),
+    ("t2", "TransE", 32, 2, True, "sgd", 1.0, 5.0, 8, 100, 25, 1, 1, 4, 2, 3),
+    ("t3", "TransE", 20, 1, True, "adagrad", 0.05, 2.0, 8, 150, 1, 0, 0, 5, 3, 6),
+    ("t4", "TransH", 20, 1, True, "adagrad", 0.03, 3.0, 8, 150, 1, 0, 0, 6, 4, 5),
+    ("t5", "TransH", 16, 2, True, "sgd", 0.5, 4.0, 8, 60, 4, 1, 1, 8, 5, 3),
+    ("t6", "TransE", 12, 2, False, "sgd", 0.1, 3.0, 8, 200, 2, 0, 1, 9, 6, 4),
+    ("t7", "TransE", 64, 2, True, "adagrad", 0.1, 1.0, 4, 90, 3, 1, 0, 10, 7, 4),
+]
+
+UNIVERSE_CASES = [
+    # name, model, dim, p_norm, n_universes, min_tc, max_tc, const_epochs, seed
+    ("u1", "TransE", 8, 1, 6, 200, 400, 2, 123),
+    ("u2", "TransH", 8, 1, 3, 150, 300, 2, 77),
+    ("u3", "TransE", 12, 2, 4, 300, 600, 3, 5),
+]
+
+LP_CASES = [
+    # name, model, dim, p_norm, torch_seed
+    ("l1", "TransE", 16, 1, 21),
+    ("l2", "TransH", 10, 2, 22),
+]
+
+
+def _import_reference(tmp):
+    dst = os.path.join(tmp, "openke")
+    if not os.path.exists(dst):
+        shutil.copytree(os.path.join(REF, "openke"), dst)
+        os.makedirs(os.path.join(dst, "release"), exist_ok=True)
+        shutil.copy(os.path.join(REPO, "oracle", "_ref", "Base.so"), os.path.join(dst, "release", "Base.so"))
+    sys.path.insert(0, tmp)
+
+
+def _silence():
+    # the reference prints from C (printf) and Python (tqdm); keep our own logs readable
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    os.dup2(devnull, 1)
+
+
+def case_glibc(out):
+    libc = ctypes.CDLL("libc.so.6")
+    seeds = [0, 1, 4, 5, 123, 2147483647, 4 + 17]
+    vals = []
+    for s in seeds:
+        libc.srand(ctypes.c_uint(s))
+        vals.append([libc.rand() for _ in range(400)])
+    np.savez_compressed(out, seeds=np.array(seeds, dtype=np.int64), values=np.array(vals, dtype=np.int64))
+
+
+def case_sampler(out, name, ds, threads, bs, neg, bern, filt, seed):
+    from openke.data import TrainDataLoader
+    dl = TrainDataLoader(in_path=DATASETS[ds], batch_size=bs, threads=threads, sampling_mode="normal",
+                         bern_flag=bern, filter_flag=filt, neg_ent=neg, neg_rel=0, random_seed=seed)
+    hs, ts, rs, ys = [], [], [], []
+    for _ in range(3):
+        d = dl.sampling()
+        hs.append(d["batch_h"].copy()); ts.append(d["batch_t"].copy())
+        rs.append(d["batch_r"].copy()); ys.append(d["batch_y"].copy())
+    np.savez_compressed(out, threads=threads, batch_size=bs, neg_ent=neg, bern=bern, filter=filt, seed=seed,
+                        dataset=ds, batch_h=np.stack(hs), batch_t=np.stack(ts), batch_r=np.stack(rs),
+                        batch_y=np.stack(ys))
+
+
+def case_train(out, name, model, dim, p, norm_flag, opt, lr, margin, threads, bs, neg, bern, filt, seed, tseed,
+               steps):
+    import torch
+    from openke.config import Trainer
+    from openke.data import TrainDataLoader
+    from openke.module.loss import MarginLoss
+    from openke.module.model import TransE, TransH
+    from openke.module.strategy import NegativeSampling
+    dl = TrainDataLoader(in_path=DATASETS["small"], batch_size=bs, threads=threads, sampling_mode="normal",
+                         bern_flag=bern, filter_flag=filt, neg_ent=neg, neg_rel=0, random_seed=seed)
+    torch.manual_seed(tseed)
+    cls = TransE if model == "TransE" else TransH
+    kge = cls(ent_tot=dl.get_ent_tot(), rel_tot=dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=norm_flag)
+    init = {k: v.detach().clone().numpy() for k, v in kge.state_dict().items() if "embeddings" in k or "norm_vector" in k}
+    ns = NegativeSampling(model=kge, loss=MarginLoss(margin=margin), batch_size=dl.get_batch_size())
+    tr = Trainer(model=ns, data_loader=dl, train_times=0, alpha=lr, use_gpu=False, opt_method=opt)
+    tr.run()  # builds the optimizer (train_times=0 runs no epoch)
+    losses, bh, bt, br, snaps = [], [], [], [], []
+    for s in range(steps):
+        d = dl.sampling()
+        bh.append(d["batch_h"].copy()); bt.append(d["batch_t"].copy()); br.append(d["batch_r"].copy())
+        losses.append(tr.train_one_step(d))
+        if s == 0:
+            snaps.append({k: v.detach().clone().numpy() for k, v in kge.state_dict().items() if k in init})
+    final = {k: v.detach().clone().numpy() for k, v in kge.state_dict().items() if k in init}
+    arrs = {}
+    for k in init:
+        short = k.split(".")[0]
+        arrs["init_" + short] = init[k]
+        arrs["step1_" + short] = snaps[0][k]
+        arrs["final_" + short] = final[k]
+    np.savez_compressed(out, model=model, dim=dim, p_norm=p, norm_flag=norm_flag, opt=opt, lr=lr, margin=margin,
+                        threads=threads, batch_size=bs, neg_ent=neg, bern=bern, filter=filt, seed=seed,
+                        torch_seed=tseed, steps=steps, losses=np.array(losses, dtype=np.float64),
+                        batch_h=np.stack(bh), batch_t=np.stack(bt), batch_r=np.stack(br), **arrs)
+
+
+def case_universes(out, name, model, dim, p, n_univ, min_tc, max_tc, epochs, seed):
+    import torch
+    from openke.config import Parallel_Universe_Config
+    from openke.data import TestDataLoader, TrainDataLoader
+    from openke.module.model import TransE, TransH
+    dl = TrainDataLoader(in_path=DATASETS["small"], nbatches=20, threads=8, sampling_mode="normal", bern_flag=0,
+                         filter_flag=0, neg_ent=1, neg_rel=0, random_seed=seed)
+    test_dl = TestDataLoader(dl.in_path, "link")  # re-seeds the C RNG to 4 (TestDataLoader.py:29, :88)
+    cls = TransE if model == "TransE" else TransH
+    pu = Parallel_Universe_Config(training_identifier=name, train_dataloader=dl, test_dataloader=test_dl,
+                                  initial_num_universes=None, min_margin=1, max_margin=4, min_lr=0.001, max_lr=0.1,
+                                  min_num_epochs=50, max_num_epochs=200, const_num_epochs=epochs,
+                                  min_triple_constraint=min_tc, max_triple_constraint=max_tc, min_balance=0.25,
+                                  max_balance=0.5, embedding_model=cls,
+                                  embedding_model_param={"dim": dim, "p_norm": p, "norm_flag": 1},
+                                  checkpoint_dir=tempfile.mkdtemp() + "/", valid_steps=10 ** 6, save_steps=None,
+                                  training_setting="static", incremental_strategy=None)
+    seed0 = pu.initial_random_seed
+    # capture the per-universe draws the same way train_parallel_universes does (:320-328),
+    # plus the first sampled batch of every universe (taken on a second, identical construction)
+    pu.train_parallel_universes(n_univ)
+    rec = {"seed0": seed0, "n_univ": n_univ}
+    for u in range(n_univ):
+        sp = pu.trained_embedding_spaces[u]
+        ent_map = pu.entity_id_mappings[u]
+        rel_map = pu.relation_id_mappings[u]
+        ent_remap = np.full(len(ent_map), -1, dtype=np.int64)
+        for g, l in ent_map.items():
+            ent_remap[l] = g
+        rel_remap = np.full(len(rel_map), -1, dtype=np.int64)
+        for g, l in rel_map.items():
+            rel_remap[l] = g
+        rec["u%d_ent_remap" % u] = ent_remap
+        rec["u%d_rel_remap" % u] = rel_remap
+        rec["u%d_ent" % u] = sp.ent_embeddings.weight.detach().numpy().copy()
+        rec["u%d_rel" % u] = sp.rel_embeddings.weight.detach().numpy().copy()
+        if model == "TransH":
+            rec["u%d_norm" % u] = sp.norm_vector.weight.detach().numpy().copy()
+    # universe construction + first batch, restated from the same seeds (state after training is reset)
+    for u in range(n_univ):
+        pu.set_random_seed(seed0 + u)
+        import random
+        tc = random.randrange(min_tc, max_tc)
+        bal = round(random.uniform(0.25, 0.5), 2)
+        dl.compile_universe_dataset(tc, bal)
+        rec["u%d_tc" % u] = tc
+        rec["u%d_balance" % u] = bal
+        rec["u%d_train_total" % u] = dl.lib.getTrainTotalUniverse()
+        margin = random.randrange(1, 4)
+        lr = round(random.uniform(0.001, 0.1), len(str(0.001).split('.')[1]))
+        rec["u%d_margin" % u] = margin
+        rec["u%d_lr" % u] = lr
+        dl.swap_helpers()
+        d = dl.sampling()
+        rec["u%d_b_h" % u] = d["batch_h"].copy()
+        rec["u%d_b_t" % u] = d["batch_t"].copy()
+        rec["u%d_b_r" % u] = d["batch_r"].copy()
+        dl.reset_universe()
+    mrr_etc = pu_lp(pu)
+    rec["lp"] = np.array(mrr_etc, dtype=np.float64)
+    np.savez_compressed(out, model=model, dim=dim, p_norm=p, min_tc=min_tc, max_tc=max_tc, epochs=epochs, seed=seed,
+                        **rec)
+
+
+def pu_lp(pu):
+    # Parallel_Universe_Config.run_link_prediction prints instead of returning; call the same chain
+    pu.data_loader.set_sampling_mode('link')
+    pu.eval_universes(eval_mode='test')
+    from openke.config import Tester
+    return Tester.run_link_prediction(pu, False)
+
+
+def case_lp(out, name, model, dim, p, tseed):
+    import torch
+    from openke.config import Tester
+    from openke.data import TestDataLoader
+    from openke.module.model import TransE, TransH
+    test_dl = TestDataLoader(DATASETS["small"], "link")
+    torch.manual_seed(tseed)
+    cls = TransE if model == "TransE" else TransH
+    kge = cls(ent_tot=test_dl.get_ent_tot(), rel_tot=test_dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=True)
+    tables = {k.split(".")[0]: v.detach().numpy().copy() for k, v in kge.state_dict().items()
+              if "embeddings" in k or "norm_vector" in k}
+    tester = Tester(model=kge, data_loader=test_dl, use_gpu=False)
+    res = tester.run_link_prediction(type_constrain=False)
+    np.savez_compressed(out, model=model, dim=dim, p_norm=p, torch_seed=tseed,
+                        metrics=np.array(res, dtype=np.float64), **tables)
+
+
+def run_case(kind, args_json, out, tmp):
+    args = json.loads(args_json)
+    _import_reference(tmp)
+    _silence()
+    {"glibc": case_glibc, "sampler": case_sampler, "train": case_train, "universes": case_universes,
+     "lp": case_lp}[kind](out, *args)
+
+
+def main():
+    subprocess.check_call(["make", "-C", os.path.join(REPO, "oracle"), "ref"])
+    for ds, path in DATASETS.items():
+        if not os.path.exists(os.path.join(path, "test2id.txt")):
+            synth_kg.write_dataset(path, *synth_kg.SHAPES[ds], seed=0, ent_skew=synth_kg.ENT_SKEW[ds])
+    tmp = tempfile.mkdtemp(prefix="refpy_")
+    jobs = [("glibc", [], "glibc_rand.npz")]
+    jobs += [("sampler", list(c), "sampler_%s.npz" % c[0]) for c in SAMPLER_CASES]
+    jobs += [("train", list(c), "train_%s.npz" % c[0]) for c in TRAIN_CASES]
+    jobs += [("universes", list(c), "universes_%s.npz" % c[0]) for c in UNIVERSE_CASES]
+    jobs += [("lp", list(c), "lp_%s.npz" % c[0]) for c in LP_CASES]
+    only = sys.argv[1:]
+    for kind, args, fname in jobs:
+        if only and not any(fname.startswith(o) for o in only):
+            continue
+        out = os.path.join(HERE, fname)
+        print("generating", fname, flush=True)
+        subprocess.check_call([sys.executable, os.path.abspath(__file__), "--case", kind, json.dumps(args), out, tmp])
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--case":
+        run_case(*sys.argv[2:6])
+    else:
+        main()
