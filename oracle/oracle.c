@@ -1,0 +1,680 @@
+/*
+ * CPU ORACLE — test infrastructure only (see oracle.h). Restates the reference algorithm; each
+ * function cites the reference file:line it follows. Parity is pinned by tests/test_oracle.py
+ * against fixtures produced by the reference itself (tests/golden/make_golden.py).
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- glibc rand (TYPE_3) ----------- */
+/* glibc stdlib/random_r.c: srandom_r seeds 31 words with 16807*x mod (2^31-1) (Schrage form), sets
+ * the feedback pointers 3 apart and discards 310 outputs; random_r adds the two taps and returns
+ * the sum >> 1. The reference calls it through srand()/rand() (Random.h:37-45, :32-34). */
+void orand_seed(orand_t *g, uint32_t seed) {
+    if (seed == 0) seed = 1;
+    int32_t word = (int32_t)seed;
+    g->state[0] = word;
+    for (int i = 1; i < 31; ++i) {
+        long hi = word / 127773;
+        long lo = word % 127773;
+        word = (int32_t)(16807 * lo - 2836 * hi);
+        if (word < 0) word += 2147483647;
+        g->state[i] = word;
+    }
+    g->f = 3;
+    g->r = 0;
+    for (int i = 0; i < 310; ++i) (void)orand_next(g);
+}
+
+int32_t orand_next(orand_t *g) {
+    uint32_t val = (uint32_t)g->state[g->f] + (uint32_t)g->state[g->r];
+    g->state[g->f] = (int32_t)val;
+    int32_t result = (int32_t)(val >> 1);
+    if (++g->f >= 31) {
+        g->f = 0;
+        ++g->r;
+    } else if (++g->r >= 31) {
+        g->r = 0;
+    }
+    return result;
+}
+
+/* rand(a,b) = rand() % (b-a) + a   (Random.h:32-34) */
+static int64_t orand_range(orand_t *g, int64_t a, int64_t b) { return (int64_t)orand_next(g) % (b - a) + a; }
+
+/* ---------------------------------------------------------------- per-thread LCG --------------- */
+/* randd / rand_max (Random.h:18-29) */
+static inline uint64_t lcg_next(uint64_t *s) {
+    *s = *s * 25214903917ULL + 11ULL;
+    return *s;
+}
+static inline int64_t lcg_max(uint64_t *s, int64_t x) { return (int64_t)(lcg_next(s) % (uint64_t)x); }
+
+void oracle_rand_reset(orand_t *g, int64_t threads, uint64_t *states) {
+    for (int64_t i = 0; i < threads; ++i) states[i] = (uint64_t)(int64_t)orand_next(g);
+}
+
+/* ---------------------------------------------------------------- graph + helpers -------------- */
+static int cmp_head(const void *a, const void *b) {   /* Triple.h:7-9 */
+    const otriple *x = a, *y = b;
+    if (x->h != y->h) return x->h < y->h ? -1 : 1;
+    if (x->r != y->r) return x->r < y->r ? -1 : 1;
+    if (x->t != y->t) return x->t < y->t ? -1 : 1;
+    return 0;
+}
+static int cmp_tail(const void *a, const void *b) {   /* Triple.h:11-13 */
+    const otriple *x = a, *y = b;
+    if (x->t != y->t) return x->t < y->t ? -1 : 1;
+    if (x->r != y->r) return x->r < y->r ? -1 : 1;
+    if (x->h != y->h) return x->h < y->h ? -1 : 1;
+    return 0;
+}
+static int cmp_rel(const void *a, const void *b) {    /* Triple.h:15-17 */
+    const otriple *x = a, *y = b;
+    if (x->h != y->h) return x->h < y->h ? -1 : 1;
+    if (x->t != y->t) return x->t < y->t ? -1 : 1;
+    if (x->r != y->r) return x->r < y->r ? -1 : 1;
+    return 0;
+}
+static int cmp_rel2(const void *a, const void *b) {   /* Triple.h:19-21 */
+    const otriple *x = a, *y = b;
+    if (x->r != y->r) return x->r < y->r ? -1 : 1;
+    if (x->h != y->h) return x->h < y->h ? -1 : 1;
+    if (x->t != y->t) return x->t < y->t ? -1 : 1;
+    return 0;
+}
+
+static int64_t count_lines(FILE *f) {                 /* Utilities.h:47-57 */
+    int64_t n = 0;
+    int c;
+    while ((c = getc(f)) != EOF)
+        if (c == '\n') ++n;
+    rewind(f);
+    return n;
+}
+
+static int64_t *alloc_i64(int64_t n, int fill_minus_one) {
+    int64_t *p = calloc((size_t)(n > 0 ? n : 1), sizeof(int64_t));
+    if (fill_minus_one) memset(p, -1, sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    return p;
+}
+
+/* Builds the four sorted copies, the [lef,rig] ranges and left/right means. `universe_form` selects
+ * loadUniverseHelpers (UniverseConstructor.h:235-325: rig arrays -1 only on [0,E_u), freqRel from the
+ * list itself) over loadHelpers (Reader.h:58-167). Both give identical arrays on a deduplicated list. */
+static void build_helpers(okg *g) {
+    int64_t n = g->train_total, E = g->ent_total, R = g->rel_total;
+    qsort(g->train_list, (size_t)n, sizeof(otriple), cmp_head);
+    g->train_head = malloc(sizeof(otriple) * (size_t)(n ? n : 1));
+    g->train_tail = malloc(sizeof(otriple) * (size_t)(n ? n : 1));
+    g->train_rel = malloc(sizeof(otriple) * (size_t)(n ? n : 1));
+    g->train_rel2 = malloc(sizeof(otriple) * (size_t)(n ? n : 1));
+    g->freq_ent = alloc_i64(E, 0);
+    g->freq_rel = alloc_i64(R, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        g->train_head[i] = g->train_tail[i] = g->train_rel[i] = g->train_rel2[i] = g->train_list[i];
+        g->freq_ent[g->train_list[i].h]++;
+        g->freq_ent[g->train_list[i].t]++;
+        g->freq_rel[g->train_list[i].r]++;
+    }
+    qsort(g->train_head, (size_t)n, sizeof(otriple), cmp_head);
+    qsort(g->train_tail, (size_t)n, sizeof(otriple), cmp_tail);
+    qsort(g->train_rel, (size_t)n, sizeof(otriple), cmp_rel);
+    qsort(g->train_rel2, (size_t)n, sizeof(otriple), cmp_rel2);
+    g->lef_head = alloc_i64(E, 0); g->rig_head = alloc_i64(E, 1);
+    g->lef_tail = alloc_i64(E, 0); g->rig_tail = alloc_i64(E, 1);
+    g->lef_rel = alloc_i64(E, 0);  g->rig_rel = alloc_i64(E, 1);
+    g->lef_rel2 = alloc_i64(R, 0); g->rig_rel2 = alloc_i64(R, 1);
+    for (int64_t i = 1; i < n; ++i) {
+        if (g->train_tail[i].t != g->train_tail[i - 1].t) {
+            g->rig_tail[g->train_tail[i - 1].t] = i - 1;
+            g->lef_tail[g->train_tail[i].t] = i;
+        }
+        if (g->train_head[i].h != g->train_head[i - 1].h) {
+            g->rig_head[g->train_head[i - 1].h] = i - 1;
+            g->lef_head[g->train_head[i].h] = i;
+        }
+        if (g->train_rel[i].h != g->train_rel[i - 1].h) {
+            g->rig_rel[g->train_rel[i - 1].h] = i - 1;
+            g->lef_rel[g->train_rel[i].h] = i;
+        }
+        if (g->train_rel2[i].r != g->train_rel2[i - 1].r) {
+            g->rig_rel2[g->train_rel2[i - 1].r] = i - 1;
+            g->lef_rel2[g->train_rel2[i].r] = i;
+        }
+    }
+    if (n > 0) {
+        g->lef_head[g->train_head[0].h] = 0;
+        g->rig_head[g->train_head[n - 1].h] = n - 1;
+        g->lef_tail[g->train_tail[0].t] = 0;
+        g->rig_tail[g->train_tail[n - 1].t] = n - 1;
+        g->lef_rel[g->train_rel[0].h] = 0;
+        g->rig_rel[g->train_rel[n - 1].h] = n - 1;
+        g->lef_rel2[g->train_rel2[0].r] = 0;
+        g->rig_rel2[g->train_rel2[n - 1].r] = n - 1;
+    }
+    g->left_mean = calloc((size_t)(R ? R : 1), sizeof(float));
+    g->right_mean = calloc((size_t)(R ? R : 1), sizeof(float));
+    for (int64_t i = 0; i < E; ++i) {
+        for (int64_t j = g->lef_head[i] + 1; j <= g->rig_head[i]; ++j)
+            if (g->train_head[j].r != g->train_head[j - 1].r) g->left_mean[g->train_head[j].r] += 1.0f;
+        if (g->lef_head[i] <= g->rig_head[i]) g->left_mean[g->train_head[g->lef_head[i]].r] += 1.0f;
+        for (int64_t j = g->lef_tail[i] + 1; j <= g->rig_tail[i]; ++j)
+            if (g->train_tail[j].r != g->train_tail[j - 1].r) g->right_mean[g->train_tail[j].r] += 1.0f;
+        if (g->lef_tail[i] <= g->rig_tail[i]) g->right_mean[g->train_tail[g->lef_tail[i]].r] += 1.0f;
+    }
+    for (int64_t i = 0; i < R; ++i) {
+        g->left_mean[i] = (float)g->freq_rel[i] / g->left_mean[i];
+        g->right_mean[i] = (float)g->freq_rel[i] / g->right_mean[i];
+    }
+}
+
+okg *okg_load(const char *dir) {                      /* importTrainFiles, Reader.h:169-234 */
+    char path[4096];
+    okg *g = calloc(1, sizeof(okg));
+    snprintf(path, sizeof path, "%srelation2id.txt", dir);
+    FILE *f = fopen(path, "r");
+    if (!f) { free(g); return NULL; }
+    g->rel_total = count_lines(f);
+    fclose(f);
+    snprintf(path, sizeof path, "%sentity2id.txt", dir);
+    f = fopen(path, "r");
+    if (!f) { free(g); return NULL; }
+    g->ent_total = count_lines(f);
+    fclose(f);
+    snprintf(path, sizeof path, "%strain2id.txt", dir);
+    f = fopen(path, "r");
+    if (!f) { free(g); return NULL; }
+    int64_t n = count_lines(f);
+    g->train_list = calloc((size_t)(n ? n : 1), sizeof(otriple));
+    for (int64_t i = 0; i < n; ++i) {
+        long a = 0, b = 0, c = 0;
+        if (fscanf(f, "%ld %ld %ld", &a, &b, &c) != 3) break;
+        g->train_list[i].h = a; g->train_list[i].t = b; g->train_list[i].r = c;
+    }
+    fclose(f);
+    qsort(g->train_list, (size_t)n, sizeof(otriple), cmp_head);
+    int64_t m = n ? 1 : 0;
+    for (int64_t i = 1; i < n; ++i)
+        if (cmp_head(&g->train_list[i], &g->train_list[i - 1]) != 0) g->train_list[m++] = g->train_list[i];
+    g->train_total = m;
+    build_helpers(g);
+    return g;
+}
+
+void okg_free(okg *g) {
+    if (!g) return;
+    free(g->train_list); free(g->train_head); free(g->train_tail); free(g->train_rel); free(g->train_rel2);
+    free(g->lef_head); free(g->rig_head); free(g->lef_tail); free(g->rig_tail);
+    free(g->lef_rel); free(g->rig_rel); free(g->lef_rel2); free(g->rig_rel2);
+    free(g->freq_ent); free(g->freq_rel); free(g->left_mean); free(g->right_mean);
+    free(g);
+}
+int64_t okg_ent_total(const okg *g) { return g->ent_total; }
+int64_t okg_rel_total(const okg *g) { return g->rel_total; }
+int64_t okg_train_total(const okg *g) { return g->train_total; }
+float okg_left_mean(const okg *g, int64_t r) { return g->left_mean[r]; }
+float okg_right_mean(const okg *g, int64_t r) { return g->right_mean[r]; }
+void okg_get_train(const okg *g, int64_t *h, int64_t *t, int64_t *r) {
+    for (int64_t i = 0; i < g->train_total; ++i) {
+        h[i] = g->train_list[i].h; t[i] = g->train_list[i].t; r[i] = g->train_list[i].r;
+    }
+}
+
+/* ---------------------------------------------------------------- negative corruption --------- */
+/* corrupt_head / corrupt_tail with filter (Corrupt.h:27-56, :75-104). `heads` selects the head-sorted
+ * list (corrupt_head: returns a replacement TAIL avoiding known (h,r,.) tails). */
+static int64_t corrupt_filtered(const okg *g, int heads, int64_t key, int64_t r, uint64_t *s) {
+    const otriple *L = heads ? g->train_head : g->train_tail;
+    const int64_t *lef = heads ? g->lef_head : g->lef_tail, *rig = heads ? g->rig_head : g->rig_tail;
+#define VAL(k) (heads ? L[(k)].t : L[(k)].h)
+    int64_t lo = lef[key] - 1, hi = rig[key], mid;
+    while (lo + 1 < hi) {
+        mid = (lo + hi) >> 1;
+        if (L[mid].r >= r) hi = mid; else lo = mid;
+    }
+    int64_t ll = hi;
+    lo = lef[key];
+    hi = rig[key] + 1;
+    while (lo + 1 < hi) {
+        mid = (lo + hi) >> 1;
+        if (L[mid].r <= r) lo = mid; else hi = mid;
+    }
+    int64_t rr = lo;
+    int64_t tmp = lcg_max(s, g->ent_total - (rr - ll + 1));
+    if (tmp < VAL(ll)) return tmp;
+    if (tmp > VAL(rr) - rr + ll - 1) return tmp + rr - ll + 1;
+    lo = ll;
+    hi = rr + 1;
+    while (lo + 1 < hi) {
+        mid = (lo + hi) >> 1;
+        if (VAL(mid) - mid + ll - 1 < tmp) lo = mid; else hi = mid;
+    }
+    return tmp + lo - ll + 1;
+#undef VAL
+}
+
+/* unfiltered: uniform over [0,E-1) skipping the PASSED entity (Corrupt.h:18-25, :68-74) */
+static int64_t corrupt_plain(const okg *g, int64_t skip, uint64_t *s) {
+    int64_t tmp = lcg_max(s, g->ent_total - 1);
+    return tmp < skip ? tmp : tmp + 1;
+}
+
+/* getBatch (Base.cpp:185-264) for every sampler thread in turn; threads write disjoint slices. */
+void oracle_sampling(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
+                     int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y) {
+    for (int64_t id = 0; id < threads; ++id) {
+        int64_t lef, rig;
+        if (bs % threads == 0) {
+            lef = id * (bs / threads);
+            rig = (id + 1) * (bs / threads);
+        } else {
+            lef = id * (bs / threads + 1);
+            rig = (id + 1) * (bs / threads + 1);
+            if (rig > bs) rig = bs;
+        }
+        uint64_t *s = &states[id];
+        float prob = 500;
+        for (int64_t b = lef; b < rig; ++b) {
+            int64_t i = lcg_max(s, g->train_total);
+            otriple p = g->train_list[i];
+            h[b] = p.h; t[b] = p.t; r[b] = p.r; y[b] = 1;
+            int64_t last = bs;
+            for (int64_t k = 0; k < neg; ++k) {
+                if (bern) prob = 1000 * g->right_mean[p.r] / (g->right_mean[p.r] + g->left_mean[p.r]);
+                if ((float)(lcg_next(s) % 1000) < prob) {
+                    h[b + last] = p.h;
+                    t[b + last] = filter ? corrupt_filtered(g, 1, p.h, p.r, s) : corrupt_plain(g, p.h, s);
+                    r[b + last] = p.r;
+                } else {
+                    h[b + last] = filter ? corrupt_filtered(g, 0, p.t, p.r, s) : corrupt_plain(g, p.t, s);
+                    t[b + last] = p.t;
+                    r[b + last] = p.r;
+                }
+                y[b + last] = -1;
+                last += bs;
+            }
+        }
+    }
+}
+
+/* ---------------------------------------------------------------- universe construction ------- */
+typedef struct { int64_t *a; int64_t n, cap; } iset;   /* sorted set, std::set<INT> iteration order */
+static void iset_init(iset *s) { s->n = 0; s->cap = 16; s->a = malloc(sizeof(int64_t) * 16); }
+static int64_t iset_lb(const iset *s, int64_t v) {
+    int64_t lo = 0, hi = s->n;
+    while (lo < hi) {
+        int64_t m = (lo + hi) / 2;
+        if (s->a[m] < v) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+static void iset_insert(iset *s, int64_t v) {
+    int64_t i = iset_lb(s, v);
+    if (i < s->n && s->a[i] == v) return;
+    if (s->n == s->cap) { s->cap *= 2; s->a = realloc(s->a, sizeof(int64_t) * (size_t)s->cap); }
+    memmove(s->a + i + 1, s->a + i, sizeof(int64_t) * (size_t)(s->n - i));
+    s->a[i] = v;
+    s->n++;
+}
+static void iset_erase_at(iset *s, int64_t i) {
+    memmove(s->a + i, s->a + i + 1, sizeof(int64_t) * (size_t)(s->n - i - 1));
+    s->n--;
+}
+
+okg *oracle_universe(const okg *g, orand_t *rng, int64_t tc, float balance, int64_t *ent_remap, int64_t *rel_remap) {
+    int64_t ntu = tc;
+    otriple *U = calloc((size_t)(tc ? tc : 1), sizeof(otriple));
+    int64_t focus = orand_range(rng, 0, g->rel_total);                    /* :336-342 */
+    int64_t threshold = (int64_t)(balance * (float)tc);                   /* :343-344 */
+    iset S;
+    iset_init(&S);
+    for (int64_t k = g->lef_rel2[focus]; k < g->rig_rel2[focus] + 1; ++k) {   /* :69-80 */
+        iset_insert(&S, g->train_rel2[k].h);
+        iset_insert(&S, g->train_rel2[k].t);
+    }
+    if ((uint64_t)S.n > (uint64_t)threshold) {                            /* get_entity_subset :55-67 */
+        iset sub;
+        iset_init(&sub);
+        while (sub.n < threshold) {
+            int64_t idx = (int64_t)((uint64_t)(int64_t)orand_next(rng) % (uint64_t)S.n);
+            iset_insert(&sub, S.a[idx]);
+            iset_erase_at(&S, idx);
+        }
+        free(S.a);
+        S = sub;
+    }
+    /* BidirectionalRandomWalk (:92-191) */
+    int64_t ui = 0, last_dup = -1, tol = 5, not_inc = 20, last_size = 0;
+    iset nsp, uent, urel;
+    iset_init(&nsp); iset_init(&uent); iset_init(&urel);
+    while (ui < ntu) {
+        int64_t i = 0;
+        while (i < S.n && ui < ntu) {
+            int64_t cur = S.a[i];
+            int64_t nh = 0, nr = 0, nt = 0, start = -1;
+            int from_head;
+            if (orand_next(rng) % 1000 < 500)
+                from_head = g->rig_head[cur] != -1 ? 1 : (g->rig_tail[cur] != -1 ? 0 : -1);
+            else
+                from_head = g->rig_tail[cur] != -1 ? 0 : (g->rig_head[cur] != -1 ? 1 : -1);
+            if (from_head == 1) {
+                int64_t k = orand_range(rng, g->lef_head[cur], g->rig_head[cur] + 1);
+                nh = g->train_head[k].h; nr = g->train_head[k].r; nt = g->train_head[k].t; start = nt;
+            } else if (from_head == 0) {
+                int64_t k = orand_range(rng, g->lef_tail[cur], g->rig_tail[cur] + 1);
+                nh = g->train_tail[k].h; nr = g->train_tail[k].r; nt = g->train_tail[k].t; start = nh;
+            }
+            int dup = 0;
+            for (int64_t q = 0; q < ui; ++q)
+                if (U[q].h == nh && U[q].r == nr && U[q].t == nt) { dup = 1; break; }
+            if (dup) {
+                if (last_dup == cur) tol--; else last_dup = cur;
+                if (tol == 0) { tol = 5; i++; }
+                continue;
+            }
+            U[ui].h = nh; U[ui].r = nr; U[ui].t = nt;
+            iset_insert(&nsp, start);
+            iset_insert(&uent, nt);
+            iset_insert(&uent, nh);
+            iset_insert(&urel, nr);
+            iset_erase_at(&S, i);
+            ui++;
+        }
+        iset tmp = S; S = nsp; nsp = tmp;                                  /* swap, leftovers kept */
+        if (ui == last_size) not_inc--; else { last_size = ui; not_inc = 20; }
+        if (not_inc == 0) { ntu = ui; break; }
+    }
+    okg *u = calloc(1, sizeof(okg));
+    u->ent_total = uent.n;
+    u->rel_total = urel.n;
+    u->train_total = ntu;
+    free(S.a); free(nsp.a); free(uent.a); free(urel.a);
+    /* enumerateTrainUniverseTriples (:193-233): ids by first appearance h, t, r */
+    int64_t *emap = alloc_i64(g->ent_total, 1), *rmap = alloc_i64(g->rel_total, 1);
+    for (int64_t i = 0; i < g->ent_total; ++i) ent_remap[i] = -1;
+    for (int64_t i = 0; i < g->rel_total; ++i) rel_remap[i] = -1;
+    int64_t ne = 0, nr = 0;
+    u->train_list = calloc((size_t)(ntu ? ntu : 1), sizeof(otriple));
+    for (int64_t i = 0; i < ntu; ++i) {
+        if (emap[U[i].h] == -1) { emap[U[i].h] = ne; ent_remap[ne++] = U[i].h; }
+        u->train_list[i].h = emap[U[i].h];
+        if (emap[U[i].t] == -1) { emap[U[i].t] = ne; ent_remap[ne++] = U[i].t; }
+        u->train_list[i].t = emap[U[i].t];
+        if (rmap[U[i].r] == -1) { rmap[U[i].r] = nr; rel_remap[nr++] = U[i].r; }
+        u->train_list[i].r = rmap[U[i].r];
+    }
+    free(emap); free(rmap); free(U);
+    build_helpers(u);                                                      /* loadUniverseHelpers */
+    return u;
+}
+
+/* ---------------------------------------------------------------- model math ------------------ */
+static float vnorm2(const float *x, int64_t d) {
+    float s = 0;
+    for (int64_t i = 0; i < d; ++i) s += x[i] * x[i];
+    return sqrtf(s);
+}
+static float vdot(const float *a, const float *b, int64_t d) {
+    float s = 0;
+    for (int64_t i = 0; i < d; ++i) s += a[i] * b[i];
+    return s;
+}
+/* F.normalize(x, 2, -1) = x / max(||x||, 1e-12) */
+static float normalize_into(const float *x, float *out, int64_t d) {
+    float n = vnorm2(x, d);
+    float den = n > 1e-12f ? n : 1e-12f;
+    for (int64_t i = 0; i < d; ++i) out[i] = x[i] / den;
+    return n;
+}
+/* backward of F.normalize: (g - xhat (xhat . g)) / n  (zero extra term when n <= eps, clamp_min) */
+static void normalize_backward(const float *x, float n, const float *g, float *out, int64_t d) {
+    if (n > 1e-12f) {
+        float c = vdot(g, x, d) / (n * n);
+        for (int64_t i = 0; i < d; ++i) out[i] = (g[i] - x[i] * c) / n;
+    } else {
+        for (int64_t i = 0; i < d; ++i) out[i] = g[i] / 1e-12f;
+    }
+}
+
+typedef struct {
+    int64_t d;
+    float *h, *t, *r, *w;          /* raw rows */
+    float *hp, *tp;                /* TransH projected rows */
+    float *nh, *nt, *nr, *nw;      /* normalized rows */
+    float *v;
+    float hn, tn, rn, wn, hpn, tpn, hdot, tdot;
+} slot_ws;
+
+/* forward of one triple; returns the score, leaves intermediates in ws (TransE.py:46-60, TransH.py:68-93) */
+static float slot_forward(int model, int p, int norm_flag, int mode, slot_ws *ws, const float *he, const float *te,
+                          const float *re, const float *we) {
+    int64_t d = ws->d;
+    const float *h = he, *t = te;
+    if (model == 1) {
+        ws->wn = normalize_into(we, ws->nw, d);
+        ws->hdot = vdot(he, ws->nw, d);
+        ws->tdot = vdot(te, ws->nw, d);
+        for (int64_t i = 0; i < d; ++i) {
+            ws->hp[i] = he[i] - ws->hdot * ws->nw[i];
+            ws->tp[i] = te[i] - ws->tdot * ws->nw[i];
+        }
+        h = ws->hp;
+        t = ws->tp;
+    }
+    if (norm_flag) {
+        ws->hpn = normalize_into(h, ws->nh, d);
+        ws->rn = normalize_into(re, ws->nr, d);
+        ws->tpn = normalize_into(t, ws->nt, d);
+    } else {
+        memcpy(ws->nh, h, sizeof(float) * (size_t)d);
+        memcpy(ws->nr, re, sizeof(float) * (size_t)d);
+        memcpy(ws->nt, t, sizeof(float) * (size_t)d);
+    }
+    float s = 0;
+    for (int64_t i = 0; i < d; ++i) {
+        ws->v[i] = mode == 1 ? ws->nh[i] + (ws->nr[i] - ws->nt[i]) : (ws->nh[i] + ws->nr[i]) - ws->nt[i];
+        s += p == 1 ? fabsf(ws->v[i]) : ws->v[i] * ws->v[i];
+    }
+    return p == 1 ? s : sqrtf(s);
+}
+
+void oracle_score(int model, int p, int norm_flag, int mode, int64_t d, const float *ent, const float *rel,
+                  const float *normv, const int64_t *h, const int64_t *t, const int64_t *r, int64_t n, float *out) {
+    float *buf = calloc((size_t)(11 * d), sizeof(float));
+    slot_ws ws = {d, 0, 0, 0, 0, buf, buf + d, buf + 2 * d, buf + 3 * d, buf + 4 * d, buf + 5 * d, buf + 6 * d,
+                  0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = slot_forward(model, p, norm_flag, mode, &ws, ent + h[i] * d, ent + t[i] * d, rel + r[i] * d,
+                              model == 1 ? normv + r[i] * d : NULL);
+    free(buf);
+}
+
+static void apply_update(int opt, float lr, float *w, float *acc, const float *g, int64_t n) {
+    if (opt == 0) {
+        for (int64_t i = 0; i < n; ++i) w[i] = w[i] + (-lr) * g[i];
+    } else {
+        for (int64_t i = 0; i < n; ++i) {
+            acc[i] = acc[i] + g[i] * g[i];
+            w[i] = w[i] + (-lr) * g[i] / (sqrtf(acc[i]) + 1e-10f);
+        }
+    }
+}
+
+float oracle_train_step(int model, int p, int norm_flag, int opt, float lr, float margin, int64_t E, int64_t R,
+                        int64_t d, float *ent, float *rel, float *normv, float *ent_acc, float *rel_acc,
+                        float *norm_acc, const int64_t *h, const int64_t *t, const int64_t *r, int64_t bs,
+                        int64_t neg) {
+    int64_t seq = bs * (1 + neg);
+    float *score = malloc(sizeof(float) * (size_t)seq);
+    float *ds = calloc((size_t)seq, sizeof(float));
+    float *ge = calloc((size_t)(E * d), sizeof(float)), *gr = calloc((size_t)(R * d), sizeof(float));
+    float *gw = model == 1 ? calloc((size_t)(R * d), sizeof(float)) : NULL;
+    float *buf = calloc((size_t)(20 * d), sizeof(float));
+    slot_ws ws = {d, 0, 0, 0, 0, buf, buf + d, buf + 2 * d, buf + 3 * d, buf + 4 * d, buf + 5 * d, buf + 6 * d,
+                  0, 0, 0, 0, 0, 0, 0, 0};
+    float *gv = buf + 7 * d, *ga = buf + 8 * d, *gb = buf + 9 * d, *gc = buf + 10 * d, *gn = buf + 11 * d;
+    float *tmp = buf + 12 * d;
+    const float *W = normv;
+    /* forward, all slots with pre-step tables (Trainer.py:44-56 is minibatch-synchronous) */
+    for (int64_t s = 0; s < seq; ++s)
+        score[s] = slot_forward(model, p, norm_flag, 0, &ws, ent + h[s] * d, ent + t[s] * d, rel + r[s] * d,
+                                model == 1 ? W + r[s] * d : NULL);
+    /* MarginLoss: mean(max(p - n, -m)) + m; NegativeSampling reshape n[i][k] = score[bs + k*bs + i] */
+    double lsum = 0;
+    float inv = 1.0f / (float)(bs * neg);
+    for (int64_t i = 0; i < bs; ++i)
+        for (int64_t k = 0; k < neg; ++k) {
+            float a = score[i] - score[bs + k * bs + i];
+            float mx = a > -margin ? a : -margin;
+            lsum += mx;
+            float c = a > -margin ? inv : (a == -margin ? inv / 2 : 0.0f);
+            ds[i] += c;
+            ds[bs + k * bs + i] -= c;
+        }
+    float loss = (float)(lsum / (double)(bs * neg)) + margin;
+    /* backward per slot, scatter-sum into dense grads (embedding_dense_backward) */
+    for (int64_t s = 0; s < seq; ++s) {
+        if (ds[s] == 0.0f) continue;
+        const float *he = ent + h[s] * d, *te = ent + t[s] * d, *re = rel + r[s] * d;
+        float sc = slot_forward(model, p, norm_flag, 0, &ws, he, te, re, model == 1 ? W + r[s] * d : NULL);
+        for (int64_t i = 0; i < d; ++i) {
+            if (p == 1) gv[i] = ws.v[i] > 0 ? ds[s] : (ws.v[i] < 0 ? -ds[s] : 0.0f);
+            else gv[i] = sc == 0.0f ? 0.0f : ws.v[i] * (ds[s] / sc);
+        }
+        /* d/d(nh) = gv, d/d(nr) = gv, d/d(nt) = -gv */
+        for (int64_t i = 0; i < d; ++i) tmp[i] = -gv[i];
+        const float *hsrc = model == 1 ? ws.hp : he, *tsrc = model == 1 ? ws.tp : te;
+        if (norm_flag) {
+            normalize_backward(hsrc, ws.hpn, gv, ga, d);
+            normalize_backward(re, ws.rn, gv, gb, d);
+            normalize_backward(tsrc, ws.tpn, tmp, gc, d);
+        } else {
+            memcpy(ga, gv, sizeof(float) * (size_t)d);
+            memcpy(gb, gv, sizeof(float) * (size_t)d);
+            memcpy(gc, tmp, sizeof(float) * (size_t)d);
+        }
+        float *Ge_h = ge + h[s] * d, *Ge_t = ge + t[s] * d, *Gr = gr + r[s] * d;
+        for (int64_t i = 0; i < d; ++i) Gr[i] += gb[i];
+        if (model == 1) {
+            /* e_perp = e - (e.n) n:  g_e = g_p - n (n.g_p);  g_n = -((e.n) g_p + (n.g_p) e) */
+            float nga = vdot(ws.nw, ga, d), ngc = vdot(ws.nw, gc, d);
+            for (int64_t i = 0; i < d; ++i) {
+                Ge_h[i] += ga[i] - ws.nw[i] * nga;
+                Ge_t[i] += gc[i] - ws.nw[i] * ngc;
+                gn[i] = -(ws.hdot * ga[i] + nga * he[i]) - (ws.tdot * gc[i] + ngc * te[i]);
+            }
+            normalize_backward(W + r[s] * d, ws.wn, gn, tmp, d);
+            float *Gw = gw + r[s] * d;
+            for (int64_t i = 0; i < d; ++i) Gw[i] += tmp[i];
+        } else {
+            for (int64_t i = 0; i < d; ++i) {
+                Ge_h[i] += ga[i];
+                Ge_t[i] += gc[i];
+            }
+        }
+    }
+    apply_update(opt, lr, ent, ent_acc, ge, E * d);
+    apply_update(opt, lr, rel, rel_acc, gr, R * d);
+    if (model == 1) apply_update(opt, lr, normv, norm_acc, gw, R * d);
+    free(score); free(ds); free(ge); free(gr); free(gw); free(buf);
+    return loss;
+}
+
+int64_t oracle_train_loop(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
+                          int64_t filter, int model, int p, int norm_flag, int opt, float lr, float margin, int64_t d,
+                          float *ent, float *rel, float *normv, float *ent_acc, float *rel_acc, float *norm_acc,
+                          int64_t steps) {
+    int64_t seq = bs * (1 + neg);
+    int64_t *h = malloc(sizeof(int64_t) * (size_t)seq), *t = malloc(sizeof(int64_t) * (size_t)seq);
+    int64_t *r = malloc(sizeof(int64_t) * (size_t)seq);
+    float *y = malloc(sizeof(float) * (size_t)seq);
+    for (int64_t s = 0; s < steps; ++s) {
+        oracle_sampling(g, states, threads, bs, neg, bern, filter, h, t, r, y);
+        oracle_train_step(model, p, norm_flag, opt, lr, margin, g->ent_total, g->rel_total, d, ent, rel, normv,
+                          ent_acc, rel_acc, norm_acc, h, t, r, bs, neg);
+    }
+    free(h); free(t); free(r); free(y);
+    return steps * seq;
+}
+
+/* ---------------------------------------------------------------- link prediction ------------- */
+void oracle_sort_test(int64_t n, int64_t *h, int64_t *t, int64_t *r) {   /* importTestFiles :311 */
+    otriple *a = malloc(sizeof(otriple) * (size_t)(n ? n : 1));
+    for (int64_t i = 0; i < n; ++i) { a[i].h = h[i]; a[i].t = t[i]; a[i].r = r[i]; }
+    qsort(a, (size_t)n, sizeof(otriple), cmp_rel2);
+    for (int64_t i = 0; i < n; ++i) { h[i] = a[i].h; t[i] = a[i].t; r[i] = a[i].r; }
+    free(a);
+}
+
+static int find_triple(const otriple *all, int64_t n, int64_t h, int64_t t, int64_t r) {   /* _find */
+    otriple key = {h, r, t};
+    return bsearch(&key, all, (size_t)n, sizeof(otriple), cmp_head) != NULL;
+}
+
+void oracle_link_prediction(int64_t E, const int64_t *ah, const int64_t *at, const int64_t *ar, int64_t n_all,
+                            const int64_t *th, const int64_t *tt, const int64_t *tr, int64_t n_test,
+                            const float *con_head, const float *con_tail, int64_t *rank_head, int64_t *frank_head,
+                            int64_t *rank_tail, int64_t *frank_tail, float *metrics) {
+    otriple *all = malloc(sizeof(otriple) * (size_t)(n_all ? n_all : 1));
+    for (int64_t i = 0; i < n_all; ++i) { all[i].h = ah[i]; all[i].t = at[i]; all[i].r = ar[i]; }
+    qsort(all, (size_t)n_all, sizeof(otriple), cmp_head);
+    float l_filter_tot = 0, l3_filter_tot = 0, l1_filter_tot = 0, l_filter_rank = 0, l_filter_reci = 0;
+    float r_filter_tot = 0, r3_filter_tot = 0, r1_filter_tot = 0, r_filter_rank = 0, r_filter_reci = 0;
+    for (int64_t q = 0; q < n_test; ++q) {
+        int64_t h = th[q], t = tt[q], r = tr[q];
+        for (int side = 0; side < 2; ++side) {     /* 0: testHead (Test.h:118-238), 1: testTail (:240-359) */
+            const float *con = (side == 0 ? con_head : con_tail) + q * E;
+            int64_t truth = side == 0 ? h : t;
+            int64_t raw = 0, filt = 0;
+            float minimal = con[0];
+            if (minimal != INFINITY) {
+                for (int64_t j = 1; j < E; ++j) {
+                    int64_t cand = j - 1 < truth ? j - 1 : j;
+                    if (con[j] < minimal) {
+                        raw++;
+                        int known = side == 0 ? find_triple(all, n_all, cand, t, r) : find_triple(all, n_all, h, cand, r);
+                        if (!known) filt++;
+                    }
+                }
+            } else {
+                raw = E;
+                filt = E;
+                for (int64_t j = 1; j < E; ++j) {
+                    int64_t cand = j - 1 < truth ? j - 1 : j;
+                    int known = side == 0 ? find_triple(all, n_all, cand, t, r) : find_triple(all, n_all, h, cand, r);
+                    if (known) filt--;
+                }
+            }
+            if (side == 0) {
+                rank_head[q] = raw; frank_head[q] = filt;
+                if (filt < 10) l_filter_tot += 1;
+                if (filt < 3) l3_filter_tot += 1;
+                if (filt < 1) l1_filter_tot += 1;
+                l_filter_rank += (float)(filt + 1);
+                l_filter_reci = (float)((double)l_filter_reci + 1.0 / (double)(filt + 1));
+            } else {
+                rank_tail[q] = raw; frank_tail[q] = filt;
+                if (filt < 10) r_filter_tot += 1;
+                if (filt < 3) r3_filter_tot += 1;
+                if (filt < 1) r1_filter_tot += 1;
+                r_filter_rank += (float)(1 + filt);
+                r_filter_reci = (float)((double)r_filter_reci + 1.0 / (double)(1 + filt));
+            }
+        }
+    }
+    float nt = (float)n_test;
+    l_filter_rank /= nt; r_filter_rank /= nt; l_filter_reci /= nt; r_filter_reci /= nt;
+    l_filter_tot /= nt; l3_filter_tot /= nt; l1_filter_tot /= nt;
+    r_filter_tot /= nt; r3_filter_tot /= nt; r1_filter_tot /= nt;
+    metrics[0] = (l_filter_reci + r_filter_reci) / 2;       /* Test.h:450-454 */
+    metrics[1] = (l_filter_rank + r_filter_rank) / 2;
+    metrics[2] = (l_filter_tot + r_filter_tot) / 2;
+    metrics[3] = (l3_filter_tot + r3_filter_tot) / 2;
+    metrics[4] = (l1_filter_tot + r1_filter_tot) / 2;
+    free(all);
+}

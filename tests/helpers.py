@@ -1,0 +1,121 @@
+"""Shared test helpers (CPU-side; reference semantics restated for the checks)."""
+import glob
+import os
+
+import numpy as np
+import torch
+
+from conftest import GOLDEN, KG_SMALL, KG_TINY
+
+DATASETS = {"small": KG_SMALL, "tiny": KG_TINY}
+
+
+def golden(pattern):
+    return sorted(glob.glob(os.path.join(GOLDEN, pattern)))
+
+
+def load(path):
+    return np.load(path, allow_pickle=False)
+
+
+def torch_init_tables(model, ent_tot, rel_tot, dim, seed):
+    """The reference model constructors' RNG use: nn.Embedding normal_ draws for every table in
+    declaration order, then xavier_uniform_ in the same order (TransE.py:17-22, TransH.py:17-23),
+    all from the global torch CPU generator after torch.manual_seed(seed)."""
+    torch.manual_seed(seed)
+    embs = [torch.nn.Embedding(ent_tot, dim), torch.nn.Embedding(rel_tot, dim)]
+    if model == "TransH":
+        embs.append(torch.nn.Embedding(rel_tot, dim))
+    for e in embs:
+        torch.nn.init.xavier_uniform_(e.weight.data)
+    out = [e.weight.data.numpy().copy() for e in embs]
+    return out[0], out[1], (out[2] if model == "TransH" else None)
+
+
+def pu_energy(E, universes, test, model, p, dim):
+    """Global energy estimation of Parallel_Universe_Config (:446-465, :556-642) restated with numpy
+    over oracle scores: per (entity, rel) key the min over every universe holding both."""
+    import oracle
+    th, tt, tr = test
+    n = len(th)
+    con_h = np.full((n, E), np.inf, dtype=np.float32)
+    con_t = np.full((n, E), np.inf, dtype=np.float32)
+    for q in range(n):
+        h, t, r = int(th[q]), int(tt[q]), int(tr[q])
+        tail_vec = np.full(E, np.inf, dtype=np.float32)
+        head_vec = np.full(E, np.inf, dtype=np.float32)
+        for u in universes:
+            em, rm = u["ent_remap"], u["rel_remap"]
+            g2l_e = {int(g): l for l, g in enumerate(em)}
+            g2l_r = {int(g): l for l, g in enumerate(rm)}
+            if r not in g2l_r:
+                continue
+            El = len(em)
+            loc = np.arange(El, dtype=np.int64)
+            if h in g2l_e:
+                s = oracle.score(model, p, True, "tail_batch", u["ent"], u["rel"], u.get("norm"),
+                                 np.array([g2l_e[h]]), loc, np.array([g2l_r[r]]))
+                tail_vec[em] = np.minimum(tail_vec[em], s)
+            if t in g2l_e:
+                s = oracle.score(model, p, True, "head_batch", u["ent"], u["rel"], u.get("norm"),
+                                 loc, np.array([g2l_e[t]]), np.array([g2l_r[r]]))
+                head_vec[em] = np.minimum(head_vec[em], s)
+        con_h[q] = head_vec[oracle.candidates(E, h)]
+        con_t[q] = tail_vec[oracle.candidates(E, t)]
+    return con_h, con_t
+
+
+class IllConditioned:
+    """Tracks Adagrad components whose update was noise-dominated at some step (see assert_tables_close).
+
+    Call before(name, acc) / after(name, acc) around every step. A component counts as noise-updated
+    when its squared-gradient increment is positive but below noise2 (|g| < 1e-7, i.e. the sum of
+    contributions of size ~1e-2 cancelled to rounding level): its sign, and so the Adagrad step
+    +-lr*g/(|g|+1e-10), is then decided by summation order alone."""
+
+    def __init__(self, cond=1e-4, noise2=1e-14):
+        self.cond2 = cond * cond
+        self.noise2 = noise2
+        self.masks = {}
+        self.prev = {}
+        self.events = 0
+
+    def before(self, name, acc):
+        if acc is not None:
+            self.prev[name] = np.array(acc, copy=True)
+
+    def after(self, name, acc):
+        if acc is None:
+            return
+        acc = np.asarray(acc)
+        inc = acc - self.prev.get(name, np.zeros_like(acc))
+        noisy = (inc > 0) & (inc < self.noise2)
+        self.events += int(noisy.sum())
+        m = (acc < self.cond2) | noisy
+        self.masks[name] = m if name not in self.masks else (self.masks[name] | m)
+
+    def update(self, name, acc):
+        self.after(name, acc)
+
+    def get(self, name):
+        return self.masks.get(name)
+
+
+def assert_tables_close(ours, ref, atol, ill=None, lr=None, max_frac=1e-3):
+    """Elementwise |ours-ref| <= atol, except on Adagrad components that were ill-conditioned.
+
+    Adagrad's update is lr*g/(sqrt(A)+1e-10): for a component whose accumulated squared gradient A is
+    at the rounding level of its summands (sqrt(A) < 1e-4 at some step), that step's update is dominated
+    by summation-order noise in g (~1e-8 absolute), so two correct float32 implementations that sum the
+    same contributions in a different order legitimately differ there (by at most 2*lr per step, and the
+    difference then persists). Such components must be rare (<= max_frac of the table); every other
+    component meets atol. `ill` is the boolean mask an IllConditioned tracker accumulated."""
+    ours = np.asarray(ours, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    err = np.abs(ours - ref)
+    bad = err > atol
+    if ill is not None and bad.any():
+        assert not (bad & ~ill).any(), "max err on well-conditioned entries %g" % err[bad & ~ill].max()
+        assert bad.mean() <= max_frac, "too many ill-conditioned mismatches: %d" % bad.sum()
+        return
+    assert not bad.any(), "max abs err %g (atol %g) at %d entries" % (err.max(), atol, bad.sum())
