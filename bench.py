@@ -1,0 +1,217 @@
+"""Benchmark: training triples/s (positive + negative slots) of the fused TransE/TransH step on MI355X.
+
+Default workload = BASELINE.json configs[1] (C2): TransE on FB15K237-shaped synthetic data, dim 200,
+batch 2000, 25 negatives per positive, L2 norm, SGD (alpha 1.0, margin 5), bern + filter sampling,
+8 emulated sampler threads. One "step" = Trainer.train_one_step's work on one batch: in-kernel sampling
+of 2000 positives x (1 + 25) slots, NegativeSampling + MarginLoss forward, backward, SGD update of the
+touched rows. Inputs (graph, tables) are resident in HBM before timing starts.
+
+  python bench.py [--gpus N --steps K --warmup W]       (N > 1 under torch.distributed.run)
+
+C2 is a single model, so N > 1 runs N independent replicas (one per GPU, "replicas only", weak
+scaling, no collective in the data path); value = slots of all ranks / max-over-ranks time.
+Prints ONE JSON line on rank 0 with roofline (live HIP-event kernel timing) and cpu_baseline (the
+oracle's single-thread C restatement timed on a bounded sample of the same workload, rank 0, N = 1).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(HERE, "openke-putranse_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, os.path.join(PKG, "tools"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+WORKLOADS = {
+    # name: (shape, model, dim, p_norm, opt, lr, margin, batch_size, neg, bern, filter)
+    "c2": ("fb15k237", "TransE", 200, 2, "sgd", 1.0, 5.0, 2000, 25, 1, 1),
+    "c1": ("wn18", "TransE", 50, 1, "sgd", 1.0, 4.0, 100, 1, 0, 1),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
+
+
+def algorithmic_bytes_per_slot(model, opt, dim):
+    """index reads (3 x int64) + one read and one write of every row a slot touches."""
+    base = {("TransE", "sgd"): 24, ("TransE", "adagrad"): 48, ("TransH", "sgd"): 32, ("TransH", "adagrad"): 64}
+    return base[(model, opt)] * dim + 24
+
+
+def dist_setup():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def cpu_baseline(path, wl, seconds=15.0):
+    """Oracle (single-thread C restatement of the reference sampler + step) on a bounded sample."""
+    sys.path.insert(0, HERE)
+    import oracle
+    shape, model, dim, p, opt, lr, margin, bs, neg, bern, filt = wl
+    kg = oracle.KG.load(path)
+    st = oracle.GlibcRand(4).rand_reset(8)
+    rng = np.random.default_rng(0)
+    bound = np.sqrt(6.0 / (kg.ent_total + dim))
+    ent = rng.uniform(-bound, bound, (kg.ent_total, dim)).astype(np.float32)
+    rel = rng.uniform(-bound, bound, (kg.rel_total, dim)).astype(np.float32)
+    nv = rng.uniform(-bound, bound, (kg.rel_total, dim)).astype(np.float32) if model == "TransH" else None
+    accs = (np.zeros_like(ent), np.zeros_like(rel), None if nv is None else np.zeros_like(nv))
+    oracle.train_loop(kg, st, 8, bs, neg, bern, filt, model, p, True, opt, lr, margin, (ent, rel, nv), accs, 1)
+    steps, slots, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        slots += oracle.train_loop(kg, st, 8, bs, neg, bern, filt, model, p, True, opt, lr, margin,
+                                   (ent, rel, nv), accs, 1)
+        steps += 1
+    el = time.perf_counter() - t0
+    return {"value": slots / el, "unit": "triples/s", "cores": 1, "kind": "port",
+            "sample": "%d steps of the same workload (batch %d x (1+%d), dim %d) on the same synthetic graph, "
+                      "oracle/oracle.c single thread, %.1f s" % (steps, bs, neg, dim, el)}
+
+
+def load_traffic(tag):
+    """Per-launch HBM bytes of k_step + k_apply from a committed rocprofv3 --pmc summary, if present."""
+    f = os.path.join(HERE, "profiles", "pmc_%s.json" % tag)
+    if not os.path.exists(f):
+        return None
+    try:
+        return json.load(open(f)).get("bytes_per_step")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "putranse_bench"))
+    args = ap.parse_args()
+
+    ws, rank, local = dist_setup()
+    wl = WORKLOADS[args.workload]
+    shape, model, dim, p, opt, lr, margin, bs, neg, bern, filt = wl
+
+    import synth_kg
+    from openke import _native
+    from openke.config import Trainer
+    from openke.data import TrainDataLoader
+    from openke.module.loss import MarginLoss
+    from openke.module.model import TransE, TransH
+    from openke.module.strategy import NegativeSampling
+
+    data_dir = os.path.join(args.data_dir, "rank%d" % rank)
+    path = synth_kg.ensure_dataset(data_dir, shape)
+    dl = TrainDataLoader(in_path=path, batch_size=bs, threads=8, sampling_mode="normal", bern_flag=bern,
+                         filter_flag=filt, neg_ent=neg, neg_rel=0, random_seed=4)
+    torch.manual_seed(rank)
+    cls = TransE if model == "TransE" else TransH
+    kge = cls(ent_tot=dl.get_ent_tot(), rel_tot=dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=True)
+    ns = NegativeSampling(model=kge, loss=MarginLoss(margin=margin), batch_size=bs)
+    tr = Trainer(model=ns, data_loader=dl, train_times=0, alpha=lr, use_gpu=True, opt_method=opt)
+    tr.run()   # moves the tables to HBM and builds the native trainer; no steps
+    L = _native.lib()
+    sampler = dl.device_sampler()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    seq = bs * (1 + neg)
+
+    # warmup (also instantiates the hipGraph of `steps` replayed steps)
+    wl_losses = torch.zeros(max(args.warmup, 1), device=dev)
+    if args.warmup > 0:
+        _native.check(L.pt_trainer_run(tr._native, sampler, bs, neg, bern, filt, args.warmup,
+                                       _native.ptr(wl_losses), _native.stream()))
+    losses = torch.zeros(args.steps, device=dev)
+    # capture the timed graph outside the timed region: run it once untimed after warmup
+    _native.check(L.pt_trainer_run(tr._native, sampler, bs, neg, bern, filt, args.steps, _native.ptr(losses),
+                                   _native.stream()))
+    torch.cuda.synchronize()
+
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _native.check(L.pt_trainer_run(tr._native, sampler, bs, neg, bern, filt, args.steps, _native.ptr(losses),
+                                   _native.stream()))
+    torch.cuda.synchronize()
+    barrier(ws)
+    el = time.perf_counter() - t0
+    if ws > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    loss_last = float(losses[-1].item())
+    assert np.isfinite(loss_last), "non-finite loss"
+
+    # live kernel timing with HIP events on the launch stream (roofline of the fused step)
+    ms_s, ms_a = ctypes.c_float(), ctypes.c_float()
+    n_t = min(50, args.steps)
+    tot_s = tot_a = 0.0
+    one = torch.zeros(1, device=dev)
+    for _ in range(n_t):
+        _native.check(L.pt_trainer_step_timed(tr._native, sampler, bs, neg, bern, filt, _native.ptr(one),
+                                              ctypes.byref(ms_s), ctypes.byref(ms_a), _native.stream()))
+        tot_s += ms_s.value
+        tot_a += ms_a.value
+    avg_s, avg_a = tot_s / n_t, tot_a / n_t
+    bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
+    achieved = bytes_step / ((avg_s + avg_a) * 1e-3) / 1e9
+
+    if rank != 0:
+        if ws > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    value = args.steps * seq * ws / el
+    rec = {
+        "metric": "training triples/sec (pos+neg)",
+        "value": value,
+        "unit": "triples/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic %s-shaped graph (tools/synth_kg.py, seed 0), xavier-uniform tables" % shape,
+        "config": {"workload": "%s %s %s-shaped dim %d p%d %s lr %g margin %g batch %d neg %d bern %d filter %d "
+                               "threads 8" % (args.workload.upper(), model, shape, dim, p, opt, lr, margin, bs, neg,
+                                              bern, filt),
+                   "global_batch": seq * ws, "slots_per_step_per_gpu": seq,
+                   "parallelism": "replicas%d" % ws if ws > 1 else "single"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.workload),
+                     "kernel": "k_step + k_apply (one fused training step)",
+                     "ms_k_step": avg_s, "ms_k_apply": avg_a,
+                     "algorithmic_bytes_per_step": bytes_step},
+        "loss_last_step": loss_last,
+    }
+    if ws == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(path, wl, args.cpu_seconds)
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

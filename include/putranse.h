@@ -1,0 +1,239 @@
+/*
+ * putranse.h — C-ABI of libputranse_hip.so, the MI355X-native PuTransE / TransE / TransH hot path.
+ *
+ * Two surfaces, both plain C (pointers + sizes, no torch types):
+ *
+ *  A. Reentrant GPU entry points (pt_*): explicit handles, device pointers owned by the caller
+ *     (torch tensors), a hipStream_t passed as void*, int status returns (0 = ok, else a PT_E* code;
+ *     pt_last_error() gives the message). Nothing here calls exit().
+ *
+ *  B. The reference's Base.so symbols for this path (same names, argument meaning and global-state
+ *     semantics as openke/base/Base.cpp + headers), so a ctypes caller written against Base.so
+ *     (TrainDataLoader.py:30-101, TestDataLoader.py:220-266, Tester.py:20-36) binds unchanged.
+ *     They run on one process-global default context; batch construction, training and scoring
+ *     still execute on the GPU (host buffers are copied over PCIe).
+ *
+ * Integer ids are int64 (the reference's INT = long, Setting.h:3), reals float32 (REAL, Setting.h:4).
+ */
+#ifndef PUTRANSE_H
+#define PUTRANSE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ status ------------------ */
+enum {
+    PT_OK = 0,
+    PT_EINVAL = 1,   /* bad argument / shape */
+    PT_EIO = 2,      /* dataset file missing or malformed */
+    PT_ENOMEM = 3,   /* host or device allocation failed */
+    PT_EHIP = 4,     /* a HIP runtime call failed */
+    PT_ESTATE = 5,   /* call out of order (e.g. no dataset imported) */
+    PT_ENOTSUP = 6   /* configuration the kernels do not implement */
+};
+const char *pt_last_error(void);
+int pt_version(void);                /* ABI version, bumped on incompatible change */
+
+/* ------------------------------------------------------------------ graphs ------------------ */
+/* A training graph: deduplicated triples in cmp_head order plus the helper indices the sampler
+ * needs (replaces importTrainFiles + loadHelpers, Reader.h:58-234). */
+typedef struct pt_graph pt_graph;
+int pt_graph_load(const char *in_path, pt_graph **out);   /* headerless h t r files, line-counted */
+int pt_graph_free(pt_graph *g);
+int64_t pt_graph_ent_total(const pt_graph *g);
+int64_t pt_graph_rel_total(const pt_graph *g);
+int64_t pt_graph_train_total(const pt_graph *g);
+/* copies the cmp_head-ordered training triples to host arrays of length train_total */
+int pt_graph_triples(const pt_graph *g, int64_t *h, int64_t *t, int64_t *r);
+
+/* ------------------------------------------------------------------ sampler ----------------- */
+/* Device sampler bound to a graph: reproduces sampling()/getBatch() (Base.cpp:185-310) bit for bit
+ * for a given (seed states, threads) — `threads` only names the RNG-stream partition emulated. */
+typedef struct pt_sampler pt_sampler;
+int pt_sampler_create(pt_graph *g, int64_t threads, const uint64_t *seeds, pt_sampler **out);
+int pt_sampler_free(pt_sampler *s);
+/* re-seed the per-thread LCG streams (randReset, Random.h:10-15) */
+int pt_sampler_set_seeds(pt_sampler *s, const uint64_t *seeds);
+int pt_sampler_get_seeds(pt_sampler *s, uint64_t *seeds);       /* current states (host copy) */
+/* one sampling() call into DEVICE arrays of length bs*(1+neg); advances the streams */
+int pt_sampler_sample(pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter, int64_t *d_h,
+                      int64_t *d_t, int64_t *d_r, float *d_y, void *stream);
+
+/* ------------------------------------------------------------------ training ---------------- */
+enum { PT_TRANSE = 0, PT_TRANSH = 1 };
+enum { PT_SGD = 0, PT_ADAGRAD = 1 };
+
+typedef struct {
+    int32_t model;        /* PT_TRANSE | PT_TRANSH */
+    int32_t p_norm;       /* 1 or 2  (TransE.py:46-60) */
+    int32_t norm_flag;    /* F.normalize of h, r, t before scoring */
+    int32_t opt;          /* PT_SGD | PT_ADAGRAD (Trainer.py:62-88; eps 1e-10, lr_decay 0) */
+    float lr;
+    float margin;         /* MarginLoss margin (MarginLoss.py:24-28) */
+    int64_t ent_total, rel_total, dim;
+    float *ent, *rel, *normv;              /* device tables [rows][dim], row-major fp32 */
+    float *ent_acc, *rel_acc, *norm_acc;   /* Adagrad state_sum (NULL for SGD) */
+} pt_model_desc;
+
+/* Workspace for minibatch-synchronous steps on one model (gradient rows, touched-row flags). */
+typedef struct pt_trainer pt_trainer;
+int pt_trainer_create(const pt_model_desc *m, pt_trainer **out);
+int pt_trainer_free(pt_trainer *t);
+int pt_trainer_update_desc(pt_trainer *t, const pt_model_desc *m);   /* new lr/margin/pointers */
+/* One training step = Trainer.train_one_step (Trainer.py:44-56): NegativeSampling + MarginLoss
+ * forward, analytic backward, sparse optimizer update.  Batch either sampled in-kernel from
+ * `sampler` (batch_h == NULL) or read from device arrays of length bs*(1+neg) in the reference
+ * layout (negative k of positive i at (k+1)*bs+i).  Adds the step's loss to *d_loss (device). */
+int pt_trainer_step(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
+                    const int64_t *d_batch_h, const int64_t *d_batch_t, const int64_t *d_batch_r, float *d_loss,
+                    void *stream);
+/* `steps` consecutive in-kernel-sampled steps (one epoch = nbatches steps), launch-overhead-free
+ * (captured once into a hipGraph per shape and replayed). d_losses[s] receives step s's loss. */
+int pt_trainer_run(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
+                   int64_t steps, float *d_losses, void *stream);
+
+/* Measurement hook: one in-kernel-sampled step with HIP events around its two kernels (the fused
+ * forward/backward `k_step` and the sparse optimizer `k_apply`) on `stream`; synchronizes. */
+int pt_trainer_step_timed(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
+                          float *d_loss, float *ms_step, float *ms_apply, void *stream);
+
+/* ------------------------------------------------------------------ scoring ------------------ */
+/* scores = ||h + r - t||_p as model.predict computes them (TransE.py:46-74, TransH.py:52-93):
+ * mode 0 normal (all three arrays length n), 1 head_batch (d_h length n, t and r length 1),
+ * 2 tail_batch (d_t length n, h and r length 1). */
+int pt_score(const pt_model_desc *m, int32_t mode, const int64_t *d_h, const int64_t *d_t, const int64_t *d_r,
+             int64_t n, float *d_out, void *stream);
+
+/* Link-prediction candidate scores: row q = query q's candidates in getHeadBatch/getTailBatch order
+ * ([truth, 0..E-1 without truth], Test.h:37-107). side 0: head prediction (scores (e, r, t), association
+ * e + (r - t)); side 1: tail prediction ((h + r) - e). d_out is [nq][ent_total]; nq <= 65535. */
+int pt_score_queries(const pt_model_desc *m, int32_t side, const int64_t *d_qh, const int64_t *d_qt,
+                     const int64_t *d_qr, int64_t nq, float *d_out, void *stream);
+/* Metrics from per-query ranks with the reference's float accumulation (Test.h:213-223, :398-454):
+ * metrics[0..4] = filtered {MRR, MR, Hits@10, Hits@3, Hits@1}, metrics[5..9] = the raw ones. */
+int pt_lp_metrics(const int64_t *rank_head, const int64_t *frank_head, const int64_t *rank_tail,
+                  const int64_t *frank_tail, int64_t n, float *metrics);
+
+/* ------------------------------------------------------------------ universes --------------- */
+/* Universe construction (getParallelUniverse, UniverseConstructor.h:327-397) with private glibc-
+ * compatible RNG state seeded like setRandomSeed(seed)+randReset() (Random.h:10-15, :37-45), so
+ * universe k is a pure function of (graph, seed0+k, tc, balance) and many can be built in parallel. */
+typedef struct pt_universe pt_universe;
+int pt_universe_build(const pt_graph *g, int64_t seed, int64_t threads, int64_t triple_constraint,
+                      float balance, pt_universe **out);
+int pt_universe_free(pt_universe *u);
+/* build n universes on host threads: seeds[i], tcs[i], balances[i] -> out[i] */
+int pt_universe_build_many(const pt_graph *g, int64_t n, const int64_t *seeds, int64_t threads,
+                           const int64_t *tcs, const float *balances, int64_t n_workers, pt_universe **out);
+int64_t pt_universe_ent_total(const pt_universe *u);
+int64_t pt_universe_rel_total(const pt_universe *u);
+int64_t pt_universe_train_total(const pt_universe *u);
+int pt_universe_remaps(const pt_universe *u, int64_t *ent_remap, int64_t *rel_remap);   /* local -> global */
+pt_graph *pt_universe_graph(pt_universe *u);      /* the universe's local training graph */
+int pt_universe_seeds(const pt_universe *u, uint64_t *seeds);   /* LCG states after randReset */
+
+/* Train many universes concurrently in one persistent launch (one workgroup per universe). */
+typedef struct {
+    const pt_graph *graph;      /* universe-local training graph (from pt_universe_graph) */
+    const uint64_t *seeds;      /* `threads` LCG states */
+    int64_t threads, batch_size, epochs, nbatches;
+    float lr, margin;
+    float *ent, *rel, *normv;   /* device tables of this universe */
+    float *ent_acc, *rel_acc, *norm_acc;
+    int64_t dim;
+} pt_universe_job;
+int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm, int32_t norm_flag,
+                       int64_t bern, int64_t filter, float *d_losses, void *stream);
+
+/* ------------------------------------------------------------------ link prediction --------- */
+/* Per-universe all-entity scoring with a float MIN reduction into per-key rows
+ * (obtain_embedding_space_score + transmit_max_scores, Parallel_Universe_Config.py:446-465, :516-543).
+ * d_key_rows: [n_keys][global_ent_total] fp32 device buffer (init +inf). A pair names one universe
+ * holding both the key's anchor entity and relation: every local entity e of that universe is scored
+ * as the missing side (side 0: tail prediction, (anchor, r, e); side 1: head prediction, (e, r, anchor))
+ * and MIN-reduced into row `key` at column ent_remap[e]. Universes of different dims may be mixed. */
+typedef struct {
+    const float *ent, *rel, *normv;        /* device tables of the universe */
+    int64_t ent_total, rel_total, dim;
+    const int64_t *d_ent_remap;            /* device, length ent_total (local -> global) */
+} pt_lp_universe;
+typedef struct {
+    int32_t key, universe, anchor, rel, side;   /* anchor / rel are universe-LOCAL ids */
+} pt_lp_pair;
+int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, int32_t model, int32_t p_norm,
+                     int32_t norm_flag, const pt_lp_pair *pairs, int64_t n_pairs, int64_t global_ent_total,
+                     float *d_key_rows, void *stream);
+
+/* Filtered / raw ranks (testHead/testTail, Test.h:118-359) for many queries at once on host threads:
+ * con rows [n][ent_total] in candidate order, anchors per query. Known-triple set from
+ * pt_known_create (tripleList, Reader.h:246-342). */
+typedef struct pt_known pt_known;
+int pt_known_create(const int64_t *h, const int64_t *t, const int64_t *r, int64_t n, pt_known **out);
+int pt_known_free(pt_known *k);
+int pt_rank_queries(const pt_known *k, int64_t ent_total, const int64_t *h, const int64_t *t, const int64_t *r,
+                    int64_t n, int32_t side, const float *con, int64_t *raw, int64_t *filt, int64_t n_workers);
+
+/* The sampler of the Base.so-compatible global context below (its LCG states follow setRandomSeed /
+ * randReset and its graph follows importTrainFiles / swapHelpers), so pt_trainer_* can train on exactly
+ * the batch stream the reference's TrainDataLoader.sampling() would produce. */
+pt_sampler *pt_legacy_sampler(void);
+int64_t pt_legacy_bern(void);
+/* test (valid = 0) or valid (valid = 1) triples of the global context in ranking order; returns the
+ * count, fills the arrays when non-NULL. The known-triple set used by the filtered rank. */
+int64_t pt_legacy_eval_triples(int32_t valid, int64_t *h, int64_t *t, int64_t *r);
+const pt_known *pt_legacy_known(void);
+
+/* ------------------------------------------------------------------ B: Base.so-compatible ---- */
+/* Same names and semantics as the reference (see file:line per symbol in DESIGN.md §Boundary). */
+void setInPath(char *path);                          /* Setting.h:12-19 */
+void setOutPath(char *path);                         /* Setting.h:21-28 */
+void setWorkThreads(int64_t threads);                /* Setting.h:36-39 */
+int64_t getWorkThreads(void);                        /* Setting.h:41-44 */
+void setBern(int64_t con);                           /* Setting.h:92-95 */
+void setRandomSeed(int64_t seed);                    /* Random.h:37-42 */
+int64_t getRandomSeed(void);                         /* Random.h:44-47 */
+void randReset(void);                                /* Random.h:10-15 */
+void importTrainFiles(void);                         /* Reader.h:169-234 */
+int64_t getEntityTotal(void);                        /* Setting.h:57-60 */
+int64_t getRelationTotal(void);                      /* Setting.h:62-65 */
+int64_t getTrainTotal(void);                         /* Setting.h:72-75 */
+int64_t getTestTotal(void);                          /* Setting.h:77-80 */
+int64_t getValidTotal(void);                         /* Setting.h:82-85 */
+int64_t getTripleTotal(void);                        /* Setting.h:67-70 */
+/* Base.cpp:266-279 — host buffers; batch built on the GPU, copied back */
+void sampling(int64_t *batch_h, int64_t *batch_t, int64_t *batch_r, float *batch_y, int64_t batchSize,
+              int64_t negRate, int64_t negRelRate, int64_t mode, int64_t filter_flag, int64_t p, int64_t val_loss);
+void getParallelUniverse(int64_t triple_constraint, float balance_parameter);   /* UniverseConstructor.h:327 */
+int64_t getEntityTotalUniverse(void);                /* UniverseSetting.h:64-67 */
+int64_t getRelationTotalUniverse(void);              /* UniverseSetting.h:69-72 */
+int64_t getTrainTotalUniverse(void);                 /* UniverseSetting.h:74-77 */
+void getEntityRemapping(int64_t *ent_remapping);     /* UniverseSetting.h:79-84 */
+void getRelationRemapping(int64_t *rel_remapping);   /* UniverseSetting.h:86-91 */
+void swapHelpers(void);                              /* UniverseSetting.h:123-154 */
+void resetUniverse(void);                            /* UniverseSetting.h:160-190 */
+void activateLoadOfAllTriples(int64_t flag);         /* Reader.h:241-244 */
+void importTestFiles(void);                          /* Reader.h:246-342 */
+void initTest(void);                                 /* Test.h:23-35 */
+void getHeadBatch(int64_t *ph, int64_t *pt, int64_t *pr);    /* Test.h:37-71 */
+void getTailBatch(int64_t *ph, int64_t *pt, int64_t *pr);    /* Test.h:73-107 */
+void testHead(float *con, int64_t lastHead, int64_t type_constrain);   /* Test.h:118-238 */
+void testTail(float *con, int64_t lastTail, int64_t type_constrain);   /* Test.h:240-359 */
+void test_link_prediction(int64_t type_constrain);   /* Test.h:398-504 */
+float getTestLinkMRR(int64_t type_constrain);        /* Test.h:562-567 */
+float getTestLinkMR(int64_t type_constrain);         /* Test.h:555-560 */
+float getTestLinkHit10(int64_t type_constrain);      /* Test.h:533-539 */
+float getTestLinkHit3(int64_t type_constrain);       /* Test.h:541-546 */
+float getTestLinkHit1(int64_t type_constrain);       /* Test.h:548-553 */
+void validInit(void);                                /* Valid.h */
+void getValidHeadBatch(int64_t *ph, int64_t *pt, int64_t *pr);
+void getValidTailBatch(int64_t *ph, int64_t *pt, int64_t *pr);
+void validHead(float *con, int64_t lastHead);
+void validTail(float *con, int64_t lastTail);
+float getValidHit10(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

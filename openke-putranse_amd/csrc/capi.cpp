@@ -1,0 +1,953 @@
+// C-ABI of libputranse_hip.so (include/putranse.h): reentrant pt_* entry points and the reference's
+// Base.so symbols for the hot path, all executing batch construction / training / scoring on the GPU.
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <tuple>
+#include <vector>
+
+#include "common.h"
+#include "graph.h"
+#include "kernels.h"
+#include "rng.h"
+#include "universe.h"
+
+// ======================================================================== errors =================
+namespace pt {
+namespace {
+thread_local std::string g_err;
+}
+void set_error(int code, const std::string &msg) { g_err = "[putranse error " + std::to_string(code) + "] " + msg; }
+int fail(int code, const std::string &msg) {
+    set_error(code, msg);
+    return code;
+}
+}  // namespace pt
+
+extern "C" const char *pt_last_error(void) { return pt::g_err.c_str(); }
+extern "C" int pt_version(void) { return 1; }
+
+// ======================================================================== objects ================
+struct pt_sampler {
+    pt::Graph *g = nullptr;        // graph sampled from (follows swaps for the legacy context)
+    int64_t threads = 0;
+    uint64_t *d_states = nullptr;  // device LCG states, one per emulated sampler thread
+    int device = -1;
+    ~pt_sampler() {
+        if (d_states) (void)hipFree(d_states);
+    }
+};
+
+struct GraphKey {
+    const void *sampler, *graph, *losses, *states;
+    int64_t bs, neg, bern, filter, steps;
+    bool operator<(const GraphKey &o) const {
+        return std::tie(sampler, graph, losses, states, bs, neg, bern, filter, steps) <
+               std::tie(o.sampler, o.graph, o.losses, o.states, o.bs, o.neg, o.bern, o.filter, o.steps);
+    }
+};
+
+struct pt_trainer {
+    pt::StepParams P{};
+    pt::StepWorkspace W{};
+    void *ws_block = nullptr;
+    int device = -1;
+    hipStream_t cap = nullptr;
+    std::map<GraphKey, hipGraphExec_t> graphs;
+    void drop_graphs() {
+        for (auto &kv : graphs) (void)hipGraphExecDestroy(kv.second);
+        graphs.clear();
+    }
+    ~pt_trainer() {
+        drop_graphs();
+        if (cap) (void)hipStreamDestroy(cap);
+        if (ws_block) (void)hipFree(ws_block);
+    }
+};
+
+namespace {
+
+int desc_to_params(const pt_model_desc *m, pt::StepParams &P) {
+    PT_CHECK(m, PT_EINVAL, "null model descriptor");
+    PT_CHECK(m->model == PT_TRANSE || m->model == PT_TRANSH, PT_EINVAL, "model must be PT_TRANSE or PT_TRANSH");
+    PT_CHECK(m->p_norm == 1 || m->p_norm == 2, PT_ENOTSUP, "p_norm must be 1 or 2");
+    PT_CHECK(m->opt == PT_SGD || m->opt == PT_ADAGRAD, PT_EINVAL, "opt must be PT_SGD or PT_ADAGRAD");
+    PT_CHECK(pt::shape_supported(m->dim), PT_ENOTSUP, "embedding dim " + std::to_string(m->dim) + " not supported");
+    PT_CHECK(m->ent && m->rel && m->ent_total > 0 && m->rel_total > 0, PT_EINVAL, "missing tables");
+    PT_CHECK(m->model == PT_TRANSE || m->normv, PT_EINVAL, "TransH needs norm_vector");
+    PT_CHECK(m->opt == PT_SGD || (m->ent_acc && m->rel_acc && (m->model == PT_TRANSE || m->norm_acc)), PT_EINVAL,
+             "Adagrad needs state_sum buffers");
+    P.model = m->model;
+    P.p_norm = m->p_norm;
+    P.norm_flag = m->norm_flag ? 1 : 0;
+    P.opt = m->opt;
+    P.lr = m->lr;
+    P.margin = m->margin;
+    P.ent_total = m->ent_total;
+    P.rel_total = m->rel_total;
+    P.dim = m->dim;
+    P.ent = m->ent; P.rel = m->rel; P.normv = m->normv;
+    P.ent_acc = m->ent_acc; P.rel_acc = m->rel_acc; P.norm_acc = m->norm_acc;
+    return PT_OK;
+}
+
+int check_step_args(const pt::StepParams &P, pt_sampler *s, int64_t bs, int64_t neg, const int64_t *bh) {
+    PT_CHECK(bs > 0 && neg > 0, PT_EINVAL, "batch_size and neg_ent must be positive");
+    if (!bh) {
+        PT_CHECK(s && s->g && s->d_states, PT_ESTATE, "in-kernel sampling needs a sampler bound to a graph");
+        PT_CHECK(s->g->ent_total <= P.ent_total && s->g->rel_total <= P.rel_total, PT_EINVAL,
+                 "graph ids exceed the model tables");
+        PT_CHECK(s->g->ent_total > 1, PT_EINVAL, "graph needs at least two entities");
+        const int64_t gpb = 256;   // worst case groups per block (G = 2 -> 128) * 2 safety
+        PT_CHECK((size_t)gpb * (size_t)neg * 8 <= 64 * 1024, PT_ENOTSUP, "neg_ent too large for the LDS draw buffer");
+    }
+    return PT_OK;
+}
+
+}  // namespace
+
+// ======================================================================== graphs =================
+extern "C" int pt_graph_load(const char *in_path, pt_graph **out) {
+    PT_CHECK(in_path && out, PT_EINVAL, "pt_graph_load: null argument");
+    auto *g = new pt_graph();
+    int rc = pt::load_graph(in_path, g->g);
+    if (rc) {
+        delete g;
+        return rc;
+    }
+    *out = g;
+    return PT_OK;
+}
+extern "C" int pt_graph_free(pt_graph *g) {
+    delete g;
+    return PT_OK;
+}
+extern "C" int64_t pt_graph_ent_total(const pt_graph *g) { return g ? g->g.ent_total : -1; }
+extern "C" int64_t pt_graph_rel_total(const pt_graph *g) { return g ? g->g.rel_total : -1; }
+extern "C" int64_t pt_graph_train_total(const pt_graph *g) { return g ? g->g.train_total : -1; }
+extern "C" int pt_graph_triples(const pt_graph *g, int64_t *h, int64_t *t, int64_t *r) {
+    PT_CHECK(g && h && t && r, PT_EINVAL, "pt_graph_triples: null argument");
+    for (int64_t i = 0; i < g->g.train_total; ++i) {
+        h[i] = g->g.list[i].h;
+        t[i] = g->g.list[i].t;
+        r[i] = g->g.list[i].r;
+    }
+    return PT_OK;
+}
+
+// ======================================================================== sampler ================
+static int sampler_init(pt_sampler *s, pt::Graph *g, int64_t threads, const uint64_t *seeds) {
+    PT_CHECK(threads > 0 && threads <= 64, PT_ENOTSUP, "threads must be in [1, 64]");
+    PT_HIP(hipGetDevice(&s->device));
+    s->g = g;
+    s->threads = threads;
+    if (g) {
+        int rc = g->upload();
+        if (rc) return rc;
+    }
+    PT_HIP(hipMalloc(&s->d_states, sizeof(uint64_t) * 64));
+    PT_HIP(hipMemset(s->d_states, 0, sizeof(uint64_t) * 64));
+    if (seeds) PT_HIP(hipMemcpy(s->d_states, seeds, sizeof(uint64_t) * (size_t)threads, hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+extern "C" int pt_sampler_create(pt_graph *g, int64_t threads, const uint64_t *seeds, pt_sampler **out) {
+    PT_CHECK(g && out && seeds, PT_EINVAL, "pt_sampler_create: null argument");
+    auto *s = new pt_sampler();
+    int rc = sampler_init(s, &g->g, threads, seeds);
+    if (rc) {
+        delete s;
+        return rc;
+    }
+    *out = s;
+    return PT_OK;
+}
+extern "C" int pt_sampler_free(pt_sampler *s) {
+    delete s;
+    return PT_OK;
+}
+extern "C" int pt_sampler_set_seeds(pt_sampler *s, const uint64_t *seeds) {
+    PT_CHECK(s && seeds, PT_EINVAL, "pt_sampler_set_seeds: null argument");
+    PT_HIP(hipMemcpy(s->d_states, seeds, sizeof(uint64_t) * (size_t)s->threads, hipMemcpyHostToDevice));
+    return PT_OK;
+}
+extern "C" int pt_sampler_get_seeds(pt_sampler *s, uint64_t *seeds) {
+    PT_CHECK(s && seeds, PT_EINVAL, "pt_sampler_get_seeds: null argument");
+    PT_HIP(hipMemcpy(seeds, s->d_states, sizeof(uint64_t) * (size_t)s->threads, hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+extern "C" int pt_sampler_sample(pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter, int64_t *d_h,
+                                 int64_t *d_t, int64_t *d_r, float *d_y, void *stream) {
+    PT_CHECK(s && s->g && d_h && d_t && d_r, PT_EINVAL, "pt_sampler_sample: null argument");
+    PT_CHECK(bs >= 0 && neg >= 0, PT_EINVAL, "negative batch size");
+    PT_CHECK(s->g->ent_total > 1, PT_EINVAL, "graph needs at least two entities");
+    int rc = s->g->upload();
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    PT_HIP(pt::launch_sample(s->g->dev, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, d_h, d_t, d_r, d_y,
+                             st));
+    PT_HIP(pt::launch_advance(s->d_states, s->threads, bs, 1 + 2 * neg, st));
+    return PT_OK;
+}
+
+// ======================================================================== training ===============
+extern "C" int pt_trainer_create(const pt_model_desc *m, pt_trainer **out) {
+    PT_CHECK(out, PT_EINVAL, "pt_trainer_create: null argument");
+    auto t = std::make_unique<pt_trainer>();
+    int rc = desc_to_params(m, t->P);
+    if (rc) return rc;
+    PT_HIP(hipGetDevice(&t->device));
+    const int64_t E = t->P.ent_total, R = t->P.rel_total, D = t->P.dim;
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t ge = al(4 * E * D), gr = al(4 * R * D), gn = m->model == PT_TRANSH ? al(4 * R * D) : 0;
+    const size_t fe = al(4 * E), fr = al(4 * R), fn = m->model == PT_TRANSH ? al(4 * R) : 0;
+    const size_t total = ge + gr + gn + fe + fr + fn;
+    PT_HIP(hipMalloc(&t->ws_block, total));
+    PT_HIP(hipMemset(t->ws_block, 0, total));
+    char *b = (char *)t->ws_block;
+    t->W.gent = (float *)b; b += ge;
+    t->W.grel = (float *)b; b += gr;
+    t->W.gnorm = gn ? (float *)b : nullptr; b += gn;
+    t->W.fent = (int *)b; b += fe;
+    t->W.frel = (int *)b; b += fr;
+    t->W.fnorm = fn ? (int *)b : nullptr;
+    PT_HIP(hipStreamCreateWithFlags(&t->cap, hipStreamNonBlocking));
+    *out = t.release();
+    return PT_OK;
+}
+extern "C" int pt_trainer_free(pt_trainer *t) {
+    delete t;
+    return PT_OK;
+}
+extern "C" int pt_trainer_update_desc(pt_trainer *t, const pt_model_desc *m) {
+    PT_CHECK(t, PT_EINVAL, "null trainer");
+    pt::StepParams P{};
+    int rc = desc_to_params(m, P);
+    if (rc) return rc;
+    PT_CHECK(P.model == t->P.model && P.ent_total <= t->P.ent_total && P.rel_total <= t->P.rel_total &&
+                 P.dim == t->P.dim,
+             PT_EINVAL, "descriptor shape differs from the trainer's workspace");
+    t->P = P;
+    t->drop_graphs();
+    return PT_OK;
+}
+
+static int enqueue_step(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
+                        const int64_t *bh, const int64_t *bt, const int64_t *br, float *d_loss, hipStream_t st) {
+    pt::StepParams P = t->P;
+    P.batch_size = bs;
+    P.neg = neg;
+    P.inv_count = 1.0f / (float)(bs * neg);
+    const bool sampled = bh == nullptr;
+    pt::DeviceGraph dg{};
+    if (sampled) dg = s->g->dev;
+    PT_HIP(pt::launch_step(P, dg, sampled ? s->d_states : nullptr, sampled ? s->threads : 0, (int)bern, (int)filter,
+                           bh, bt, br, t->W, d_loss, st));
+    PT_HIP(pt::launch_apply(P, t->W, sampled ? s->d_states : nullptr, sampled ? s->threads : 0, bs, 1 + 2 * neg,
+                            d_loss, st));
+    return PT_OK;
+}
+
+extern "C" int pt_trainer_step(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
+                               const int64_t *d_bh, const int64_t *d_bt, const int64_t *d_br, float *d_loss,
+                               void *stream) {
+    PT_CHECK(t, PT_EINVAL, "null trainer");
+    int rc = check_step_args(t->P, s, bs, neg, d_bh);
+    if (rc) return rc;
+    if (!d_bh) {
+        rc = s->g->upload();
+        if (rc) return rc;
+    } else {
+        PT_CHECK(d_bt && d_br, PT_EINVAL, "external batch needs h, t and r arrays");
+    }
+    return enqueue_step(t, s, bs, neg, bern, filter, d_bh, d_bt, d_br, d_loss, (hipStream_t)stream);
+}
+
+// One in-kernel-sampled step with HIP events around each of its two kernels on `stream` (measurement
+// hook for bench.py's roofline: the average k_step / k_apply durations). Synchronizes the stream.
+extern "C" int pt_trainer_step_timed(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern,
+                                     int64_t filter, float *d_loss, float *ms_step, float *ms_apply, void *stream) {
+    PT_CHECK(t && ms_step && ms_apply, PT_EINVAL, "pt_trainer_step_timed: null argument");
+    int rc = check_step_args(t->P, s, bs, neg, nullptr);
+    if (rc) return rc;
+    rc = s->g->upload();
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t ev[3];
+    for (auto &e : ev) PT_HIP(hipEventCreate(&e));
+    pt::StepParams P = t->P;
+    P.batch_size = bs;
+    P.neg = neg;
+    P.inv_count = 1.0f / (float)(bs * neg);
+    PT_HIP(hipEventRecord(ev[0], st));
+    PT_HIP(pt::launch_step(P, s->g->dev, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr, nullptr,
+                           t->W, d_loss, st));
+    PT_HIP(hipEventRecord(ev[1], st));
+    PT_HIP(pt::launch_apply(P, t->W, s->d_states, s->threads, bs, 1 + 2 * neg, d_loss, st));
+    PT_HIP(hipEventRecord(ev[2], st));
+    PT_HIP(hipEventSynchronize(ev[2]));
+    PT_HIP(hipEventElapsedTime(ms_step, ev[0], ev[1]));
+    PT_HIP(hipEventElapsedTime(ms_apply, ev[1], ev[2]));
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    return PT_OK;
+}
+
+extern "C" int pt_trainer_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
+                              int64_t steps, float *d_losses, void *stream) {
+    PT_CHECK(t && d_losses, PT_EINVAL, "pt_trainer_run: null argument");
+    PT_CHECK(steps > 0, PT_EINVAL, "steps must be positive");
+    int rc = check_step_args(t->P, s, bs, neg, nullptr);
+    if (rc) return rc;
+    rc = s->g->upload();
+    if (rc) return rc;
+    GraphKey key{s, s->g->dev.list_h, d_losses, s->d_states, bs, neg, bern, filter, steps};
+    auto it = t->graphs.find(key);
+    if (it == t->graphs.end()) {
+        hipGraph_t graph;
+        PT_HIP(hipStreamBeginCapture(t->cap, hipStreamCaptureModeThreadLocal));
+        int erc = PT_OK;
+        if (hipMemsetAsync(d_losses, 0, sizeof(float) * (size_t)steps, t->cap) != hipSuccess) erc = PT_EHIP;
+        for (int64_t i = 0; i < steps && !erc; ++i)
+            erc = enqueue_step(t, s, bs, neg, bern, filter, nullptr, nullptr, nullptr, d_losses + i, t->cap);
+        hipError_t ce = hipStreamEndCapture(t->cap, &graph);
+        if (erc) return erc;
+        PT_HIP(ce);
+        hipGraphExec_t exec;
+        hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        PT_HIP(ie);
+        it = t->graphs.emplace(key, exec).first;
+    }
+    PT_HIP(hipGraphLaunch(it->second, (hipStream_t)stream));
+    return PT_OK;
+}
+
+extern "C" int pt_score(const pt_model_desc *m, int32_t mode, const int64_t *d_h, const int64_t *d_t,
+                        const int64_t *d_r, int64_t n, float *d_out, void *stream) {
+    pt::StepParams P{};
+    pt_model_desc mm = *m;
+    if (!mm.ent_acc) { mm.opt = PT_SGD; }
+    int rc = desc_to_params(&mm, P);
+    if (rc) return rc;
+    PT_CHECK(mode >= 0 && mode <= 2, PT_EINVAL, "mode must be 0 (normal), 1 (head_batch) or 2 (tail_batch)");
+    PT_CHECK(d_h && d_t && d_r && d_out, PT_EINVAL, "pt_score: null argument");
+    PT_HIP(pt::launch_score(P, mode, d_h, d_t, d_r, n, d_out, (hipStream_t)stream));
+    return PT_OK;
+}
+
+extern "C" int pt_score_queries(const pt_model_desc *m, int32_t side, const int64_t *d_qh, const int64_t *d_qt,
+                                const int64_t *d_qr, int64_t nq, float *d_out, void *stream) {
+    pt::StepParams P{};
+    pt_model_desc mm = *m;
+    if (!mm.ent_acc) mm.opt = PT_SGD;
+    int rc = desc_to_params(&mm, P);
+    if (rc) return rc;
+    PT_CHECK(side == 0 || side == 1, PT_EINVAL, "side must be 0 (head prediction) or 1 (tail prediction)");
+    PT_CHECK(nq <= 65535, PT_EINVAL, "at most 65535 queries per call");
+    PT_CHECK((d_qh && d_qt && d_qr && d_out) || nq == 0, PT_EINVAL, "pt_score_queries: null argument");
+    PT_HIP(pt::launch_score_queries(P, side, d_qh, d_qt, d_qr, nq, P.ent_total, d_out, (hipStream_t)stream));
+    return PT_OK;
+}
+
+// Test.h:213-223 + :398-454 accumulation for n ranked queries (float accumulators, same order)
+extern "C" int pt_lp_metrics(const int64_t *rank_head, const int64_t *frank_head, const int64_t *rank_tail,
+                             const int64_t *frank_tail, int64_t n, float *metrics) {
+    PT_CHECK(metrics && (n == 0 || (rank_head && frank_head && rank_tail && frank_tail)), PT_EINVAL,
+             "pt_lp_metrics: null argument");
+    float lf10 = 0, lf3 = 0, lf1 = 0, lfr = 0, lfi = 0, rf10 = 0, rf3 = 0, rf1 = 0, rfr = 0, rfi = 0;
+    float l10 = 0, l3 = 0, l1 = 0, lr = 0, li = 0, r10 = 0, r3 = 0, r1 = 0, rr = 0, ri = 0;
+    for (int64_t q = 0; q < n; ++q) {
+        const int64_t a = rank_head[q], fa = frank_head[q], b = rank_tail[q], fb = frank_tail[q];
+        if (fa < 10) lf10 += 1; if (a < 10) l10 += 1; if (fa < 3) lf3 += 1; if (a < 3) l3 += 1;
+        if (fa < 1) lf1 += 1; if (a < 1) l1 += 1;
+        lfr += (float)(fa + 1); lr += (float)(1 + a);
+        lfi = (float)((double)lfi + 1.0 / (double)(fa + 1)); li = (float)((double)li + 1.0 / (double)(a + 1));
+        if (fb < 10) rf10 += 1; if (b < 10) r10 += 1; if (fb < 3) rf3 += 1; if (b < 3) r3 += 1;
+        if (fb < 1) rf1 += 1; if (b < 1) r1 += 1;
+        rfr += (float)(1 + fb); rr += (float)(1 + b);
+        rfi = (float)((double)rfi + 1.0 / (double)(1 + fb)); ri = (float)((double)ri + 1.0 / (double)(1 + b));
+    }
+    const float N = (float)n;
+    lfr /= N; rfr /= N; lfi /= N; rfi /= N; lf10 /= N; lf3 /= N; lf1 /= N; rf10 /= N; rf3 /= N; rf1 /= N;
+    lr /= N; rr /= N; li /= N; ri /= N; l10 /= N; l3 /= N; l1 /= N; r10 /= N; r3 /= N; r1 /= N;
+    metrics[0] = (lfi + rfi) / 2; metrics[1] = (lfr + rfr) / 2; metrics[2] = (lf10 + rf10) / 2;
+    metrics[3] = (lf3 + rf3) / 2; metrics[4] = (lf1 + rf1) / 2;
+    metrics[5] = (li + ri) / 2; metrics[6] = (lr + rr) / 2; metrics[7] = (l10 + r10) / 2;
+    metrics[8] = (l3 + r3) / 2; metrics[9] = (l1 + r1) / 2;
+    return PT_OK;
+}
+
+// ======================================================================== universes ==============
+extern "C" int pt_universe_build(const pt_graph *g, int64_t seed, int64_t threads, int64_t tc, float balance,
+                                 pt_universe **out) {
+    PT_CHECK(g && out, PT_EINVAL, "pt_universe_build: null argument");
+    PT_CHECK(threads > 0 && threads <= 64 && tc > 0, PT_EINVAL, "bad threads / triple constraint");
+    auto *u = new pt_universe();
+    pt::GlibcRand rng((uint32_t)seed);   // srand(seed) (Random.h:37-42)
+    u->u.seeds.resize((size_t)threads);
+    for (auto &x : u->u.seeds) x = (uint64_t)(int64_t)rng.next();   // randReset (Random.h:10-15)
+    pt::build_universe(g->g, rng, tc, balance, u->u);
+    *out = u;
+    return PT_OK;
+}
+
+extern "C" int pt_universe_build_many(const pt_graph *g, int64_t n, const int64_t *seeds, int64_t threads,
+                                      const int64_t *tcs, const float *balances, int64_t n_workers, pt_universe **out) {
+    PT_CHECK(g && seeds && tcs && balances && out, PT_EINVAL, "pt_universe_build_many: null argument");
+    if (n_workers <= 0) n_workers = std::max(1u, std::thread::hardware_concurrency());
+    n_workers = std::min<int64_t>(n_workers, std::max<int64_t>(n, 1));
+    std::atomic<int64_t> next{0};
+    std::atomic<int> err{0};
+    auto work = [&]() {
+        for (int64_t i; (i = next.fetch_add(1)) < n;) {
+            pt_universe *u = nullptr;
+            int rc = pt_universe_build(g, seeds[i], threads, tcs[i], balances[i], &u);
+            if (rc) err = rc;
+            out[i] = u;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int64_t w = 1; w < n_workers; ++w) pool.emplace_back(work);
+    work();
+    for (auto &th : pool) th.join();
+    return err.load();
+}
+extern "C" int pt_universe_free(pt_universe *u) {
+    delete u;
+    return PT_OK;
+}
+extern "C" int64_t pt_universe_ent_total(const pt_universe *u) { return u ? u->u.g.ent_total : -1; }
+extern "C" int64_t pt_universe_rel_total(const pt_universe *u) { return u ? u->u.g.rel_total : -1; }
+extern "C" int64_t pt_universe_train_total(const pt_universe *u) { return u ? u->u.g.train_total : -1; }
+extern "C" int pt_universe_remaps(const pt_universe *u, int64_t *ent_remap, int64_t *rel_remap) {
+    PT_CHECK(u, PT_EINVAL, "null universe");
+    if (ent_remap) std::copy(u->u.ent_remap.begin(), u->u.ent_remap.end(), ent_remap);
+    if (rel_remap) std::copy(u->u.rel_remap.begin(), u->u.rel_remap.end(), rel_remap);
+    return PT_OK;
+}
+extern "C" pt_graph *pt_universe_graph(pt_universe *u) {
+    // pt_graph is a thin wrapper over pt::Graph; the universe owns it
+    return u ? reinterpret_cast<pt_graph *>(&u->u.g) : nullptr;
+}
+extern "C" int pt_universe_seeds(const pt_universe *u, uint64_t *seeds) {
+    PT_CHECK(u && seeds, PT_EINVAL, "null argument");
+    std::copy(u->u.seeds.begin(), u->u.seeds.end(), seeds);
+    return PT_OK;
+}
+
+// Train many universes: each universe is an independent chain of epochs*nbatches minibatch-
+// synchronous steps. Chains are issued round-robin on a pool of streams so they run concurrently;
+// each chain's epoch is one replayed hipGraph.
+extern "C" int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm,
+                                  int32_t norm_flag, int64_t bern, int64_t filter, float *d_losses, void *stream) {
+    PT_CHECK(jobs || n == 0, PT_EINVAL, "null jobs");
+    hipStream_t user = (hipStream_t)stream;
+    const int NS = 16;
+    hipStream_t ss[NS];
+    for (int i = 0; i < NS; ++i) PT_HIP(hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking));
+    hipEvent_t start;
+    PT_HIP(hipEventCreateWithFlags(&start, hipEventDisableTiming));
+    PT_HIP(hipEventRecord(start, user));
+    for (int i = 0; i < NS; ++i) PT_HIP(hipStreamWaitEvent(ss[i], start, 0));
+    std::vector<std::unique_ptr<pt_trainer>> trainers;
+    std::vector<std::unique_ptr<pt_sampler>> samplers;
+    int rc = PT_OK;
+    int64_t loss_off = 0;
+    for (int64_t i = 0; i < n && !rc; ++i) {
+        const pt_universe_job &J = jobs[i];
+        pt::Graph *g = const_cast<pt::Graph *>(reinterpret_cast<const pt::Graph *>(J.graph));
+        pt_model_desc m{};
+        m.model = model; m.p_norm = p_norm; m.norm_flag = norm_flag; m.opt = PT_ADAGRAD;
+        m.lr = J.lr; m.margin = J.margin;
+        m.ent_total = g->ent_total; m.rel_total = g->rel_total; m.dim = J.dim;
+        m.ent = J.ent; m.rel = J.rel; m.normv = J.normv;
+        m.ent_acc = J.ent_acc; m.rel_acc = J.rel_acc; m.norm_acc = J.norm_acc;
+        pt_trainer *t = nullptr;
+        rc = pt_trainer_create(&m, &t);
+        if (rc) break;
+        trainers.emplace_back(t);
+        auto s = std::make_unique<pt_sampler>();
+        rc = sampler_init(s.get(), g, J.threads, J.seeds);
+        if (rc) break;
+        const int64_t bs = J.batch_size;
+        if (bs <= 0 || J.epochs <= 0) {
+            samplers.push_back(std::move(s));
+            continue;
+        }
+        for (int64_t e = 0; e < J.epochs && !rc; ++e)
+            rc = pt_trainer_run(t, s.get(), bs, 1, bern, filter, J.nbatches, d_losses + loss_off, ss[i % NS]);
+        loss_off += J.nbatches;
+        samplers.push_back(std::move(s));
+    }
+    for (int i = 0; i < NS; ++i) {
+        hipEvent_t done;
+        (void)hipEventCreateWithFlags(&done, hipEventDisableTiming);
+        (void)hipEventRecord(done, ss[i]);
+        (void)hipStreamWaitEvent(user, done, 0);
+        (void)hipEventDestroy(done);
+    }
+    // trainers/samplers own device workspace used by the queued work: wait before freeing
+    (void)hipStreamSynchronize(user);
+    trainers.clear();
+    samplers.clear();
+    for (int i = 0; i < NS; ++i) (void)hipStreamDestroy(ss[i]);
+    (void)hipEventDestroy(start);
+    return rc;
+}
+
+// ======================================================================== link prediction =======
+extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, int32_t model, int32_t p_norm,
+                                int32_t norm_flag, const pt_lp_pair *pairs, int64_t n_pairs,
+                                int64_t global_ent_total, float *d_key_rows, void *stream) {
+    PT_CHECK((us && pairs && d_key_rows) || n_pairs == 0, PT_EINVAL, "pt_lp_min_scores: null argument");
+    if (n_pairs == 0) return PT_OK;
+    hipStream_t st = (hipStream_t)stream;
+    // group pairs by universe dim (one kernel shape per dim)
+    std::map<int64_t, std::vector<pt::LpPair>> by_dim;
+    std::map<int64_t, int64_t> max_ent;
+    for (int64_t i = 0; i < n_pairs; ++i) {
+        const pt_lp_pair &p = pairs[i];
+        PT_CHECK(p.universe >= 0 && p.universe < n_universes, PT_EINVAL, "pair universe out of range");
+        const pt_lp_universe &U = us[p.universe];
+        PT_CHECK(p.anchor >= 0 && p.anchor < U.ent_total && p.rel >= 0 && p.rel < U.rel_total, PT_EINVAL,
+                 "pair local ids out of range");
+        by_dim[U.dim].push_back(pt::LpPair{p.key, p.universe, p.anchor, p.rel, p.side});
+        max_ent[U.dim] = std::max(max_ent[U.dim], U.ent_total);
+    }
+    std::vector<pt::LpUniverseDev> hu((size_t)n_universes);
+    for (int64_t i = 0; i < n_universes; ++i)
+        hu[i] = pt::LpUniverseDev{us[i].ent, us[i].rel, us[i].normv, us[i].d_ent_remap, us[i].ent_total, us[i].dim};
+    pt::LpUniverseDev *du = nullptr;
+    PT_HIP(hipMallocAsync((void **)&du, sizeof(pt::LpUniverseDev) * hu.size(), st));
+    PT_HIP(hipMemcpyAsync(du, hu.data(), sizeof(pt::LpUniverseDev) * hu.size(), hipMemcpyHostToDevice, st));
+    for (auto &kv : by_dim) {
+        PT_CHECK(pt::shape_supported(kv.first), PT_ENOTSUP, "dim not supported");
+        auto &v = kv.second;
+        // y-grid limit 65535 per launch
+        for (size_t off = 0; off < v.size(); off += 65535) {
+            const size_t cnt = std::min<size_t>(65535, v.size() - off);
+            pt::LpPair *dp = nullptr;
+            PT_HIP(hipMallocAsync((void **)&dp, sizeof(pt::LpPair) * cnt, st));
+            PT_HIP(hipMemcpyAsync(dp, v.data() + off, sizeof(pt::LpPair) * cnt, hipMemcpyHostToDevice, st));
+            PT_HIP(pt::launch_lp_min(du, dp, (int64_t)cnt, kv.first, max_ent[kv.first], model, p_norm, norm_flag,
+                                     global_ent_total, d_key_rows, st));
+            PT_HIP(hipFreeAsync(dp, st));
+        }
+    }
+    PT_HIP(hipFreeAsync(du, st));
+    PT_HIP(hipStreamSynchronize(st));   // host vectors above must outlive the async copies
+    return PT_OK;
+}
+
+// ======================================================================== Base.so surface ========
+// One process-global context with the reference's semantics (Setting.h / Random.h / Reader.h /
+// UniverseSetting.h / Test.h / Valid.h globals). Sampling, training and scoring run on the GPU.
+namespace {
+
+struct TestAcc {   // the reference's float accumulators (Test.h:14-21)
+    float l_filter_tot = 0, l3_filter_tot = 0, l1_filter_tot = 0, l_filter_rank = 0, l_filter_reci = 0;
+    float r_filter_tot = 0, r3_filter_tot = 0, r1_filter_tot = 0, r_filter_rank = 0, r_filter_reci = 0;
+    float l_tot = 0, l3_tot = 0, l1_tot = 0, l_rank = 0, l_reci = 0;
+    float r_tot = 0, r3_tot = 0, r1_tot = 0, r_rank = 0, r_reci = 0;
+};
+
+struct Legacy {
+    std::mutex mu;
+    std::string in_path = "../data/FB15K/";
+    int64_t threads = 1, bern = 0, seed = 0;
+    pt::GlibcRand rng{1};
+    std::vector<uint64_t> states;
+    std::unique_ptr<pt::Graph> train;        // importTrainFiles
+    std::string train_path;
+    std::unique_ptr<pt::Universe> uni;       // getParallelUniverse
+    bool swapped = false;
+    pt_sampler sampler;                      // device states; g follows the active graph
+    bool sampler_ready = false;
+    // device batch buffers for the host-pointer sampling()
+    int64_t *dbuf = nullptr;
+    size_t dbuf_cap = 0;
+    // test / valid data
+    bool load_all = false;
+    int64_t ent_total = 0, rel_total = 0, test_total = 0, valid_total = 0, triple_total = 0, train_lines = 0;
+    std::vector<pt::Triple> test, valid;
+    pt_known *known = nullptr;
+    int64_t last_head = 0, last_tail = 0, last_vhead = 0, last_vtail = 0;
+    TestAcc acc;
+    float mrr = 0, mr = 0, hit10 = 0, hit3 = 0, hit1 = 0;
+    float l_valid = 0, r_valid = 0, valid_hit10 = 0;
+
+    pt::Graph *active() { return swapped && uni ? &uni->g : train.get(); }
+    int64_t E() { pt::Graph *g = active(); return g ? g->ent_total : ent_total; }
+};
+
+Legacy &L() {
+    static Legacy *l = new Legacy();   // never destroyed: device frees at exit are unsafe
+    return *l;
+}
+
+void legacy_err(int rc) {
+    if (rc) fprintf(stderr, "%s\n", pt_last_error());
+}
+
+int legacy_sync_sampler(Legacy &l) {
+    if (!l.sampler_ready) {
+        int rc = sampler_init(&l.sampler, nullptr, 64, nullptr);
+        if (rc) return rc;
+        l.sampler.threads = std::max<int64_t>(1, l.threads);
+        l.sampler_ready = true;
+    }
+    l.sampler.g = l.active();
+    return PT_OK;
+}
+
+int legacy_push_states(Legacy &l) {
+    int rc = legacy_sync_sampler(l);
+    if (rc) return rc;
+    std::vector<uint64_t> s(64, 0);
+    std::copy(l.states.begin(), l.states.end(), s.begin());
+    PT_HIP(hipMemcpy(l.sampler.d_states, s.data(), sizeof(uint64_t) * 64, hipMemcpyHostToDevice));
+    l.sampler.threads = std::max<int64_t>(1, (int64_t)l.states.size());
+    return PT_OK;
+}
+
+}  // namespace
+
+extern "C" pt_sampler *pt_legacy_sampler(void) {
+    Legacy &l = L();
+    std::lock_guard<std::mutex> lk(l.mu);
+    if (legacy_sync_sampler(l)) return nullptr;
+    return &l.sampler;
+}
+
+extern "C" void setInPath(char *path) {
+    Legacy &l = L();
+    std::lock_guard<std::mutex> lk(l.mu);
+    l.in_path = path ? path : "";
+    printf("Input Files Path : %s\n", l.in_path.c_str());
+}
+extern "C" void setOutPath(char *path) { (void)path; }
+extern "C" void setWorkThreads(int64_t threads) { L().threads = threads; }
+extern "C" int64_t getWorkThreads(void) { return L().threads; }
+extern "C" void setBern(int64_t con) { L().bern = con; }
+extern "C" void setRandomSeed(int64_t seed) {
+    Legacy &l = L();
+    l.seed = seed == -1 ? (int64_t)time(nullptr) : seed;
+    l.rng.seed_with((uint32_t)l.seed);
+}
+extern "C" int64_t getRandomSeed(void) { return L().seed; }
+extern "C" void randReset(void) {
+    Legacy &l = L();
+    std::lock_guard<std::mutex> lk(l.mu);
+    l.states.assign((size_t)std::max<int64_t>(1, l.threads), 0);
+    for (auto &s : l.states) s = (uint64_t)(int64_t)l.rng.next();
+    legacy_err(legacy_push_states(l));
+}
+extern "C" void importTrainFiles(void) {
+    Legacy &l = L();
+    std::lock_guard<std::mutex> lk(l.mu);
+    printf("The toolkit is importing datasets.\n");
+    if (l.train && l.train_path == l.in_path && !l.swapped) return;   // identical re-import
+    auto g = std::make_unique<pt::Graph>();
+    int rc = pt::load_graph(l.in_path, *g);
+    if (rc) {
+        legacy_err(rc);
+        return;
+    }
+    (void)hipDeviceSynchronize();   // an older graph may still be read by queued kernels
+    l.train = std::move(g);
+    l.train_path = l.in_path;
+    l.ent_total = l.train->ent_total;
+    l.rel_total = l.train->rel_total;
+    legacy_err(l.train->upload());
+    legacy_err(legacy_sync_sampler(l));
+    printf("The total of train triples is %ld.\n", (long)l.train->train_total);
+}
+extern "C" int64_t getEntityTotal(void) { Legacy &l = L(); return l.active() ? l.active()->ent_total : l.ent_total; }
+extern "C" int64_t getRelationTotal(void) { Legacy &l = L(); return l.active() ? l.active()->rel_total : l.rel_total; }
+extern "C" int64_t getTrainTotal(void) { Legacy &l = L(); return l.active() ? l.active()->train_total : l.train_lines; }
+extern "C" int64_t getTestTotal(void) { return L().test_total; }
+extern "C" int64_t getValidTotal(void) { return L().valid_total; }
+extern "C" int64_t getTripleTotal(void) { return L().triple_total; }
+
+extern "C" void sampling(int64_t *bh, int64_t *bt, int64_t *br, float *by, int64_t bs, int64_t neg, int64_t neg_rel,
+                         int64_t mode, int64_t filter, int64_t p, int64_t val_loss) {
+    (void)p;
+    Legacy &l = L();
+    std::lock_guard<std::mutex> lk(l.mu);
+    if (val_loss) {   // positives of the validation list (Base.cpp:255-262)
+        for (int64_t b = 0; b < bs && b < (int64_t)l.valid.size(); ++b) {
+            bh[b] = l.valid[b].h; bt[b] = l.valid[b].t; br[b] = l.valid[b].r; by[b] = 1;
+        }
+        return;
+    }
+    if (neg_rel != 0 || mode != 0) {
+        legacy_err(pt::fail(PT_ENOTSUP, "sampling: only mode 0 with neg_rel 0 runs on the GPU path"));
+        return;
+    }
+    if (!l.active()) {
+        legacy_err(pt::fail(PT_ESTATE, "sampling before importTrainFiles"));
+        return;
+    }
+    int rc = legacy_sync_sampler(l);
+    if (rc) return legacy_err(rc);
+    const int64_t seq = bs * (1 + neg);
+    const size_t need = (size_t)seq * 3 * sizeof(int64_t) + (size_t)seq * sizeof(float);
+    if (need > l.dbuf_cap) {
+        if (l.dbuf) (void)hipFree(l.dbuf);
+        l.dbuf = nullptr;
+        if (hipMalloc(&l.dbuf, need) != hipSuccess) return legacy_err(pt::fail(PT_ENOMEM, "sampling buffers"));
+        l.dbuf_cap = need;
+    }
+    int64_t *dh = l.dbuf, *dt = dh + seq, *dr = dt + seq;
+    float *dy = (float *)(dr + seq);
+    rc = pt_sampler_sample(&l.sampler, bs, neg, l.bern, filter, dh, dt, dr, dy, nullptr);
+    if (rc) return legacy_err(rc);
+    (void)hipMemcpy(bh, dh, sizeof(int64_t) * seq, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(bt, dt, sizeof(int64_t) * seq, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(br, dr, sizeof(int64_t) * seq, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(by, dy, sizeof(float) * seq, hipMemcpyDeviceToHost);
+}
+
+extern "C" int64_t pt_legacy_bern(void) { return L().bern; }
+
+// the global context's test / valid lists in the reference's ranking order (cmp_rel2, Reader.h:311-312)
+extern "C" int64_t pt_legacy_eval_triples(int32_t valid, int64_t *h, int64_t *t, int64_t *r) {
+    Legacy &l = L();
+    const std::vector<pt::Triple> &v = valid ? l.valid : l.test;
+    if (h && t && r)
+        for (size_t i = 0; i < v.size(); ++i) { h[i] = v[i].h; t[i] = v[i].t; r[i] = v[i].r; }
+    return (int64_t)v.size();
+}
+extern "C" const pt_known *pt_legacy_known(void) { return L().known; }
+
+extern "C" void getParallelUniverse(int64_t tc, float balance) {
+    Legacy &l = L();
+    std::lock_guard<std::mutex> lk(l.mu);
+    if (!l.train) return legacy_err(pt::fail(PT_ESTATE, "getParallelUniverse before importTrainFiles"));
+    l.uni = std::make_unique<pt::Universe>();
+    pt::build_universe(*l.train, l.rng, tc, balance, *l.uni);
+    printf("Universe configured. \n");
+}
+extern "C" int64_t getEntityTotalUniverse(void) {
+    Legacy &l = L();
+    if (!l.uni) return 0;
+    return l.swapped ? l.train->ent_total : l.uni->g.ent_total;
+}
+extern "C" int64_t getRelationTotalUniverse(void) {
+    Legacy &l = L();
+    if (!l.uni) return 0;
+    return l.swapped ? l.train->rel_total : l.uni->g.rel_total;
+}
+extern "C" int64_t getTrainTotalUniverse(void) {
+    Legacy &l = L();
+    if (!l.uni) return 0;
+    return l.swapped ? l.train->train_total : l.uni->g.train_total;
+}
+extern "C" void getEntityRemapping(int64_t *out) {
+    Legacy &l = L();
+    if (l.uni) std::copy(l.uni->ent_remap.begin(), l.uni->ent_remap.end(), out);
+}
+extern "C" void getRelationRemapping(int64_t *out) {
+    Legacy &l = L();
+    if (l.uni) std::copy(l.uni->rel_remap.begin(), l.uni->rel_remap.end(), out);
+}
+extern "C" void swapHelpers(void) {
+    Legacy &l = L();
+    std::lock_guard<std::mutex> lk(l.mu);
+    if (!l.uni) return legacy_err(pt::fail(PT_ESTATE, "swapHelpers without a universe"));
+    l.swapped = !l.swapped;
+    if (l.swapped) legacy_err(l.uni->g.upload());
+    legacy_err(legacy_sync_sampler(l));
+}
+extern "C" void resetUniverse(void) {
+    Legacy &l = L();
+    std::lock_guard<std::mutex> lk(l.mu);
+    l.swapped = false;
+    (void)hipDeviceSynchronize();   // queued steps may still read the universe graph
+    l.uni.reset();
+    legacy_err(legacy_sync_sampler(l));
+}
+
+// ----------------------------------------------------------------------- test / valid ----------
+static bool read_list(const std::string &path, std::vector<pt::Triple> &out) {
+    bool ok = true;
+    const int64_t n = pt::count_lines(path, &ok);
+    if (!ok) return false;
+    FILE *f = fopen(path.c_str(), "r");
+    out.resize((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        long a, b, c;
+        if (fscanf(f, "%ld %ld %ld", &a, &b, &c) != 3) { out.resize((size_t)i); break; }
+        out[(size_t)i] = pt::Triple{a, c, b};   // file order h t r
+    }
+    fclose(f);
+    return true;
+}
+
+extern "C" void activateLoadOfAllTriples(int64_t) { L().load_all = true; }
+
+extern "C" void importTestFiles(void) {
+    Legacy &l = L();
+    std::lock_guard<std::mutex> lk(l.mu);
+    bool ok = true;
+    l.rel_total = pt::count_lines(l.in_path + "relation2id.txt", &ok);
+    l.ent_total = pt::count_lines(l.in_path + "entity2id.txt", &ok);
+    std::vector<pt::Triple> train_all;
+    if (!read_list(l.in_path + "test2id.txt", l.test) || !read_list(l.in_path + "train2id.txt", train_all) ||
+        !read_list(l.in_path + "valid2id.txt", l.valid))
+        return legacy_err(pt::fail(PT_EIO, "importTestFiles: missing test/train/valid file under " + l.in_path));
+    l.test_total = (int64_t)l.test.size();
+    l.valid_total = (int64_t)l.valid.size();
+    l.train_lines = (int64_t)train_all.size();
+    std::vector<pt::Triple> all;
+    if (l.load_all) {
+        if (!read_list(l.in_path + "triple2id.txt", all))
+            return legacy_err(pt::fail(PT_EIO, "importTestFiles: triple2id.txt missing"));
+    } else {
+        all = l.test;
+        all.insert(all.end(), train_all.begin(), train_all.end());
+        all.insert(all.end(), l.valid.begin(), l.valid.end());
+    }
+    l.triple_total = (int64_t)all.size();
+    std::vector<int64_t> h(all.size()), t(all.size()), r(all.size());
+    for (size_t i = 0; i < all.size(); ++i) { h[i] = all[i].h; t[i] = all[i].t; r[i] = all[i].r; }
+    pt_known *k = nullptr;
+    pt_known_create(h.data(), t.data(), r.data(), (int64_t)all.size(), &k);
+    if (l.known) pt_known_free(l.known);
+    l.known = k;
+    std::sort(l.test.begin(), l.test.end(), pt::cmp_rel2);    // Reader.h:311-312
+    std::sort(l.valid.begin(), l.valid.end(), pt::cmp_rel2);
+    printf("The total of test triples is %ld.\n", (long)l.test_total);
+}
+
+namespace pt {
+void rank_one(const pt_known &k, int64_t E, int64_t h, int64_t t, int64_t r, int side, const float *con,
+              int64_t *raw, int64_t *filt);
+}
+
+extern "C" void initTest(void) {
+    Legacy &l = L();
+    l.last_head = l.last_tail = 0;
+    l.acc = TestAcc{};
+}
+
+static void fill_batch(const pt::Triple &q, int64_t E, int side, int64_t *ph, int64_t *pt_, int64_t *pr) {
+    ph[0] = q.h; pt_[0] = q.t; pr[0] = q.r;
+    const int64_t truth = side == 0 ? q.h : q.t;
+    for (int64_t i = 1; i < E; ++i) {
+        const int64_t c = i - 1 < truth ? i - 1 : i;
+        ph[i] = side == 0 ? c : q.h;
+        pt_[i] = side == 0 ? q.t : c;
+        pr[i] = q.r;
+    }
+}
+
+extern "C" void getHeadBatch(int64_t *ph, int64_t *pt_, int64_t *pr) {
+    Legacy &l = L();
+    fill_batch(l.test[(size_t)l.last_head++], l.ent_total, 0, ph, pt_, pr);
+}
+extern "C" void getTailBatch(int64_t *ph, int64_t *pt_, int64_t *pr) {
+    Legacy &l = L();
+    fill_batch(l.test[(size_t)l.last_tail++], l.ent_total, 1, ph, pt_, pr);
+}
+
+static void accumulate(TestAcc &a, int side, int64_t raw, int64_t filt) {
+    float &ft = side == 0 ? a.l_filter_tot : a.r_filter_tot, &f3 = side == 0 ? a.l3_filter_tot : a.r3_filter_tot,
+          &f1 = side == 0 ? a.l1_filter_tot : a.r1_filter_tot, &fr = side == 0 ? a.l_filter_rank : a.r_filter_rank,
+          &fi = side == 0 ? a.l_filter_reci : a.r_filter_reci;
+    float &rt = side == 0 ? a.l_tot : a.r_tot, &r3 = side == 0 ? a.l3_tot : a.r3_tot,
+          &r1 = side == 0 ? a.l1_tot : a.r1_tot, &rr = side == 0 ? a.l_rank : a.r_rank,
+          &ri = side == 0 ? a.l_reci : a.r_reci;
+    if (filt < 10) ft += 1;
+    if (raw < 10) rt += 1;
+    if (filt < 3) f3 += 1;
+    if (raw < 3) r3 += 1;
+    if (filt < 1) f1 += 1;
+    if (raw < 1) r1 += 1;
+    fr += (float)(filt + 1);
+    rr += (float)(1 + raw);
+    fi = (float)((double)fi + 1.0 / (double)(filt + 1));
+    ri = (float)((double)ri + 1.0 / (double)(raw + 1));
+}
+
+extern "C" void testHead(float *con, int64_t idx, int64_t type_constrain) {
+    Legacy &l = L();
+    if (type_constrain) legacy_err(pt::fail(PT_ENOTSUP, "type_constrain is not part of this path; ignored"));
+    const pt::Triple &q = l.test[(size_t)idx];
+    int64_t raw, filt;
+    pt::rank_one(*l.known, l.ent_total, q.h, q.t, q.r, 0, con, &raw, &filt);
+    accumulate(l.acc, 0, raw, filt);
+}
+extern "C" void testTail(float *con, int64_t idx, int64_t type_constrain) {
+    Legacy &l = L();
+    if (type_constrain) legacy_err(pt::fail(PT_ENOTSUP, "type_constrain is not part of this path; ignored"));
+    const pt::Triple &q = l.test[(size_t)idx];
+    int64_t raw, filt;
+    pt::rank_one(*l.known, l.ent_total, q.h, q.t, q.r, 1, con, &raw, &filt);
+    accumulate(l.acc, 1, raw, filt);
+}
+extern "C" void test_link_prediction(int64_t type_constrain) {
+    (void)type_constrain;
+    Legacy &l = L();
+    TestAcc &a = l.acc;
+    const float n = (float)l.test_total;
+    a.l_rank /= n; a.r_rank /= n; a.l_reci /= n; a.r_reci /= n;
+    a.l_tot /= n; a.l3_tot /= n; a.l1_tot /= n; a.r_tot /= n; a.r3_tot /= n; a.r1_tot /= n;
+    a.l_filter_rank /= n; a.r_filter_rank /= n; a.l_filter_reci /= n; a.r_filter_reci /= n;
+    a.l_filter_tot /= n; a.l3_filter_tot /= n; a.l1_filter_tot /= n;
+    a.r_filter_tot /= n; a.r3_filter_tot /= n; a.r1_filter_tot /= n;
+    printf("metric:\t\t\t MRR \t\t MR \t\t hit@10 \t hit@3  \t hit@1 \n");
+    printf("averaged(raw):\t\t %f \t %f \t %f \t %f \t %f \n", (a.l_reci + a.r_reci) / 2, (a.l_rank + a.r_rank) / 2,
+           (a.l_tot + a.r_tot) / 2, (a.l3_tot + a.r3_tot) / 2, (a.l1_tot + a.r1_tot) / 2);
+    l.mrr = (a.l_filter_reci + a.r_filter_reci) / 2;
+    l.mr = (a.l_filter_rank + a.r_filter_rank) / 2;
+    l.hit10 = (a.l_filter_tot + a.r_filter_tot) / 2;
+    l.hit3 = (a.l3_filter_tot + a.r3_filter_tot) / 2;
+    l.hit1 = (a.l1_filter_tot + a.r1_filter_tot) / 2;
+    printf("averaged(filter):\t %f \t %f \t %f \t %f \t %f \n", l.mrr, l.mr, l.hit10, l.hit3, l.hit1);
+}
+extern "C" float getTestLinkMRR(int64_t) { return L().mrr; }
+extern "C" float getTestLinkMR(int64_t) { return L().mr; }
+extern "C" float getTestLinkHit10(int64_t) { return L().hit10; }
+extern "C" float getTestLinkHit3(int64_t) { return L().hit3; }
+extern "C" float getTestLinkHit1(int64_t) { return L().hit1; }
+
+extern "C" void validInit(void) {
+    Legacy &l = L();
+    l.last_vhead = l.last_vtail = 0;
+    l.l_valid = l.r_valid = 0;
+}
+extern "C" void getValidHeadBatch(int64_t *ph, int64_t *pt_, int64_t *pr) {
+    Legacy &l = L();
+    fill_batch(l.valid[(size_t)l.last_vhead++], l.ent_total, 0, ph, pt_, pr);
+}
+extern "C" void getValidTailBatch(int64_t *ph, int64_t *pt_, int64_t *pr) {
+    Legacy &l = L();
+    fill_batch(l.valid[(size_t)l.last_vtail++], l.ent_total, 1, ph, pt_, pr);
+}
+extern "C" void validHead(float *con, int64_t idx) {
+    Legacy &l = L();
+    const pt::Triple &q = l.valid[(size_t)idx];
+    int64_t raw, filt;
+    pt::rank_one(*l.known, l.ent_total, q.h, q.t, q.r, 0, con, &raw, &filt);
+    if (filt < 10) l.l_valid += 1;
+}
+extern "C" void validTail(float *con, int64_t idx) {
+    Legacy &l = L();
+    const pt::Triple &q = l.valid[(size_t)idx];
+    int64_t raw, filt;
+    pt::rank_one(*l.known, l.ent_total, q.h, q.t, q.r, 1, con, &raw, &filt);
+    if (filt < 10) l.r_valid += 1;
+}
+extern "C" float getValidHit10(void) {
+    Legacy &l = L();
+    l.l_valid /= (float)l.valid_total;
+    l.r_valid /= (float)l.valid_total;
+    l.valid_hit10 = (l.l_valid + l.r_valid) / 2;
+    return l.valid_hit10;
+}

@@ -1,0 +1,196 @@
+// Training-graph ingest and helper indices (replaces Reader.h:58-234 importTrainFiles/loadHelpers).
+#include "graph.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace pt {
+
+bool cmp_head(const Triple &a, const Triple &b) {   // Triple.h:7-9
+    return a.h != b.h ? a.h < b.h : (a.r != b.r ? a.r < b.r : a.t < b.t);
+}
+bool cmp_tail(const Triple &a, const Triple &b) {   // Triple.h:11-13
+    return a.t != b.t ? a.t < b.t : (a.r != b.r ? a.r < b.r : a.h < b.h);
+}
+bool cmp_rel(const Triple &a, const Triple &b) {    // Triple.h:15-17
+    return a.h != b.h ? a.h < b.h : (a.t != b.t ? a.t < b.t : a.r < b.r);
+}
+bool cmp_rel2(const Triple &a, const Triple &b) {   // Triple.h:19-21
+    return a.r != b.r ? a.r < b.r : (a.h != b.h ? a.h < b.h : a.t < b.t);
+}
+
+Graph::~Graph() {
+    if (dev_block) {
+        int cur = 0;
+        if (hipGetDevice(&cur) == hipSuccess && cur != device) {
+            (void)hipSetDevice(device);
+            (void)hipFree(dev_block);
+            (void)hipSetDevice(cur);
+        } else {
+            (void)hipFree(dev_block);
+        }
+    }
+}
+
+// The line count is the record count: the reference never reads the count header (Reader.h:176-196,
+// Utilities.h:47-57), so we keep that contract for drop-in parity on headerless benchmark folders.
+int64_t count_lines(const std::string &path, bool *ok) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) {
+        *ok = false;
+        return 0;
+    }
+    int64_t n = 0;
+    char buf[1 << 16];
+    size_t k;
+    while ((k = fread(buf, 1, sizeof buf, f)) > 0)
+        for (size_t i = 0; i < k; ++i) n += buf[i] == '\n';
+    fclose(f);
+    *ok = true;
+    return n;
+}
+
+static bool read_triples(const std::string &path, int64_t n, std::vector<Triple> &out) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    out.resize((size_t)n);
+    // hand-rolled integer scanner (fscanf per field dominates ingest time on 10^6-line files)
+    std::vector<char> data;
+    {
+        fseek(f, 0, SEEK_END);
+        long sz = ftell(f);
+        fseek(f, 0, SEEK_SET);
+        data.resize((size_t)sz + 1);
+        size_t got = fread(data.data(), 1, (size_t)sz, f);
+        data[got] = 0;
+    }
+    fclose(f);
+    const char *p = data.data();
+    auto next_int = [&](int64_t &v) -> bool {
+        while (*p && !(*p == '-' || (*p >= '0' && *p <= '9'))) ++p;
+        if (!*p) return false;
+        bool neg = *p == '-';
+        if (neg) ++p;
+        int64_t x = 0;
+        while (*p >= '0' && *p <= '9') x = x * 10 + (*p++ - '0');
+        v = neg ? -x : x;
+        return true;
+    };
+    for (int64_t i = 0; i < n; ++i) {
+        Triple &tr = out[(size_t)i];
+        if (!next_int(tr.h) || !next_int(tr.t) || !next_int(tr.r)) {   // file order: h t r
+            out.resize((size_t)i);
+            return true;
+        }
+    }
+    return true;
+}
+
+void Graph::build_helpers() {
+    const int64_t n = train_total, E = ent_total, R = rel_total;
+    std::sort(list.begin(), list.end(), cmp_head);
+    head = tail = rel = rel2 = list;
+    freq_ent.assign((size_t)E, 0);
+    freq_rel.assign((size_t)R, 0);
+    for (const Triple &x : list) {
+        freq_ent[(size_t)x.h]++;
+        freq_ent[(size_t)x.t]++;
+        freq_rel[(size_t)x.r]++;
+    }
+    // head == list already (cmp_head)
+    std::sort(tail.begin(), tail.end(), cmp_tail);
+    std::sort(rel.begin(), rel.end(), cmp_rel);
+    std::sort(rel2.begin(), rel2.end(), cmp_rel2);
+    lef_head.assign((size_t)E, 0); rig_head.assign((size_t)E, -1);
+    lef_tail.assign((size_t)E, 0); rig_tail.assign((size_t)E, -1);
+    lef_rel.assign((size_t)E, 0);  rig_rel.assign((size_t)E, -1);
+    lef_rel2.assign((size_t)R, 0); rig_rel2.assign((size_t)R, -1);
+    for (int64_t i = 1; i < n; ++i) {
+        if (tail[i].t != tail[i - 1].t) { rig_tail[tail[i - 1].t] = i - 1; lef_tail[tail[i].t] = i; }
+        if (head[i].h != head[i - 1].h) { rig_head[head[i - 1].h] = i - 1; lef_head[head[i].h] = i; }
+        if (rel[i].h != rel[i - 1].h) { rig_rel[rel[i - 1].h] = i - 1; lef_rel[rel[i].h] = i; }
+        if (rel2[i].r != rel2[i - 1].r) { rig_rel2[rel2[i - 1].r] = i - 1; lef_rel2[rel2[i].r] = i; }
+    }
+    if (n > 0) {
+        lef_head[head[0].h] = 0; rig_head[head[n - 1].h] = n - 1;
+        lef_tail[tail[0].t] = 0; rig_tail[tail[n - 1].t] = n - 1;
+        lef_rel[rel[0].h] = 0;   rig_rel[rel[n - 1].h] = n - 1;
+        lef_rel2[rel2[0].r] = 0; rig_rel2[rel2[n - 1].r] = n - 1;
+    }
+    // relation-wise mean #tails per head (left) and #heads per tail (right), Reader.h:148-166
+    left_mean.assign((size_t)R, 0.f);
+    right_mean.assign((size_t)R, 0.f);
+    for (int64_t i = 0; i < E; ++i) {
+        for (int64_t j = lef_head[i] + 1; j <= rig_head[i]; ++j)
+            if (head[j].r != head[j - 1].r) left_mean[head[j].r] += 1.0f;
+        if (lef_head[i] <= rig_head[i]) left_mean[head[lef_head[i]].r] += 1.0f;
+        for (int64_t j = lef_tail[i] + 1; j <= rig_tail[i]; ++j)
+            if (tail[j].r != tail[j - 1].r) right_mean[tail[j].r] += 1.0f;
+        if (lef_tail[i] <= rig_tail[i]) right_mean[tail[lef_tail[i]].r] += 1.0f;
+    }
+    for (int64_t i = 0; i < R; ++i) {
+        left_mean[i] = (float)freq_rel[i] / left_mean[i];
+        right_mean[i] = (float)freq_rel[i] / right_mean[i];
+    }
+}
+
+int load_graph(const std::string &dir, Graph &g) {
+    bool ok = true;
+    g.rel_total = count_lines(dir + "relation2id.txt", &ok);
+    PT_CHECK(ok, PT_EIO, "cannot open " + dir + "relation2id.txt");
+    g.ent_total = count_lines(dir + "entity2id.txt", &ok);
+    PT_CHECK(ok, PT_EIO, "cannot open " + dir + "entity2id.txt");
+    int64_t n = count_lines(dir + "train2id.txt", &ok);
+    PT_CHECK(ok, PT_EIO, "cannot open " + dir + "train2id.txt");
+    PT_CHECK(read_triples(dir + "train2id.txt", n, g.list), PT_EIO, "cannot read " + dir + "train2id.txt");
+    for (const Triple &x : g.list)
+        PT_CHECK(x.h >= 0 && x.t >= 0 && x.r >= 0 && x.h < g.ent_total && x.t < g.ent_total && x.r < g.rel_total,
+                 PT_EIO, "triple id out of range in " + dir + "train2id.txt (count-header file?)");
+    std::sort(g.list.begin(), g.list.end(), cmp_head);
+    g.list.erase(std::unique(g.list.begin(), g.list.end(),
+                             [](const Triple &a, const Triple &b) { return a.h == b.h && a.r == b.r && a.t == b.t; }),
+                 g.list.end());
+    g.train_total = (int64_t)g.list.size();
+    PT_CHECK(g.train_total > 0, PT_EIO, "empty training set in " + dir);
+    g.build_helpers();
+    return PT_OK;
+}
+
+int Graph::upload() {
+    int cur = 0;
+    PT_HIP(hipGetDevice(&cur));
+    if (dev_block && device == cur) return PT_OK;
+    PT_CHECK(!dev_block, PT_ESTATE, "graph already uploaded to another device");
+    const int64_t n = train_total, E = ent_total, R = rel_total;
+    // one allocation: 5 int32 arrays of n, 4 of E, 1 float array of R (each 256-B aligned)
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    size_t off_lh = 0, off_lr = off_lh + al(4 * n), off_lt = off_lr + al(4 * n), off_th = off_lt + al(4 * n),
+           off_tr = off_th + al(4 * n), off_leh = off_tr + al(4 * n), off_rih = off_leh + al(4 * E),
+           off_let = off_rih + al(4 * E), off_rit = off_let + al(4 * E), off_bp = off_rit + al(4 * E),
+           total = off_bp + al(4 * (R ? R : 1));
+    std::vector<char> host(total, 0);
+    auto put32 = [&](size_t off, int64_t i, int64_t v) { ((int32_t *)(host.data() + off))[i] = (int32_t)v; };
+    for (int64_t i = 0; i < n; ++i) {
+        put32(off_lh, i, list[i].h); put32(off_lr, i, list[i].r); put32(off_lt, i, list[i].t);
+        put32(off_th, i, tail[i].h); put32(off_tr, i, tail[i].r);
+    }
+    for (int64_t i = 0; i < E; ++i) {
+        put32(off_leh, i, lef_head[i]); put32(off_rih, i, rig_head[i]);
+        put32(off_let, i, lef_tail[i]); put32(off_rit, i, rig_tail[i]);
+    }
+    float *bp = (float *)(host.data() + off_bp);
+    for (int64_t r = 0; r < R; ++r) bp[r] = 1000 * right_mean[r] / (right_mean[r] + left_mean[r]);
+    PT_HIP(hipMalloc(&dev_block, total));
+    PT_HIP(hipMemcpy(dev_block, host.data(), total, hipMemcpyHostToDevice));
+    char *b = (char *)dev_block;
+    dev.ent_total = E; dev.rel_total = R; dev.train_total = n;
+    dev.list_h = (int32_t *)(b + off_lh); dev.list_r = (int32_t *)(b + off_lr); dev.list_t = (int32_t *)(b + off_lt);
+    dev.tail_h = (int32_t *)(b + off_th); dev.tail_r = (int32_t *)(b + off_tr);
+    dev.lef_head = (int32_t *)(b + off_leh); dev.rig_head = (int32_t *)(b + off_rih);
+    dev.lef_tail = (int32_t *)(b + off_let); dev.rig_tail = (int32_t *)(b + off_rit);
+    dev.bern_prob = (float *)(b + off_bp);
+    device = cur;
+    return PT_OK;
+}
+
+}  // namespace pt

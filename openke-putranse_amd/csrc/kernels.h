@@ -1,0 +1,52 @@
+// Host-side launch interface of the HIP kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "graph.h"
+
+namespace pt {
+
+struct StepParams {
+    int model, p_norm, norm_flag, opt;
+    float lr, margin;
+    int64_t ent_total, rel_total, dim;
+    float *ent, *rel, *normv;
+    float *ent_acc, *rel_acc, *norm_acc;
+    int64_t batch_size, neg;
+    float inv_count;   // 1 / (batch_size * neg)
+};
+
+struct StepWorkspace {
+    float *gent = nullptr, *grel = nullptr, *gnorm = nullptr;   // gradient rows (zero between steps)
+    int *fent = nullptr, *frel = nullptr, *fnorm = nullptr;      // touched-row flags
+};
+
+struct LpUniverseDev {
+    const float *ent, *rel, *normv;
+    const int64_t *remap;   // local -> global entity
+    int64_t ent_total, dim;
+};
+
+struct LpPair {
+    int32_t key, universe, anchor, rel, side;   // local anchor entity / relation ids
+};
+
+bool shape_supported(int64_t dim);
+hipError_t launch_sample(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
+                         int bern, int filter, int64_t *h, int64_t *t, int64_t *r, float *y, hipStream_t st);
+hipError_t launch_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t dpp, hipStream_t st);
+hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t *states, int64_t threads, int bern,
+                       int filter, const int64_t *bh, const int64_t *bt, const int64_t *br, const StepWorkspace &W,
+                       float *loss, hipStream_t st);
+hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *states, int64_t threads, int64_t bs,
+                        int64_t dpp, float *loss, hipStream_t st);
+hipError_t launch_score(const StepParams &P, int mode, const int64_t *h, const int64_t *t, const int64_t *r, int64_t n,
+                        float *out, hipStream_t st);
+hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh, const int64_t *qt, const int64_t *qr,
+                                int64_t nq, int64_t E, float *out, hipStream_t st);
+hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, int64_t dim, int64_t max_ent,
+                         int model, int p_norm, int norm_flag, int64_t global_E, float *rows, hipStream_t st);
+
+}  // namespace pt

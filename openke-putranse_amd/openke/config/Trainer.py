@@ -1,0 +1,187 @@
+# coding:utf-8
+"""Trainer (mirror of openke/config/Trainer.py:12-138).
+
+Same constructor, attributes and setters. run() keeps the epoch/batch loop of Trainer.py:91-100 but
+each epoch is ONE replayed hipGraph of `nbatches` fused steps: every step samples its batch inside the
+kernel from the data loader's stream (bit-identical to TrainDataLoader.sampling()), computes
+NegativeSampling + MarginLoss forward and the analytic backward, and applies SGD or Adagrad to the
+touched rows only (identical to the reference's dense update). Losses stay on the device until the
+end of the epoch (one host sync per epoch instead of one per step)."""
+import ctypes
+import os
+
+import numpy as np
+import torch
+from tqdm import tqdm
+
+from .. import _native
+from ..module.loss import MarginLoss
+from ..module.model.Model import Model
+from ..module.strategy import NegativeSampling
+
+
+class NativeOptimizer(object):
+    """Optimizer state of the fused path (Adagrad state_sum per table, eps 1e-10, lr_decay 0,
+    initial accumulator 0 — torch.optim.Adagrad defaults used by Trainer.py:64-70)."""
+
+    def __init__(self, method, lr, tables):
+        self.method = method
+        self.lr = lr
+        self.state_sum = tuple(torch.zeros_like(t) if (t is not None and method == _native.PT_ADAGRAD) else None
+                               for t in tables)
+
+    def zero_grad(self):
+        pass
+
+
+class Trainer(object):
+
+    def __init__(self, model=None, data_loader=None, valid_dataloader=None, train_times=1000, alpha=0.5,
+                 use_gpu=True, opt_method="sgd", save_steps=None, checkpoint_dir=None):
+        self.work_threads = 8
+        self.train_times = train_times
+        self.opt_method = opt_method
+        self.optimizer = None
+        self.lr_decay = 0
+        self.weight_decay = 0
+        self.alpha = alpha
+        self.model = model
+        self.data_loader = data_loader
+        self.use_gpu = use_gpu
+        self.save_steps = save_steps
+        self.checkpoint_dir = checkpoint_dir
+        self._native = None
+        self._native_key = None
+
+    # ------------------------------------------------------------------ native setup ------------
+    def _parts(self):
+        ns = self.model
+        if not isinstance(ns, NegativeSampling):
+            raise NotImplementedError("the accelerated Trainer trains NegativeSampling(TransE|TransH, MarginLoss)")
+        kge, loss = ns.model, ns.loss
+        if not isinstance(kge, Model) or kge.native_model is None:
+            raise NotImplementedError("model %s is outside the accelerated path" % type(kge).__name__)
+        if not isinstance(loss, MarginLoss) or loss.adv_flag:
+            raise NotImplementedError("only MarginLoss without adversarial temperature is accelerated")
+        if ns.regul_rate != 0 or ns.l3_regul_rate != 0:
+            raise NotImplementedError("regularisation is outside the accelerated path")
+        if self.lr_decay != 0 or self.weight_decay != 0:
+            raise NotImplementedError("lr_decay / weight_decay are 0 in the reference path")
+        return ns, kge, loss
+
+    def _setup(self):
+        _native.require_gpu()
+        ns, kge, loss = self._parts()
+        ns.cuda()
+        if self.optimizer is None:
+            m = self.opt_method
+            if m in ("Adagrad", "adagrad"):
+                method = _native.PT_ADAGRAD
+            elif m in ("Adadelta", "adadelta", "Adam", "adam"):
+                raise NotImplementedError("%s is outside the accelerated path (SGD and Adagrad are)" % m)
+            else:
+                method = _native.PT_SGD
+            self.optimizer = NativeOptimizer(method, self.alpha, kge.tables())
+        opt = self.optimizer
+        margin = float(loss.margin.item())
+        desc = kge.native_desc(opt.method, opt.lr, margin, opt.state_sum)
+        key = (id(kge), kge.tables()[0].data_ptr(), opt.method, opt.lr, margin)
+        L = _native.lib()
+        if self._native is None:
+            h = ctypes.c_void_p()
+            _native.check(L.pt_trainer_create(ctypes.byref(desc), ctypes.byref(h)))
+            self._native = h
+        elif key != self._native_key:
+            _native.check(L.pt_trainer_update_desc(self._native, ctypes.byref(desc)))
+        self._native_key = key
+        return ns, kge, loss
+
+    def __del__(self):
+        if getattr(self, "_native", None) is not None:
+            try:
+                torch.cuda.synchronize()
+                _native.lib().pt_trainer_free(self._native)
+            except Exception:
+                pass
+            self._native = None
+
+    # ------------------------------------------------------------------ reference API -----------
+    def train_one_step(self, data):
+        """One step on an explicitly given batch (Trainer.py:44-56); returns loss.item()."""
+        ns, kge, loss = self._setup()
+        dev = kge.ent_embeddings.weight.device
+        bs = ns.batch_size
+        h = torch.as_tensor(np.asarray(data['batch_h']), dtype=torch.int64).to(dev).contiguous()
+        t = torch.as_tensor(np.asarray(data['batch_t']), dtype=torch.int64).to(dev).contiguous()
+        r = torch.as_tensor(np.asarray(data['batch_r']), dtype=torch.int64).to(dev).contiguous()
+        if data.get('mode', 'normal') != 'normal':
+            raise NotImplementedError("cross-sampled batches are outside the accelerated path")
+        n = h.numel()
+        if n % bs != 0 or n // bs < 2:
+            raise ValueError("batch of %d triples does not match batch_size %d with negatives" % (n, bs))
+        neg = n // bs - 1
+        out = torch.zeros(1, dtype=torch.float32, device=dev)
+        _native.check(_native.lib().pt_trainer_step(self._native, None, bs, neg, 0, 0, _native.ptr(h),
+                                                    _native.ptr(t), _native.ptr(r), _native.ptr(out),
+                                                    _native.stream()))
+        return out.item()
+
+    def run(self):
+        ns, kge, loss = self._setup()
+        dl = self.data_loader
+        bs, nb, neg = dl.batch_size, dl.nbatches, dl.negative_ent
+        if ns.batch_size != bs:
+            raise ValueError("NegativeSampling.batch_size (%d) differs from the loader's (%d)" % (ns.batch_size, bs))
+        L = _native.lib()
+        sampler = dl.device_sampler()
+        bern = L.pt_legacy_bern()
+        dev = kge.ent_embeddings.weight.device
+        losses = torch.zeros(max(nb, 1), dtype=torch.float32, device=dev)
+        print("Finish initializing...")
+        training_range = tqdm(range(self.train_times))
+        for epoch in training_range:
+            if nb > 0:
+                _native.check(L.pt_trainer_run(self._native, sampler, bs, neg, bern, dl.filter, nb,
+                                               _native.ptr(losses), _native.stream()))
+            host = losses.cpu().numpy()
+            res = float(host[:nb].sum())
+            loss_v = float(host[nb - 1]) if nb > 0 else 0.0
+            training_range.set_description("Epoch %d | loss: %f" % (epoch, loss_v))
+            if self.save_steps and self.checkpoint_dir and (epoch + 1) % self.save_steps == 0:
+                print("Epoch %d has finished, saving..." % (epoch))
+                kge.save_checkpoint(os.path.join(self.checkpoint_dir + "-" + str(epoch) + ".ckpt"))
+        self.last_epoch_loss = res if self.train_times > 0 else 0.0
+
+    def set_model(self, model):
+        self.model = model
+
+    def to_var(self, x, use_gpu):
+        return torch.from_numpy(x).cuda()
+
+    def set_use_gpu(self, use_gpu):
+        self.use_gpu = use_gpu
+
+    def set_alpha(self, alpha):
+        self.alpha = alpha
+        if self.optimizer is not None:
+            self.optimizer.lr = alpha
+
+    def set_lr_decay(self, lr_decay):
+        self.lr_decay = lr_decay
+
+    def set_weight_decay(self, weight_decay):
+        self.weight_decay = weight_decay
+
+    def set_opt_method(self, opt_method):
+        self.opt_method = opt_method
+
+    def set_train_times(self, train_times):
+        self.train_times = train_times
+
+    def set_save_steps(self, save_steps, checkpoint_dir=None):
+        self.save_steps = save_steps
+        if not self.checkpoint_dir:
+            self.set_checkpoint_dir(checkpoint_dir)
+
+    def set_checkpoint_dir(self, checkpoint_dir):
+        self.checkpoint_dir = checkpoint_dir

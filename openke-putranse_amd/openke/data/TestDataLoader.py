@@ -1,0 +1,128 @@
+# coding:utf-8
+"""Link-prediction data loader (mirror of openke/data/TestDataLoader.py of the reference).
+
+read() has the reference's side effects on the global context (re-seeding the sampler with its
+random_seed, default 4, and re-importing the training set, TestDataLoader.py:276-290)."""
+import ctypes
+
+import numpy as np
+
+from .. import _native
+
+
+class TestDataSampler(object):
+
+    def __init__(self, data_total, data_sampler):
+        self.data_total = data_total
+        self.data_sampler = data_sampler
+        self.total = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        self.total += 1
+        if self.total > self.data_total:
+            raise StopIteration()
+        return self.data_sampler()
+
+    def __len__(self):
+        return self.data_total
+
+
+class TestDataLoader(object):
+
+    def __init__(self, in_path="./", sampling_mode='link', random_seed=4, mode='test', setting="static",
+                 load_all_triples=False):
+        self.lib = _native.lib()
+        if setting != "static":
+            raise NotImplementedError("only the static setting is part of the accelerated path")
+        self.setting = setting
+        self.mode = mode
+        self.load_all_triples = load_all_triples
+        self.in_path = in_path
+        self.sampling_mode = sampling_mode
+        self.random_seed = random_seed
+        self.read()
+
+    def set_path(self, in_path):
+        self.lib.setInPath(ctypes.create_string_buffer(in_path.encode(), len(in_path) * 2))
+
+    def read(self):
+        self.set_path(self.in_path)
+        self.lib.setRandomSeed(self.random_seed)
+        self.lib.randReset()
+        self.lib.importTrainFiles()
+        if self.load_all_triples:
+            self.lib.activateLoadOfAllTriples(1)
+        self.lib.importTestFiles()
+        self.relTotal = self.lib.getRelationTotal()
+        self.entTotal = self.lib.getEntityTotal()
+        E = self.entTotal
+        if self.mode == 'test':
+            self.testTotal = self.lib.getTestTotal()
+            self.test_h = np.zeros(E, dtype=np.int64)
+            self.test_t = np.zeros(E, dtype=np.int64)
+            self.test_r = np.zeros(E, dtype=np.int64)
+        elif self.mode == 'valid':
+            self.validTotal = self.lib.getValidTotal()
+            self.valid_h = np.zeros(E, dtype=np.int64)
+            self.valid_t = np.zeros(E, dtype=np.int64)
+            self.valid_r = np.zeros(E, dtype=np.int64)
+
+    @staticmethod
+    def _addr(a):
+        return a.__array_interface__["data"][0]
+
+    def sampling_lp(self):
+        res = []
+        if self.mode == 'test':
+            h, t, r = self.test_h, self.test_t, self.test_r
+            head_fn, tail_fn = self.lib.getHeadBatch, self.lib.getTailBatch
+        else:
+            h, t, r = self.valid_h, self.valid_t, self.valid_r
+            head_fn, tail_fn = self.lib.getValidHeadBatch, self.lib.getValidTailBatch
+        head_fn(self._addr(h), self._addr(t), self._addr(r))
+        res.append({"batch_h": h.copy(), "batch_t": t[:1].copy(), "batch_r": r[:1].copy(), "mode": "head_batch"})
+        tail_fn(self._addr(h), self._addr(t), self._addr(r))
+        res.append({"batch_h": h[:1], "batch_t": t, "batch_r": r[:1], "mode": "tail_batch"})
+        return res
+
+    def sampling_tc(self):
+        raise NotImplementedError("triple classification is outside the accelerated path")
+
+    def eval_triples(self):
+        """(h, t, r) int64 arrays of this loader's split in the reference's ranking order."""
+        valid = 1 if self.mode == 'valid' else 0
+        n = self.lib.pt_legacy_eval_triples(valid, None, None, None)
+        h, t, r = (np.zeros(n, dtype=np.int64) for _ in range(3))
+        self.lib.pt_legacy_eval_triples(valid, self._addr(h), self._addr(t), self._addr(r))
+        return h, t, r
+
+    """interfaces to get essential parameters"""
+
+    def get_ent_tot(self):
+        return self.entTotal
+
+    def get_rel_tot(self):
+        return self.relTotal
+
+    def get_triple_tot(self):
+        return self.testTotal
+
+    def set_sampling_mode(self, sampling_mode):
+        self.sampling_mode = sampling_mode
+
+    def __len__(self):
+        return self.testTotal if self.mode == 'test' else self.validTotal
+
+    def __iter__(self):
+        if self.sampling_mode == 'link':
+            if self.mode == 'test':
+                self.lib.initTest()
+                eval_total = self.testTotal
+            else:
+                self.lib.validInit()
+                eval_total = self.validTotal
+            return TestDataSampler(eval_total, self.sampling_lp)
+        raise NotImplementedError("triple classification is outside the accelerated path")

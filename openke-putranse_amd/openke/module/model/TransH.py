@@ -1,0 +1,80 @@
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ... import _native
+from .Model import Model
+
+
+class TransH(Model):
+    """TransH (openke/module/model/TransH.py:8-114): relation-specific hyperplane projection
+    e - (e.n)n with n = normalize(norm_vector[r]) before the TransE score. Same parameters and
+    initialisation order as the reference; scoring and training run in the HIP kernels."""
+
+    native_model = _native.PT_TRANSH
+
+    def __init__(self, ent_tot, rel_tot, dim=100, p_norm=1, norm_flag=True, margin=None, epsilon=None):
+        super(TransH, self).__init__(ent_tot, rel_tot)
+        self.dim = dim
+        self.margin = margin
+        self.epsilon = epsilon
+        self.norm_flag = norm_flag
+        self.p_norm = p_norm
+        self.ent_embeddings = nn.Embedding(self.ent_tot, self.dim)
+        self.rel_embeddings = nn.Embedding(self.rel_tot, self.dim)
+        self.norm_vector = nn.Embedding(self.rel_tot, self.dim)
+        if margin is None or epsilon is None:
+            nn.init.xavier_uniform_(self.ent_embeddings.weight.data)
+            nn.init.xavier_uniform_(self.rel_embeddings.weight.data)
+            nn.init.xavier_uniform_(self.norm_vector.weight.data)
+        else:
+            self.embedding_range = nn.Parameter(torch.Tensor([(self.margin + self.epsilon) / self.dim]),
+                                                requires_grad=False)
+            for emb in (self.ent_embeddings, self.rel_embeddings, self.norm_vector):
+                nn.init.uniform_(tensor=emb.weight.data, a=-self.embedding_range.item(),
+                                 b=self.embedding_range.item())
+        if margin is not None:
+            self.margin = nn.Parameter(torch.Tensor([margin]))
+            self.margin.requires_grad = False
+            self.margin_flag = True
+        else:
+            self.margin_flag = False
+
+    def _calc(self, h, t, r, mode):
+        if self.norm_flag:
+            h = F.normalize(h, 2, -1)
+            r = F.normalize(r, 2, -1)
+            t = F.normalize(t, 2, -1)
+        if mode != 'normal':
+            h = h.view(-1, r.shape[0], h.shape[-1])
+            t = t.view(-1, r.shape[0], t.shape[-1])
+            r = r.view(-1, r.shape[0], r.shape[-1])
+        if mode == 'head_batch':
+            score = h + (r - t)
+        else:
+            score = (h + r) - t
+        return torch.norm(score, self.p_norm, -1).flatten()
+
+    def _transfer(self, e, norm):
+        norm = F.normalize(norm, p=2, dim=-1)
+        if e.shape[0] != norm.shape[0]:
+            e = e.view(-1, norm.shape[0], e.shape[-1])
+            norm = norm.view(-1, norm.shape[0], norm.shape[-1])
+            e = e - torch.sum(e * norm, -1, True) * norm
+            return e.view(-1, e.shape[-1])
+        return e - torch.sum(e * norm, -1, True) * norm
+
+    def forward(self, data):
+        score = self.native_score(data)
+        if self.margin_flag:
+            return self.margin - score
+        return score
+
+    def regularization(self, data):
+        raise NotImplementedError("regularisation is outside the accelerated path (regul_rate is 0 in every config)")
+
+    def predict(self, data):
+        score = self.forward(data)
+        if self.margin_flag:
+            score = self.margin - score
+        return score.cpu().data.numpy()

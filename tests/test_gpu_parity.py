@@ -1,0 +1,224 @@
+"""GPU parity tests: the HIP path (through the C-ABI and the drop-in openke API) against the
+reference's golden vectors and the CPU oracle. Run on an MI355X: pytest -m gpu."""
+import ctypes
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import KG_SMALL, KG_TINY, PKG
+from helpers import DATASETS, IllConditioned, assert_tables_close, golden, load, torch_init_tables
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    assert torch.cuda.is_available(), "GPU tests need a visible HIP device"
+
+
+def _loader(ds, threads, bs, neg, bern, filt, seed):
+    from openke.data import TrainDataLoader
+    return TrainDataLoader(in_path=DATASETS[ds], batch_size=bs, threads=threads, sampling_mode="normal",
+                           bern_flag=bern, filter_flag=filt, neg_ent=neg, neg_rel=0, random_seed=seed)
+
+
+@pytest.mark.parametrize("path", golden("sampler_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_sampler_bit_exact_on_gpu(path):
+    """TrainDataLoader.sampling() (GPU sampler behind the Base.so-compatible ABI) == reference."""
+    z = load(path)
+    dl = _loader(str(z["dataset"]), int(z["threads"]), int(z["batch_size"]), int(z["neg_ent"]), int(z["bern"]),
+                 int(z["filter"]), int(z["seed"]))
+    for c in range(z["batch_h"].shape[0]):
+        d = dl.sampling()
+        np.testing.assert_array_equal(d["batch_h"], z["batch_h"][c])
+        np.testing.assert_array_equal(d["batch_t"], z["batch_t"][c])
+        np.testing.assert_array_equal(d["batch_r"], z["batch_r"][c])
+        np.testing.assert_array_equal(d["batch_y"], z["batch_y"][c])
+
+
+def _model(z, dl):
+    from openke.module.loss import MarginLoss
+    from openke.module.model import TransE, TransH
+    from openke.module.strategy import NegativeSampling
+    torch.manual_seed(int(z["torch_seed"]))
+    cls = TransE if str(z["model"]) == "TransE" else TransH
+    kge = cls(ent_tot=dl.get_ent_tot(), rel_tot=dl.get_rel_tot(), dim=int(z["dim"]), p_norm=int(z["p_norm"]),
+              norm_flag=bool(z["norm_flag"]))
+    ns = NegativeSampling(model=kge, loss=MarginLoss(margin=float(z["margin"])), batch_size=dl.get_batch_size())
+    return kge, ns
+
+
+def _tables(kge):
+    out = {"ent": kge.ent_embeddings.weight.detach().cpu().numpy(),
+           "rel": kge.rel_embeddings.weight.detach().cpu().numpy()}
+    if hasattr(kge, "norm_vector"):
+        out["norm"] = kge.norm_vector.weight.detach().cpu().numpy()
+    return out
+
+
+GOLD_KEYS = {"ent": "ent_embeddings", "rel": "rel_embeddings", "norm": "norm_vector"}
+
+
+@pytest.mark.parametrize("path", golden("train_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_train_one_step_matches_reference(path):
+    """Trainer.train_one_step on the reference's own batches: loss and updated tables."""
+    from openke.config import Trainer
+    z = load(path)
+    dl = _loader("small", int(z["threads"]), int(z["batch_size"]), int(z["neg_ent"]), int(z["bern"]),
+                 int(z["filter"]), int(z["seed"]))
+    kge, ns = _model(z, dl)
+    tr = Trainer(model=ns, data_loader=dl, train_times=0, alpha=float(z["lr"]), use_gpu=True,
+                 opt_method=str(z["opt"]))
+    tr.run()
+    ada = str(z["opt"]) == "adagrad"
+    ill = IllConditioned()
+    for s in range(int(z["steps"])):
+        d = dl.sampling()
+        np.testing.assert_array_equal(d["batch_h"], z["batch_h"][s])
+        np.testing.assert_array_equal(d["batch_t"], z["batch_t"][s])
+        np.testing.assert_array_equal(d["batch_r"], z["batch_r"][s])
+        if ada:
+            for name, a in zip(("ent", "rel", "norm"), tr.optimizer.state_sum):
+                ill.before(name, None if a is None else a.cpu().numpy())
+        loss = tr.train_one_step(d)
+        assert abs(loss - z["losses"][s]) <= 1e-5 * max(1.0, abs(z["losses"][s])), (s, loss, z["losses"][s])
+        if ada:
+            for name, a in zip(("ent", "rel", "norm"), tr.optimizer.state_sum):
+                ill.after(name, None if a is None else a.cpu().numpy())
+        if s == 0:
+            for k, v in _tables(kge).items():
+                assert_tables_close(v, z["step1_" + GOLD_KEYS[k]], 2e-6, ill.get(k))
+    for k, v in _tables(kge).items():
+        assert_tables_close(v, z["final_" + GOLD_KEYS[k]], 1e-5, ill.get(k))
+
+
+@pytest.mark.parametrize("path", golden("train_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_fused_epoch_matches_reference(path):
+    """Trainer.run(): in-kernel sampling + fused steps replayed as one hipGraph == reference."""
+    from openke.config import Trainer
+    z = load(path)
+    steps = int(z["steps"])
+    dl = _loader("small", int(z["threads"]), int(z["batch_size"]), int(z["neg_ent"]), int(z["bern"]),
+                 int(z["filter"]), int(z["seed"]))
+    dl.nbatches = steps
+    kge, ns = _model(z, dl)
+    tr = Trainer(model=ns, data_loader=dl, train_times=1, alpha=float(z["lr"]), use_gpu=True,
+                 opt_method=str(z["opt"]))
+    tr.run()
+    ada = str(z["opt"]) == "adagrad"
+    ill = IllConditioned(noise2=1e-14)
+    if ada:
+        for name, a in zip(("ent", "rel", "norm"), tr.optimizer.state_sum):
+            ill.after(name, None if a is None else a.cpu().numpy())
+    np.testing.assert_allclose(tr.last_epoch_loss, float(np.sum(z["losses"])), rtol=1e-5)
+    for k, v in _tables(kge).items():
+        assert_tables_close(v, z["final_" + GOLD_KEYS[k]], 1e-5, ill.get(k))
+    # the stream advanced exactly like `steps` sampling() calls: the next batch matches the oracle's
+    kg = oracle.KG.load(KG_SMALL)
+    st = oracle.GlibcRand(int(z["seed"])).rand_reset(int(z["threads"]))
+    for _ in range(steps + 1):
+        h, t, r, _ = kg.sample(st, int(z["threads"]), int(z["batch_size"]), int(z["neg_ent"]), int(z["bern"]),
+                               int(z["filter"]))
+    d = dl.sampling()
+    np.testing.assert_array_equal(d["batch_h"], h)
+    np.testing.assert_array_equal(d["batch_t"], t)
+
+
+@pytest.mark.parametrize("path", golden("lp_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_link_prediction_matches_reference(path):
+    """Tester.run_link_prediction over the HIP scoring kernel == the reference's metrics."""
+    from openke.config import Tester
+    from openke.data import TestDataLoader
+    from openke.module.model import TransE, TransH
+    z = load(path)
+    test_dl = TestDataLoader(KG_SMALL, "link")
+    cls = TransE if str(z["model"]) == "TransE" else TransH
+    kge = cls(ent_tot=test_dl.get_ent_tot(), rel_tot=test_dl.get_rel_tot(), dim=int(z["dim"]),
+              p_norm=int(z["p_norm"]), norm_flag=True)
+    with torch.no_grad():
+        kge.ent_embeddings.weight.copy_(torch.from_numpy(z["ent_embeddings"]))
+        kge.rel_embeddings.weight.copy_(torch.from_numpy(z["rel_embeddings"]))
+        if str(z["model"]) == "TransH":
+            kge.norm_vector.weight.copy_(torch.from_numpy(z["norm_vector"]))
+    tester = Tester(model=kge, data_loader=test_dl, use_gpu=True)
+    res = tester.run_link_prediction(type_constrain=False)
+    np.testing.assert_allclose(np.array(res, dtype=np.float32), z["metrics"].astype(np.float32), rtol=1e-6)
+
+
+@pytest.mark.parametrize("model,p,norm_flag", [("TransE", 1, True), ("TransE", 2, True), ("TransE", 2, False),
+                                               ("TransH", 1, True), ("TransH", 2, True)])
+@pytest.mark.parametrize("dim", [8, 20, 50, 200, 300])
+def test_scores_match_oracle(model, p, norm_flag, dim):
+    """pt_score (model.predict) in all three modes against the oracle's restatement."""
+    from openke.module.model import TransE, TransH
+    E, R = 300, 9
+    torch.manual_seed(dim + p)
+    cls = TransE if model == "TransE" else TransH
+    kge = cls(E, R, dim=dim, p_norm=p, norm_flag=norm_flag).cuda()
+    T = _tables(kge)
+    rng = np.random.default_rng(dim)
+    n = 1000
+    h, t, r = rng.integers(0, E, n), rng.integers(0, E, n), rng.integers(0, R, n)
+    for mode, hh, tt, rr in (("normal", h, t, r), ("head_batch", h, t[:1], r[:1]), ("tail_batch", h[:1], t, r[:1])):
+        got = kge.predict({"batch_h": hh, "batch_t": tt, "batch_r": rr, "mode": mode})
+        ref = oracle.score(model, p, norm_flag, mode, T["ent"], T["rel"], T.get("norm"), hh, tt, rr)
+        np.testing.assert_allclose(got, ref, rtol=2e-6, atol=2e-6)
+
+
+def test_full_size_fb15k237_step_matches_oracle(tmp_path):
+    """C2 shape (FB15K237-shaped synthetic: E=14,541, R=237, D=200, bs=2000, neg=25, L2, bern, filter):
+    the GPU sampler is bit-exact with the oracle at full size and one fused SGD step matches the
+    oracle's step from the same state within fp32 tolerance."""
+    import sys
+    sys.path.insert(0, os.path.join(PKG, "tools"))
+    import synth_kg
+    from openke.config import Trainer
+    from openke.module.loss import MarginLoss
+    from openke.module.model import TransE
+    from openke.module.strategy import NegativeSampling
+    path = synth_kg.ensure_dataset(str(tmp_path), "fb15k237")
+    bs, neg = 2000, 25
+    dl = _loader_path(path, 8, bs, neg, 1, 1, 4)
+    kg = oracle.KG.load(path)
+    st = oracle.GlibcRand(4).rand_reset(8)
+    h, t, r, _ = kg.sample(st, 8, bs, neg, 1, 1)
+    d = dl.sampling()
+    np.testing.assert_array_equal(d["batch_h"], h)
+    np.testing.assert_array_equal(d["batch_t"], t)
+    np.testing.assert_array_equal(d["batch_r"], r)
+    torch.manual_seed(0)
+    kge = TransE(dl.get_ent_tot(), dl.get_rel_tot(), dim=200, p_norm=2, norm_flag=True)
+    ent0 = kge.ent_embeddings.weight.detach().numpy().copy()
+    rel0 = kge.rel_embeddings.weight.detach().numpy().copy()
+    ns = NegativeSampling(model=kge, loss=MarginLoss(margin=5.0), batch_size=bs)
+    tr = Trainer(model=ns, data_loader=dl, train_times=0, alpha=1.0, use_gpu=True)
+    tr.run()
+    # fused in-kernel-sampled step (the bench's step) vs oracle on the next batch
+    dl.nbatches = 1
+    tr.train_times = 1
+    tr.run()
+    h2, t2, r2, _ = kg.sample(st, 8, bs, neg, 1, 1)
+    ent, rel = ent0.copy(), rel0.copy()
+    loss = oracle.train_step("TransE", 2, True, "sgd", 1.0, 5.0, ent, rel, None, (None, None, None), h2, t2, r2, bs, neg)
+    np.testing.assert_allclose(tr.last_epoch_loss, loss, rtol=1e-5)
+    got = _tables(kge)
+    assert_tables_close(got["ent"], ent, 1e-5)
+    assert_tables_close(got["rel"], rel, 1e-5)
+
+
+def _loader_path(path, threads, bs, neg, bern, filt, seed):
+    from openke.data import TrainDataLoader
+    return TrainDataLoader(in_path=path, batch_size=bs, threads=threads, sampling_mode="normal",
+                           bern_flag=bern, filter_flag=filt, neg_ent=neg, neg_rel=0, random_seed=seed)
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    from openke import _native
+    monkeypatch.setattr(_native, "_LIB", None)
+    monkeypatch.setattr(_native, "LIB_PATH", "/nonexistent/libputranse_hip.so")
+    with pytest.raises(_native.NativeError):
+        _native.lib()

@@ -1,0 +1,164 @@
+"""CPU-side checks of the product library: it loads, exports every symbol include/putranse.h
+declares, and its host-side parts (graph ingest, universe construction, ranking, metrics) match the
+oracle / the reference's golden vectors. No GPU compute is called here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import KG_SMALL, REPO
+from helpers import golden, load
+from openke import _native
+
+
+def header_symbols():
+    src = open(os.path.join(REPO, "include", "putranse.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\([^;]*\)\s*;", src, flags=re.M)
+    return sorted(set(n for n in names if n not in ("if", "sizeof")))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _native.lib()
+    names = header_symbols()
+    assert len(names) > 60, names
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    # and the Python binding declares a signature for each of them
+    assert not [n for n in names if n not in _native.SIGNATURES], [n for n in names if n not in _native.SIGNATURES]
+    assert L.pt_version() == 1
+
+
+def _graph(path):
+    h = ctypes.c_void_p()
+    _native.check(_native.lib().pt_graph_load(path.encode(), ctypes.byref(h)))
+    return h
+
+
+def test_graph_ingest_matches_oracle():
+    L = _native.lib()
+    g = _graph(KG_SMALL)
+    kg = oracle.KG.load(KG_SMALL)
+    assert L.pt_graph_ent_total(g) == kg.ent_total
+    assert L.pt_graph_rel_total(g) == kg.rel_total
+    n = L.pt_graph_train_total(g)
+    assert n == kg.train_total
+    h, t, r = (np.zeros(n, dtype=np.int64) for _ in range(3))
+    _native.check(L.pt_graph_triples(g, h.ctypes.data, t.ctypes.data, r.ctypes.data))
+    oh, ot, orr = kg.train()
+    np.testing.assert_array_equal(h, oh)
+    np.testing.assert_array_equal(t, ot)
+    np.testing.assert_array_equal(r, orr)
+    L.pt_graph_free(g)
+
+
+def test_graph_load_errors_are_reported_not_fatal():
+    L = _native.lib()
+    h = ctypes.c_void_p()
+    rc = L.pt_graph_load(b"/nonexistent/dir/", ctypes.byref(h))
+    assert rc == 2
+    assert b"cannot open" in L.pt_last_error()
+
+
+@pytest.mark.parametrize("path", golden("universes_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_universe_construction_matches_reference(path):
+    z = load(path)
+    L = _native.lib()
+    g = _graph(KG_SMALL)
+    seed0, n = int(z["seed0"]), int(z["n_univ"])
+    seeds = np.array([seed0 + u for u in range(n)], dtype=np.int64)
+    tcs = np.array([int(z["u%d_tc" % u]) for u in range(n)], dtype=np.int64)
+    bals = np.array([float(z["u%d_balance" % u]) for u in range(n)], dtype=np.float32)
+    outs = (ctypes.c_void_p * n)()
+    _native.check(L.pt_universe_build_many(g, n, seeds.ctypes.data, 8, tcs.ctypes.data, bals.ctypes.data, 4, outs))
+    for u in range(n):
+        U = ctypes.c_void_p(outs[u])
+        assert L.pt_universe_train_total(U) == int(z["u%d_train_total" % u])
+        E, R = L.pt_universe_ent_total(U), L.pt_universe_rel_total(U)
+        em, rm = np.zeros(E, dtype=np.int64), np.zeros(R, dtype=np.int64)
+        _native.check(L.pt_universe_remaps(U, em.ctypes.data, rm.ctypes.data))
+        np.testing.assert_array_equal(em, z["u%d_ent_remap" % u])
+        np.testing.assert_array_equal(rm, z["u%d_rel_remap" % u])
+        # the universe graph's helper-sorted triples equal the oracle's restatement
+        rng = oracle.GlibcRand(seed0 + u)
+        st = rng.rand_reset(8)
+        seeds_out = np.zeros(8, dtype=np.uint64)
+        _native.check(L.pt_universe_seeds(U, seeds_out.ctypes.data))
+        np.testing.assert_array_equal(seeds_out, st)
+        L.pt_universe_free(U)
+    L.pt_graph_free(g)
+
+
+def test_universe_construction_matches_oracle_on_many_seeds():
+    """Bit-exact universes for 40 seeds and a range of sizes/balances on the small KG."""
+    L = _native.lib()
+    g = _graph(KG_SMALL)
+    kg = oracle.KG.load(KG_SMALL)
+    for k in range(40):
+        tc = 100 + 37 * k
+        bal = 0.25 + 0.006 * k
+        U = ctypes.c_void_p()
+        _native.check(L.pt_universe_build(g, 1000 + k, 8, tc, ctypes.c_float(bal), ctypes.byref(U)))
+        rng = oracle.GlibcRand(1000 + k)
+        rng.rand_reset(8)
+        ug, em, rm = kg.universe(rng, tc, bal)
+        assert L.pt_universe_train_total(U) == ug.train_total
+        E = L.pt_universe_ent_total(U)
+        pem = np.zeros(E, dtype=np.int64)
+        _native.check(L.pt_universe_remaps(U, pem.ctypes.data, None))
+        np.testing.assert_array_equal(pem, em)
+        G = L.pt_universe_graph(U)
+        n = L.pt_graph_train_total(G)
+        h, t, r = (np.zeros(n, dtype=np.int64) for _ in range(3))
+        _native.check(L.pt_graph_triples(G, h.ctypes.data, t.ctypes.data, r.ctypes.data))
+        oh, ot, orr = ug.train()
+        np.testing.assert_array_equal(h, oh)
+        np.testing.assert_array_equal(t, ot)
+        np.testing.assert_array_equal(r, orr)
+        L.pt_universe_free(U)
+    L.pt_graph_free(g)
+
+
+@pytest.mark.parametrize("path", golden("lp_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_ranking_and_metrics_match_reference(path):
+    """Host ranking (pt_rank_queries) + float metric accumulation (pt_lp_metrics) on oracle scores
+    reproduce the reference's link-prediction numbers."""
+    z = load(path)
+    L = _native.lib()
+    model, p = str(z["model"]), int(z["p_norm"])
+    kg = oracle.KG.load(KG_SMALL)
+    E = kg.ent_total
+    ent, rel = z["ent_embeddings"], z["rel_embeddings"]
+    nv = z["norm_vector"] if model == "TransH" else None
+    th, tt, tr = oracle.sort_test(*oracle.read_triples(KG_SMALL + "test2id.txt"))
+    all_tr = [np.ascontiguousarray(np.concatenate(x)) for x in zip(*(oracle.read_triples(KG_SMALL + f)
+                                                                  for f in ("test2id.txt", "train2id.txt",
+                                                                            "valid2id.txt")))]
+    n = len(th)
+    con_h = np.zeros((n, E), dtype=np.float32)
+    con_t = np.zeros((n, E), dtype=np.float32)
+    for q in range(n):
+        con_h[q] = oracle.score(model, p, True, "head_batch", ent, rel, nv, oracle.candidates(E, th[q]), [tt[q]], [tr[q]])
+        con_t[q] = oracle.score(model, p, True, "tail_batch", ent, rel, nv, [th[q]], oracle.candidates(E, tt[q]), [tr[q]])
+    known = ctypes.c_void_p()
+    _native.check(L.pt_known_create(all_tr[0].ctypes.data, all_tr[1].ctypes.data, all_tr[2].ctypes.data,
+                                    len(all_tr[0]), ctypes.byref(known)))
+    ranks = []
+    for side, con in ((0, con_h), (1, con_t)):
+        raw, filt = np.zeros(n, dtype=np.int64), np.zeros(n, dtype=np.int64)
+        _native.check(L.pt_rank_queries(known, E, th.ctypes.data, tt.ctypes.data, tr.ctypes.data, n, side,
+                                        con.ctypes.data, raw.ctypes.data, filt.ctypes.data, 4))
+        ranks += [raw, filt]
+    _, (orh, ofh, ort, oft) = oracle.link_prediction(E, all_tr, (th, tt, tr), con_h, con_t)
+    np.testing.assert_array_equal(ranks[0], orh)
+    np.testing.assert_array_equal(ranks[1], ofh)
+    np.testing.assert_array_equal(ranks[2], ort)
+    np.testing.assert_array_equal(ranks[3], oft)
+    met = np.zeros(10, dtype=np.float32)
+    _native.check(L.pt_lp_metrics(ranks[0].ctypes.data, ranks[1].ctypes.data, ranks[2].ctypes.data,
+                                  ranks[3].ctypes.data, n, met.ctypes.data))
+    np.testing.assert_array_equal(met[:5], z["metrics"].astype(np.float32))
+    L.pt_known_free(known)
