@@ -150,6 +150,8 @@ def train_step(model, p, norm_flag, opt, lr, margin, ent, rel, normv, accs, h, t
     dummy = np.zeros(1, dtype=np.float32)
     nv = normv if normv is not None else dummy
     ea, ra, na = accs
+    ea = ea if ea is not None else dummy
+    ra = ra if ra is not None else dummy
     na = na if na is not None else dummy
     h = np.ascontiguousarray(h, dtype=np.int64)
     t = np.ascontiguousarray(t, dtype=np.int64)
@@ -211,6 +213,8 @@ def train_loop(kg, states, threads, bs, neg, bern, filt, model, p, norm_flag, op
     ea, ra, na = accs
     dummy = np.zeros(1, dtype=np.float32)
     nv = normv if normv is not None else dummy
+    ea = ea if ea is not None else dummy
+    ra = ra if ra is not None else dummy
     na = na if na is not None else dummy
     return lib().oracle_train_loop(kg.h, _p(states, u64p), threads, bs, neg, bern, filt, MODELS[model], p,
                                    int(norm_flag), OPTS[opt], lr, margin, ent.shape[1], _p(ent, f32p),
