@@ -305,7 +305,7 @@ extern "C" int pt_trainer_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t 
     if (rc) return rc;
     rc = s->g->upload();
     if (rc) return rc;
-    GraphKey key{s, s->g->dev.list_h, d_losses, s->d_states, bs, neg, bern, filter, steps};
+    GraphKey key{s, s->g->dev.rec, d_losses, s->d_states, bs, neg, bern, filter, steps};
     auto it = t->graphs.find(key);
     if (it == t->graphs.end()) {
         hipGraph_t graph;

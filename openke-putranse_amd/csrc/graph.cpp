@@ -161,34 +161,53 @@ int Graph::upload() {
     PT_HIP(hipGetDevice(&cur));
     if (dev_block && device == cur) return PT_OK;
     PT_CHECK(!dev_block, PT_ESTATE, "graph already uploaded to another device");
-    const int64_t n = train_total, E = ent_total, R = rel_total;
-    // one allocation: 5 int32 arrays of n, 4 of E, 1 float array of R (each 256-B aligned)
-    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    size_t off_lh = 0, off_lr = off_lh + al(4 * n), off_lt = off_lr + al(4 * n), off_th = off_lt + al(4 * n),
-           off_tr = off_th + al(4 * n), off_leh = off_tr + al(4 * n), off_rih = off_leh + al(4 * E),
-           off_let = off_rih + al(4 * E), off_rit = off_let + al(4 * E), off_bp = off_rit + al(4 * E),
-           total = off_bp + al(4 * (R ? R : 1));
-    std::vector<char> host(total, 0);
-    auto put32 = [&](size_t off, int64_t i, int64_t v) { ((int32_t *)(host.data() + off))[i] = (int32_t)v; };
-    for (int64_t i = 0; i < n; ++i) {
-        put32(off_lh, i, list[i].h); put32(off_lr, i, list[i].r); put32(off_lt, i, list[i].t);
-        put32(off_th, i, tail[i].h); put32(off_tr, i, tail[i].r);
+    const int64_t n = train_total, R = rel_total;
+    std::vector<TripleRec> rec((size_t)n);
+    // (h,r) runs of the cmp_head list
+    for (int64_t i = 0; i < n;) {
+        int64_t j = i;
+        while (j + 1 < n && list[j + 1].h == list[i].h && list[j + 1].r == list[i].r) ++j;
+        for (int64_t k = i; k <= j; ++k) {
+            rec[k] = TripleRec{(int32_t)list[k].h, (int32_t)list[k].r, (int32_t)list[k].t, (int32_t)i, (int32_t)j,
+                               0, 0, 0};
+        }
+        i = j + 1;
     }
-    for (int64_t i = 0; i < E; ++i) {
-        put32(off_leh, i, lef_head[i]); put32(off_rih, i, rig_head[i]);
-        put32(off_let, i, lef_tail[i]); put32(off_rit, i, rig_tail[i]);
+    // (t,r) runs of the cmp_tail list, mapped back to head order
+    std::vector<int64_t> order((size_t)n);
+    for (int64_t i = 0; i < n; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return cmp_tail(list[a], list[b]); });
+    for (int64_t i = 0; i < n;) {
+        int64_t j = i;
+        while (j + 1 < n && tail[j + 1].t == tail[i].t && tail[j + 1].r == tail[i].r) ++j;
+        for (int64_t k = i; k <= j; ++k) {
+            rec[order[k]].tr_lo = (int32_t)i;
+            rec[order[k]].tr_hi = (int32_t)j;
+        }
+        i = j + 1;
+    }
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t off_rec = 0, off_ht = off_rec + al(sizeof(TripleRec) * n), off_th = off_ht + al(4 * n),
+                 off_bp = off_th + al(4 * n), total = off_bp + al(4 * (R ? R : 1));
+    std::vector<char> host(total, 0);
+    memcpy(host.data() + off_rec, rec.data(), sizeof(TripleRec) * n);
+    int32_t *ht = (int32_t *)(host.data() + off_ht), *th = (int32_t *)(host.data() + off_th);
+    for (int64_t i = 0; i < n; ++i) {
+        ht[i] = (int32_t)head[i].t;
+        th[i] = (int32_t)tail[i].h;
     }
     float *bp = (float *)(host.data() + off_bp);
     for (int64_t r = 0; r < R; ++r) bp[r] = 1000 * right_mean[r] / (right_mean[r] + left_mean[r]);
     PT_HIP(hipMalloc(&dev_block, total));
     PT_HIP(hipMemcpy(dev_block, host.data(), total, hipMemcpyHostToDevice));
     char *b = (char *)dev_block;
-    dev.ent_total = E; dev.rel_total = R; dev.train_total = n;
-    dev.list_h = (int32_t *)(b + off_lh); dev.list_r = (int32_t *)(b + off_lr); dev.list_t = (int32_t *)(b + off_lt);
-    dev.tail_h = (int32_t *)(b + off_th); dev.tail_r = (int32_t *)(b + off_tr);
-    dev.lef_head = (int32_t *)(b + off_leh); dev.rig_head = (int32_t *)(b + off_rih);
-    dev.lef_tail = (int32_t *)(b + off_let); dev.rig_tail = (int32_t *)(b + off_rit);
-    dev.bern_prob = (float *)(b + off_bp);
+    dev.ent_total = ent_total;
+    dev.rel_total = R;
+    dev.train_total = n;
+    dev.rec = (const TripleRec *)(b + off_rec);
+    dev.head_t = (const int32_t *)(b + off_ht);
+    dev.tail_h = (const int32_t *)(b + off_th);
+    dev.bern_prob = (const float *)(b + off_bp);
     device = cur;
     return PT_OK;
 }

@@ -12,12 +12,20 @@ struct Triple {
     int64_t h, r, t;
 };
 
-// Device mirror consumed by the kernels (ids as int32: every benchmark id fits, halves the bytes).
+// One training triple as the sampler needs it (ids as int32: every benchmark id fits). hr_lo/hr_hi
+// bound the triple's (h,r) run in the cmp_head list and tr_lo/tr_hi its (t,r) run in the cmp_tail
+// list: exactly the [ll, rr] the reference finds with two binary searches per filtered corruption
+// (Corrupt.h:27-42, :75-90), precomputed once so a corruption costs one dependent load, not ~2 log n.
+struct TripleRec {
+    int32_t h, r, t, hr_lo, hr_hi, tr_lo, tr_hi, pad;
+};
+
+// Device mirror consumed by the kernels.
 struct DeviceGraph {
     int64_t ent_total = 0, rel_total = 0, train_total = 0;
-    const int32_t *list_h = nullptr, *list_r = nullptr, *list_t = nullptr;   // cmp_head order (= trainHead)
-    const int32_t *tail_h = nullptr, *tail_r = nullptr;                      // cmp_tail order (trainTail)
-    const int32_t *lef_head = nullptr, *rig_head = nullptr, *lef_tail = nullptr, *rig_tail = nullptr;
+    const TripleRec *rec = nullptr;     // cmp_head order (trainList == trainHead after the reader's sort)
+    const int32_t *head_t = nullptr;    // trainHead[k].t: values corrupt_head searches
+    const int32_t *tail_h = nullptr;    // trainTail[k].h: values corrupt_tail searches
     const float *bern_prob = nullptr;   // per relation: 1000*right_mean/(right_mean+left_mean) (Base.cpp:219-221)
 };
 

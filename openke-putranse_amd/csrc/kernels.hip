@@ -165,59 +165,21 @@ __device__ __forceinline__ void vpnorm_bwd(const V<G, VEC, KCH> &v, float nv, in
 // ---------------------------------------------------------------- sampler --------------------
 __device__ __forceinline__ int64_t rand_max(uint64_t &s, int64_t x) { return (int64_t)(lcg_next(s) % (uint64_t)x); }
 
-// corrupt_head with filter (Corrupt.h:27-56): replacement TAIL avoiding known (h,r,.) tails,
-// searched in the cmp_head list (trainHead == trainList after the reader's sort).
-__device__ int64_t corrupt_head_filtered(const DeviceGraph &g, int64_t h, int64_t r, uint64_t &s) {
-    int64_t lo = (int64_t)g.lef_head[h] - 1, hi = g.rig_head[h], mid;
-    while (lo + 1 < hi) {
-        mid = (lo + hi) >> 1;
-        if (g.list_r[mid] >= r) hi = mid; else lo = mid;
+// Filtered corruption (Corrupt.h:27-56 / :75-104): `vals` is the searched column of the sorted list
+// (trainHead[].t for corrupt_head, trainTail[].h for corrupt_tail) and [lo, hi] the run of known
+// partners of the positive's (entity, relation) - the [ll, rr] of the reference's two binary searches,
+// precomputed per triple (TripleRec). The draw and the final search are the reference's.
+__device__ __forceinline__ int64_t corrupt_in_run(const int32_t *__restrict__ vals, int64_t lo, int64_t hi, int64_t E,
+                                                  uint64_t &s) {
+    const int64_t tmp = rand_max(s, E - (hi - lo + 1));
+    if (tmp < vals[lo]) return tmp;
+    if (tmp > vals[hi] - hi + lo - 1) return tmp + hi - lo + 1;
+    int64_t l = lo, r = hi + 1;
+    while (l + 1 < r) {
+        const int64_t mid = (l + r) >> 1;
+        if (vals[mid] - mid + lo - 1 < tmp) l = mid; else r = mid;
     }
-    const int64_t ll = hi;
-    lo = g.lef_head[h];
-    hi = (int64_t)g.rig_head[h] + 1;
-    while (lo + 1 < hi) {
-        mid = (lo + hi) >> 1;
-        if (g.list_r[mid] <= r) lo = mid; else hi = mid;
-    }
-    const int64_t rr = lo;
-    const int64_t tmp = rand_max(s, g.ent_total - (rr - ll + 1));
-    if (tmp < g.list_t[ll]) return tmp;
-    if (tmp > g.list_t[rr] - rr + ll - 1) return tmp + rr - ll + 1;
-    lo = ll;
-    hi = rr + 1;
-    while (lo + 1 < hi) {
-        mid = (lo + hi) >> 1;
-        if (g.list_t[mid] - mid + ll - 1 < tmp) lo = mid; else hi = mid;
-    }
-    return tmp + lo - ll + 1;
-}
-
-// corrupt_tail with filter (Corrupt.h:75-104): replacement HEAD avoiding known (.,r,t) heads.
-__device__ int64_t corrupt_tail_filtered(const DeviceGraph &g, int64_t t, int64_t r, uint64_t &s) {
-    int64_t lo = (int64_t)g.lef_tail[t] - 1, hi = g.rig_tail[t], mid;
-    while (lo + 1 < hi) {
-        mid = (lo + hi) >> 1;
-        if (g.tail_r[mid] >= r) hi = mid; else lo = mid;
-    }
-    const int64_t ll = hi;
-    lo = g.lef_tail[t];
-    hi = (int64_t)g.rig_tail[t] + 1;
-    while (lo + 1 < hi) {
-        mid = (lo + hi) >> 1;
-        if (g.tail_r[mid] <= r) lo = mid; else hi = mid;
-    }
-    const int64_t rr = lo;
-    const int64_t tmp = rand_max(s, g.ent_total - (rr - ll + 1));
-    if (tmp < g.tail_h[ll]) return tmp;
-    if (tmp > g.tail_h[rr] - rr + ll - 1) return tmp + rr - ll + 1;
-    lo = ll;
-    hi = rr + 1;
-    while (lo + 1 < hi) {
-        mid = (lo + hi) >> 1;
-        if (g.tail_h[mid] - mid + ll - 1 < tmp) lo = mid; else hi = mid;
-    }
-    return tmp + lo - ll + 1;
+    return tmp + l - lo + 1;
 }
 
 // state of the sampler stream that produces positive b of this call (Base.cpp:200-207 split)
@@ -228,22 +190,39 @@ __device__ __forceinline__ uint64_t positive_state(const uint64_t *states, int64
     return lcg_jump(states[id], (uint64_t)((b - id * per) * dpp));
 }
 
-// negative k of a positive whose stream (after its index draw) is s1: returns the corrupted entity,
-// *tail_side = 1 when the tail was replaced (corrupt_head), 0 when the head was (Base.cpp:219-230)
-__device__ __forceinline__ int64_t draw_negative(const DeviceGraph &g, uint64_t s1, int64_t k, int64_t hp,
-                                                 int64_t rp, int64_t tp, int bern, int filter, int *tail_side) {
-    uint64_t s = lcg_jump(s1, (uint64_t)(2 * k));
-    const float prob = bern ? g.bern_prob[rp] : 500.f;
+struct PosDraw {
+    int64_t h, r, t;
+    int32_t hr_lo, hr_hi, tr_lo, tr_hi;
+    uint64_t s1;   // stream state after the positive's index draw
+};
+
+// positive b: i = rand_max(trainTotal), trainList[i] (Base.cpp:210-215)
+__device__ __forceinline__ PosDraw draw_positive(const DeviceGraph &g, const uint64_t *states, int64_t threads,
+                                                 int64_t bs, int64_t b, int64_t dpp) {
+    uint64_t s = positive_state(states, threads, bs, b, dpp);
+    const int64_t i = rand_max(s, g.train_total);
+    const int4 *p = reinterpret_cast<const int4 *>(g.rec + i);
+    const int4 a = p[0], c = p[1];
+    return PosDraw{a.x, a.y, a.z, a.w, c.x, c.y, c.z, s};
+}
+
+// negative k of a positive (stream offsets 1+2k coin, 2+2k corruption; Base.cpp:217-232): returns the
+// corrupted entity, *tail_side = 1 when the tail was replaced (corrupt_head), 0 when the head was
+__device__ __forceinline__ int64_t draw_negative(const DeviceGraph &g, const PosDraw &p, int64_t k, int bern,
+                                                 int filter, int *tail_side) {
+    uint64_t s = lcg_jump(p.s1, (uint64_t)(2 * k));
+    const float prob = bern ? g.bern_prob[p.r] : 500.f;
+    const int64_t E = g.ent_total;
     if ((float)(lcg_next(s) % 1000ULL) < prob) {
         *tail_side = 1;
-        if (filter) return corrupt_head_filtered(g, hp, rp, s);
-        const int64_t tmp = rand_max(s, g.ent_total - 1);   // skips the passed entity h (Corrupt.h:18-25)
-        return tmp < hp ? tmp : tmp + 1;
+        if (filter) return corrupt_in_run(g.head_t, p.hr_lo, p.hr_hi, E, s);
+        const int64_t tmp = rand_max(s, E - 1);   // skips the passed entity h (Corrupt.h:18-25)
+        return tmp < p.h ? tmp : tmp + 1;
     }
     *tail_side = 0;
-    if (filter) return corrupt_tail_filtered(g, tp, rp, s);
-    const int64_t tmp = rand_max(s, g.ent_total - 1);       // skips t (Corrupt.h:68-74)
-    return tmp < tp ? tmp : tmp + 1;
+    if (filter) return corrupt_in_run(g.tail_h, p.tr_lo, p.tr_hi, E, s);
+    const int64_t tmp = rand_max(s, E - 1);       // skips t (Corrupt.h:68-74)
+    return tmp < p.t ? tmp : tmp + 1;
 }
 
 // sampling() into arrays (one thread per positive); the stream advance is a separate kernel
@@ -252,15 +231,13 @@ __global__ void k_sample(DeviceGraph g, const uint64_t *__restrict__ states, int
                          int64_t *__restrict__ orr, float *__restrict__ oy) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= bs) return;
-    const int64_t dpp = 1 + 2 * neg;
-    uint64_t s = positive_state(states, threads, bs, b, dpp);
-    const int64_t i = rand_max(s, g.train_total);
-    const int64_t hp = g.list_h[i], rp = g.list_r[i], tp = g.list_t[i];
+    const PosDraw pd = draw_positive(g, states, threads, bs, b, 1 + 2 * neg);
+    const int64_t hp = pd.h, rp = pd.r, tp = pd.t;
     oh[b] = hp; ot[b] = tp; orr[b] = rp;
     if (oy) oy[b] = 1.f;
     for (int64_t k = 0; k < neg; ++k) {
         int tail_side;
-        const int64_t e = draw_negative(g, s, k, hp, rp, tp, bern, filter, &tail_side);
+        const int64_t e = draw_negative(g, pd, k, bern, filter, &tail_side);
         const int64_t o = (k + 1) * bs + b;
         oh[o] = tail_side ? hp : e;
         ot[o] = tail_side ? e : tp;
@@ -493,60 +470,185 @@ __device__ __forceinline__ float group_step(const StepParams &P, int64_t hp, int
     return lsum;
 }
 
-template <int MODEL, int G, int VEC, int KCH, bool SAMPLED>
-__global__ __launch_bounds__(256) void k_step(StepParams P, DeviceGraph g, const uint64_t *__restrict__ states,
-                                              int64_t threads, int bern, int filter, const int64_t *__restrict__ bh,
+// General step on an externally given batch (Trainer.train_one_step): any (h, r, t) per slot.
+template <int MODEL, int G, int VEC, int KCH>
+__global__ __launch_bounds__(256) void k_step(StepParams P, const int64_t *__restrict__ bh,
                                               const int64_t *__restrict__ bt, const int64_t *__restrict__ br,
                                               GlobalSink sink, float *__restrict__ loss) {
     constexpr int GPB = 256 / G;
-    extern __shared__ __attribute__((aligned(16))) int64_t s_neg[];   // [GPB][neg] packed (entity<<1 | side)
+    const int lane = threadIdx.x % G;
+    const int64_t bs = P.batch_size, neg = P.neg;
+    const int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    if (b >= bs) return;
+    const int64_t hp = bh[b], tp = bt[b], rp = br[b];
+    const float lsum = group_step<MODEL, G, VEC, KCH>(
+        P, hp, rp, tp, neg,
+        [&](int64_t k, int64_t &h, int64_t &t, int64_t &r) {
+            const int64_t o = (k + 1) * bs + b;
+            h = bh[o]; t = bt[o]; r = br[o];
+        },
+        sink, lane);
+    if (lane == 0 && loss) atomicAdd(loss, lsum * P.inv_count);
+}
+
+// Fused step with in-kernel sampling (the Trainer.run hot loop). One lane group per positive; the
+// group's negatives are drawn lane-parallel into LDS, then EVERY row the group needs is loaded
+// before the first gradient atomic is issued (s_waitcnt vmcnt counts loads and atomics in issue
+// order, so a load behind an atomic would wait for it), NCH negative rows held in registers.
+// Rows use the VEC=1 layout so each atomic wave-instruction covers 64 contiguous floats.
+template <int MODEL, int G, int KCH, int NCH>
+__global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph g, const uint64_t *__restrict__ states,
+                                                      int64_t threads, int bern, int filter, GlobalSink sink,
+                                                      float *__restrict__ loss) {
+    using Vec = V<G, 1, KCH>;
+    constexpr int GPB = 256 / G;
+    extern __shared__ __attribute__((aligned(16))) int64_t s_neg[];   // [GPB][neg] (entity << 1 | tail_side)
     const int lane = threadIdx.x % G;
     const int grp = threadIdx.x / G;
     const int64_t bs = P.batch_size, neg = P.neg;
     const int64_t b = (int64_t)blockIdx.x * GPB + grp;
     const bool active = b < bs;
-    int64_t hp = 0, rp = 0, tp = 0;
-    uint64_t s1 = 0;
-    if constexpr (SAMPLED) {
-        if (active) {
-            uint64_t s = positive_state(states, threads, bs, b, 1 + 2 * neg);
-            const int64_t i = rand_max(s, g.train_total);
-            hp = g.list_h[i]; rp = g.list_r[i]; tp = g.list_t[i];
-            s1 = s;
-            // lane-parallel negative draws (stream offsets 1+2k, 2+2k after the index draw)
-            for (int64_t k = lane; k < neg; k += G) {
-                int side;
-                const int64_t e = draw_negative(g, s1, k, hp, rp, tp, bern, filter, &side);
-                s_neg[grp * neg + k] = (e << 1) | side;
+    PosDraw pd{};
+    if (active) {
+        pd = draw_positive(g, states, threads, bs, b, 1 + 2 * neg);
+        for (int64_t k = lane; k < neg; k += G) {
+            int side;
+            const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
+            s_neg[grp * neg + k] = (e << 1) | side;
+        }
+    }
+    __syncthreads();
+    if (!active) return;
+    const int64_t *mine = s_neg + grp * neg;
+    const int D = (int)P.dim;
+    const int p = P.p_norm;
+    const bool nf = P.norm_flag != 0;
+    const int64_t hp = pd.h, rp = pd.r, tp = pd.t;
+    Vec H, T, Rr, W, nW, hh, th, rh, vpos;
+    vload(H, P.ent + hp * D, D, lane);
+    vload(T, P.ent + tp * D, D, lane);
+    vload(Rr, P.rel + rp * D, D, lane);
+    if constexpr (MODEL == 1) vload(W, P.normv + rp * D, D, lane);
+    Vec E[NCH];
+    auto load_chunk = [&](int64_t c0) {
+#pragma unroll
+        for (int k = 0; k < NCH; ++k)
+            if (c0 + k < neg) vload(E[k], P.ent + (mine[c0 + k] >> 1) * D, D, lane);
+    };
+    load_chunk(0);
+    // ---- positive forward
+    Vec Hs = H, Ts = T;
+    float hn = 0, tn = 0, hdot = 0, tdot = 0;
+    if constexpr (MODEL == 1) {
+        vnormalize(W, nW);
+        hdot = vdot(H, nW);
+        tdot = vdot(T, nW);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            Hs.x[i] = H.x[i] - hdot * nW.x[i];
+            Ts.x[i] = T.x[i] - tdot * nW.x[i];
+        }
+    }
+    if (nf) {
+        hn = vnormalize(Hs, hh);
+        vnormalize(Rr, rh);
+        tn = vnormalize(Ts, th);
+    } else {
+        hh = Hs; rh = Rr; th = Ts;
+    }
+#pragma unroll
+    for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
+    const float ps = vpnorm(vpos, p);
+    Vec aH, aT, aR, aW;
+    vzero(aH); vzero(aT); vzero(aR); vzero(aW);
+    float csum = 0.f, lsum = 0.f;
+    const float m = P.margin, inv = P.inv_count;
+    for (int64_t c0 = 0;;) {
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+            if (c0 + k >= neg) break;
+            const int64_t v = mine[c0 + k];
+            const int64_t e = v >> 1;
+            const bool tail_side = v & 1;
+            Vec Es = E[k], eh, vk;
+            float ed = 0.f, en = 0.f;
+            if constexpr (MODEL == 1) {
+                ed = vdot(E[k], nW);
+#pragma unroll
+                for (int i = 0; i < Vec::N; ++i) Es.x[i] = E[k].x[i] - ed * nW.x[i];
+            }
+            if (nf) en = vnormalize(Es, eh); else eh = Es;
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i)
+                vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - eh.x[i] : (eh.x[i] + rh.x[i]) - th.x[i];
+            const float ns = vpnorm(vk, p);
+            const float a = ps - ns;
+            lsum += a > -m ? a : -m;
+            const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
+            if (c == 0.f) continue;
+            csum += c;
+            Vec gk, gs;
+            vpnorm_bwd(vk, ns, p, -c, gk);
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) {
+                aR.x[i] += gk.x[i];
+                if (tail_side) aH.x[i] += gk.x[i]; else aT.x[i] -= gk.x[i];
+                gs.x[i] = tail_side ? -gk.x[i] : gk.x[i];   // corrupted tail gets -g, corrupted head +g
+            }
+            if constexpr (MODEL == 0) {
+                sink.ent(e, gs, D, lane);
+            } else {
+                Vec gp, ge;
+                if (nf) vnormalize_bwd(Es, en, gs, gp); else gp = gs;
+                const float ng = vdot(nW, gp);
+#pragma unroll
+                for (int i = 0; i < Vec::N; ++i) {
+                    ge.x[i] = gp.x[i] - nW.x[i] * ng;
+                    aW.x[i] -= ed * gp.x[i] + ng * E[k].x[i];
+                }
+                sink.ent(e, ge, D, lane);
             }
         }
-        __syncthreads();
-    } else {
-        if (active) { hp = bh[b]; tp = bt[b]; rp = br[b]; }
+        c0 += NCH;
+        if (c0 >= neg) break;
+        load_chunk(c0);
     }
-    if (!active) return;
-    float lsum;
-    if constexpr (SAMPLED) {
-        const int64_t *mine = s_neg + grp * neg;
-        lsum = group_step<MODEL, G, VEC, KCH>(
-            P, hp, rp, tp, neg,
-            [&](int64_t k, int64_t &h, int64_t &t, int64_t &r) {
-                const int64_t v = mine[k];
-                const int64_t e = v >> 1;
-                if (v & 1) { h = hp; t = e; } else { h = e; t = tp; }
-                r = rp;
-            },
-            sink, lane);
-    } else {
-        lsum = group_step<MODEL, G, VEC, KCH>(
-            P, hp, rp, tp, neg,
-            [&](int64_t k, int64_t &h, int64_t &t, int64_t &r) {
-                const int64_t o = (k + 1) * bs + b;
-                h = bh[o]; t = bt[o]; r = br[o];
-            },
-            sink, lane);
+    // ---- positive backward and the group's on-chip accumulators
+    if (csum != 0.f) {
+        Vec gv;
+        vpnorm_bwd(vpos, ps, p, csum, gv);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            aH.x[i] += gv.x[i];
+            aR.x[i] += gv.x[i];
+            aT.x[i] -= gv.x[i];
+        }
+        sink.rel(rp, aR, D, lane);
+        if constexpr (MODEL == 0) {
+            sink.ent(hp, aH, D, lane);
+            sink.ent(tp, aT, D, lane);
+        } else {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const Vec &acc = s2 == 0 ? aH : aT;
+                const Vec &Ev = s2 == 0 ? H : T;
+                const Vec &Esv = s2 == 0 ? Hs : Ts;
+                const float enn = s2 == 0 ? hn : tn;
+                const float edd = s2 == 0 ? hdot : tdot;
+                Vec gp, ge;
+                if (nf) vnormalize_bwd(Esv, enn, acc, gp); else gp = acc;
+                const float ng = vdot(nW, gp);
+#pragma unroll
+                for (int i = 0; i < Vec::N; ++i) {
+                    ge.x[i] = gp.x[i] - nW.x[i] * ng;
+                    aW.x[i] -= edd * gp.x[i] + ng * Ev.x[i];
+                }
+                sink.ent(s2 == 0 ? hp : tp, ge, D, lane);
+            }
+            sink.norm(rp, aW, D, lane);
+        }
     }
-    if (lane == 0 && loss) atomicAdd(loss, lsum * P.inv_count);
+    if (lane == 0 && loss) atomicAdd(loss, lsum * inv);
 }
 
 // Sparse apply: for every touched row finish the gradient (normalize Jacobian of the pre-step row
@@ -780,14 +882,31 @@ struct Shape {
     int G, VEC, KCH;
 };
 
-Shape pick_shape(int64_t D) {
-    const int VEC = D % 4 == 0 ? 4 : 1;
+Shape pick_shape(int64_t D, bool vec4 = true) {
+    const int VEC = vec4 && D % 4 == 0 ? 4 : 1;
     const int64_t chunks = D / VEC;
     int G = 1;
     while (G < chunks && G < 64) G <<= 1;
     if (G < 2) G = 2;
-    const int KCH = (int)((chunks + G - 1) / G);
+    int KCH = (int)((chunks + G - 1) / G);
+    if (VEC == 1) {   // VEC=1 instantiations exist for power-of-two chunk counts
+        int k = 1;
+        while (k < KCH) k <<= 1;
+        KCH = k;
+    }
     return Shape{G, VEC, KCH};
+}
+
+// negatives held in registers per chunk: smallest of {1,4,8,32} >= neg, at most 128 VGPRs of rows
+int pick_nch(int64_t neg, int kch) {
+    static const int opts[4] = {1, 4, 8, 32};
+    int best = 1;
+    for (int o : opts) {
+        if (o * kch > 128) break;
+        best = o;
+        if (o >= neg) break;
+    }
+    return best;
 }
 
 #define PT_SHAPES(X)                                                                                  \
@@ -795,15 +914,25 @@ Shape pick_shape(int64_t D) {
     X(2, 1, 1) X(4, 1, 1) X(8, 1, 1) X(16, 1, 1) X(32, 1, 1) X(64, 1, 1) X(64, 1, 2) X(64, 1, 4)    \
     X(64, 1, 8)
 
+// VEC=1 shapes x NCH of the sampled step kernel
+#define PT_SSHAPES(X)                                                                                 \
+    X(2, 1, 1) X(2, 1, 4) X(2, 1, 8) X(2, 1, 32) X(4, 1, 1) X(4, 1, 4) X(4, 1, 8) X(4, 1, 32)         \
+    X(8, 1, 1) X(8, 1, 4) X(8, 1, 8) X(8, 1, 32) X(16, 1, 1) X(16, 1, 4) X(16, 1, 8) X(16, 1, 32)     \
+    X(32, 1, 1) X(32, 1, 4) X(32, 1, 8) X(32, 1, 32) X(64, 1, 1) X(64, 1, 4) X(64, 1, 8) X(64, 1, 32) \
+    X(64, 2, 1) X(64, 2, 4) X(64, 2, 8) X(64, 2, 32) X(64, 4, 1) X(64, 4, 4) X(64, 4, 8) X(64, 4, 32) \
+    X(64, 8, 1) X(64, 8, 4) X(64, 8, 8)
+
 }  // namespace
 
 bool shape_supported(int64_t dim) {
     if (dim <= 0) return false;
-    const Shape s = pick_shape(dim);
-#define PT_SUP(g, v, k) if (s.G == g && s.VEC == v && s.KCH == k) return true;
+    bool a = false, b = false;
+    const Shape s = pick_shape(dim), s1 = pick_shape(dim, false);
+#define PT_SUP(g, v, k) if (s.G == g && s.VEC == v && s.KCH == k) a = true; \
+                        if (s1.G == g && s1.VEC == v && s1.KCH == k) b = true;
     PT_SHAPES(PT_SUP)
 #undef PT_SUP
-    return false;
+    return a && b;
 }
 
 hipError_t launch_sample(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
@@ -823,34 +952,41 @@ hipError_t launch_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t
 hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t *states, int64_t threads, int bern,
                        int filter, const int64_t *bh, const int64_t *bt, const int64_t *br, const StepWorkspace &W,
                        float *loss, hipStream_t st) {
-    const Shape s = pick_shape(P.dim);
-    const bool sampled = bh == nullptr;
+    if (P.batch_size <= 0) return hipSuccess;
     dev::GlobalSink sink{W.gent, W.grel, W.gnorm, W.fent, W.frel, W.fnorm};
+    if (bh) {   // external batch
+        const Shape s = pick_shape(P.dim);
+        const int64_t gpb = 256 / s.G;
+        const dim3 grid((unsigned)((P.batch_size + gpb - 1) / gpb)), block(256);
+#define PT_STEP(G_, V_, K_)                                                                                        \
+        if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                                           \
+            if (P.model == 0)                                                                                      \
+                hipLaunchKernelGGL((dev::k_step<0, G_, V_, K_>), grid, block, 0, st, P, bh, bt, br, sink, loss);   \
+            else                                                                                                   \
+                hipLaunchKernelGGL((dev::k_step<1, G_, V_, K_>), grid, block, 0, st, P, bh, bt, br, sink, loss);   \
+            return hipGetLastError();                                                                              \
+        }
+        PT_SHAPES(PT_STEP)
+#undef PT_STEP
+        return hipErrorInvalidValue;
+    }
+    const Shape s = pick_shape(P.dim, false);
+    const int nch = pick_nch(P.neg, s.KCH);
     const int64_t gpb = 256 / s.G;
     const dim3 grid((unsigned)((P.batch_size + gpb - 1) / gpb)), block(256);
-    const size_t lds = sampled ? (size_t)gpb * (size_t)P.neg * sizeof(int64_t) : 0;
-    if (P.batch_size <= 0) return hipSuccess;
-#define PT_STEP(G_, V_, K_)                                                                                        \
-    if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                                               \
-        if (P.model == 0) {                                                                                        \
-            if (sampled)                                                                                           \
-                hipLaunchKernelGGL((dev::k_step<0, G_, V_, K_, true>), grid, block, lds, st, P, g, states, threads, \
-                                   bern, filter, bh, bt, br, sink, loss);                                          \
-            else                                                                                                   \
-                hipLaunchKernelGGL((dev::k_step<0, G_, V_, K_, false>), grid, block, lds, st, P, g, states, threads,\
-                                   bern, filter, bh, bt, br, sink, loss);                                          \
-        } else {                                                                                                   \
-            if (sampled)                                                                                           \
-                hipLaunchKernelGGL((dev::k_step<1, G_, V_, K_, true>), grid, block, lds, st, P, g, states, threads, \
-                                   bern, filter, bh, bt, br, sink, loss);                                          \
-            else                                                                                                   \
-                hipLaunchKernelGGL((dev::k_step<1, G_, V_, K_, false>), grid, block, lds, st, P, g, states, threads,\
-                                   bern, filter, bh, bt, br, sink, loss);                                          \
-        }                                                                                                          \
-        return hipGetLastError();                                                                                  \
+    const size_t lds = (size_t)gpb * (size_t)P.neg * sizeof(int64_t);
+#define PT_SSTEP(G_, K_, N_)                                                                                      \
+    if (s.G == G_ && s.KCH == K_ && nch == N_) {                                                                \
+        if (P.model == 0)                                                                                         \
+            hipLaunchKernelGGL((dev::k_step_sampled<0, G_, K_, N_>), grid, block, lds, st, P, g, states, threads,  \
+                               bern, filter, sink, loss);                                                         \
+        else                                                                                                      \
+            hipLaunchKernelGGL((dev::k_step_sampled<1, G_, K_, N_>), grid, block, lds, st, P, g, states, threads,  \
+                               bern, filter, sink, loss);                                                         \
+        return hipGetLastError();                                                                                 \
     }
-    PT_SHAPES(PT_STEP)
-#undef PT_STEP
+    PT_SSHAPES(PT_SSTEP)
+#undef PT_SSTEP
     return hipErrorInvalidValue;
 }
 
