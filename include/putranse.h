@@ -94,10 +94,13 @@ int pt_trainer_step(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg,
 int pt_trainer_run(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
                    int64_t steps, float *d_losses, void *stream);
 
-/* Measurement hook: one in-kernel-sampled step with HIP events around its two kernels (the fused
- * forward/backward `k_step` and the sparse optimizer `k_apply`) on `stream`; synchronizes. */
-int pt_trainer_step_timed(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
-                          float *d_loss, float *ms_step, float *ms_apply, void *stream);
+/* Measurement hook: `steps` in-kernel-sampled steps launched one by one (no graph) with an event pair
+ * around every launch on `stream`. ms4[k] = total duration of kernel kind k divided by `steps`:
+ * 0 batch sampling (k_sample_csr, large-neg path only, one launch per chunk of steps), 1 bucket scan
+ * (k_scan_counts, idem), 2 fused forward/backward (k_step_sampled), 3 sparse optimizer (k_apply).
+ * Synchronizes the stream. */
+int pt_trainer_run_timed(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
+                         int64_t steps, float *d_losses, float *ms4, void *stream);
 
 /* ------------------------------------------------------------------ scoring ------------------ */
 /* scores = ||h + r - t||_p as model.predict computes them (TransE.py:46-74, TransH.py:52-93):

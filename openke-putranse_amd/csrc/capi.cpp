@@ -56,6 +56,11 @@ struct pt_trainer {
     pt::StepParams P{};
     pt::StepWorkspace W{};
     void *ws_block = nullptr;
+    // counting-sort gradient path for large neg (allocated on first use, grown as needed)
+    void *csr_block = nullptr;
+    size_t csr_cap = 0;
+    pt::CsrWork csr{};
+    int64_t csr_bs = 0, csr_neg = 0, csr_chunk = 0;   // layout the workspace was carved for
     int device = -1;
     hipStream_t cap = nullptr;
     std::map<GraphKey, hipGraphExec_t> graphs;
@@ -67,6 +72,7 @@ struct pt_trainer {
         drop_graphs();
         if (cap) (void)hipStreamDestroy(cap);
         if (ws_block) (void)hipFree(ws_block);
+        if (csr_block) (void)hipFree(csr_block);
     }
 };
 
@@ -237,19 +243,139 @@ extern "C" int pt_trainer_update_desc(pt_trainer *t, const pt_model_desc *m) {
     return PT_OK;
 }
 
-static int enqueue_step(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
-                        const int64_t *bh, const int64_t *bt, const int64_t *br, float *d_loss, hipStream_t st) {
+// negatives at or above this count take the counting-sort path (PT_CSR=0/1 overrides)
+static bool use_csr(int64_t neg) {
+    static int forced = [] {
+        const char *v = getenv("PT_CSR");
+        return v ? atoi(v) : -1;
+    }();
+    return forced >= 0 ? forced != 0 : neg >= 4;
+}
+
+static const int64_t kCsrChunk = 256;   // steps pre-sampled per sampling/scan launch pair
+
+// Workspace of the counting-sort path, carved once per (bs, neg): room for a chunk of pre-sampled
+// steps (<= kCsrChunk, fewer when a step's arrays are large) plus one step's gradient rows. A new
+// (bs, neg) re-carves it (and drops captured graphs, whose kernels hold the old pointers).
+static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
+    if (t->csr_block && t->csr_bs == bs && t->csr_neg == neg) return PT_OK;
+    const int64_t E = t->P.ent_total, D = t->P.dim;
+    const int64_t cs = (E + 3) & ~int64_t(3), ss = (E + 4) & ~int64_t(3);
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t per_call = 16 * bs + 8 * bs * neg + 4 * cs + 4 * ss + 1024;
+    int64_t chunk = (int64_t)std::max<size_t>(1, ((size_t)512 << 20) / per_call);
+    chunk = std::min(chunk, kCsrChunk);
+    const size_t a_pos = al(16 * bs * chunk), a_neg = al(4 * bs * neg * chunk), a_off = a_neg,
+                 a_cnt = al(4 * cs * chunk), a_start = al(4 * ss * chunk), a_con = al(4 * bs * neg * D);
+    const size_t need = a_pos + a_neg + a_off + a_cnt + a_start + a_con;
+    PT_HIP(hipDeviceSynchronize());   // queued work may still use the old carving
+    t->drop_graphs();
+    if (need > t->csr_cap) {
+        if (t->csr_block) (void)hipFree(t->csr_block);
+        t->csr_block = nullptr;
+        t->csr_cap = 0;
+        PT_HIP(hipMalloc(&t->csr_block, need));
+        t->csr_cap = need;
+    }
+    PT_HIP(hipMemset(t->csr_block, 0, need));   // bucket counts start at zero; the scan re-zeroes them
+    char *b = (char *)t->csr_block;
+    t->csr.pos = (int4 *)b; b += a_pos;
+    t->csr.neg = (int32_t *)b; b += a_neg;
+    t->csr.off = (int32_t *)b; b += a_off;
+    t->csr.cnt = (int32_t *)b; b += a_cnt;
+    t->csr.start = (int32_t *)b; b += a_start;
+    t->csr.contrib = (float *)b;
+    t->csr.cnt_stride = cs;
+    t->csr.start_stride = ss;
+    t->csr_bs = bs;
+    t->csr_neg = neg;
+    t->csr_chunk = chunk;
+    return PT_OK;
+}
+
+// Launch recorder for the measurement hook: an event pair around every launch, by kernel kind
+// (0 sampling, 1 bucket scan, 2 forward/backward, 3 optimizer apply).
+struct Timing {
+    std::vector<std::tuple<int, hipEvent_t, hipEvent_t>> ev;
+    int begin(int kind, hipStream_t st, hipEvent_t *a) {
+        PT_HIP(hipEventCreate(a));
+        PT_HIP(hipEventRecord(*a, st));
+        ev.emplace_back(kind, *a, nullptr);
+        return PT_OK;
+    }
+    int end(hipStream_t st) {
+        hipEvent_t b;
+        PT_HIP(hipEventCreate(&b));
+        PT_HIP(hipEventRecord(b, st));
+        std::get<2>(ev.back()) = b;
+        return PT_OK;
+    }
+};
+
+#define PT_TIMED(kind, call)                                  \
+    do {                                                      \
+        hipEvent_t a_;                                        \
+        if (tm && tm->begin(kind, st, &a_)) return PT_EHIP;   \
+        PT_HIP(call);                                         \
+        if (tm && tm->end(st)) return PT_EHIP;                \
+    } while (0)
+
+// Enqueue `steps` in-kernel-sampled steps; step i adds its loss to d_losses[i]. Large neg takes the
+// counting-sort path: one sampling + one scan launch per chunk of up to kCsrChunk steps (the batch
+// stream does not depend on the tables, so it is drawn ahead), then k_step + k_apply per step.
+static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
+                       int64_t steps, float *d_losses, hipStream_t st, Timing *tm = nullptr) {
     pt::StepParams P = t->P;
     P.batch_size = bs;
     P.neg = neg;
     P.inv_count = 1.0f / (float)(bs * neg);
-    const bool sampled = bh == nullptr;
-    pt::DeviceGraph dg{};
-    if (sampled) dg = s->g->dev;
-    PT_HIP(pt::launch_step(P, dg, sampled ? s->d_states : nullptr, sampled ? s->threads : 0, (int)bern, (int)filter,
-                           bh, bt, br, t->W, d_loss, st));
-    PT_HIP(pt::launch_apply(P, t->W, sampled ? s->d_states : nullptr, sampled ? s->threads : 0, bs, 1 + 2 * neg,
-                            d_loss, st));
+    const int64_t dpp = 1 + 2 * neg;
+    const pt::DeviceGraph dg = s->g->dev;
+    if (use_csr(neg)) {
+        PT_CHECK(t->csr_block, PT_ESTATE, "counting-sort workspace not allocated");
+        const int64_t chunk = t->csr_chunk;
+        for (int64_t c0 = 0; c0 < steps; c0 += chunk) {
+            const int64_t calls = std::min(chunk, steps - c0);
+            PT_TIMED(0, pt::launch_sample_csr(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls,
+                                              t->csr, st));
+            PT_TIMED(1, pt::launch_scan_counts(t->csr, P.ent_total, calls, s->d_states, s->threads, bs, dpp, st));
+            for (int64_t j = 0; j < calls; ++j) {
+                const pt::CsrWork v = pt::csr_view(t->csr, j, bs, neg);
+                float *loss = d_losses ? d_losses + c0 + j : nullptr;
+                PT_TIMED(2, pt::launch_step(P, dg, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr,
+                                            nullptr, t->W, loss, st, &v));
+                PT_TIMED(3, pt::launch_apply(P, t->W, nullptr, 0, bs, dpp, loss, st, &v));
+            }
+        }
+    } else {
+        for (int64_t i = 0; i < steps; ++i) {
+            float *loss = d_losses ? d_losses + i : nullptr;
+            PT_TIMED(2, pt::launch_step(P, dg, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr,
+                                        nullptr, t->W, loss, st));
+            PT_TIMED(3, pt::launch_apply(P, t->W, s->d_states, s->threads, bs, dpp, loss, st));
+        }
+    }
+    return PT_OK;
+}
+
+static int enqueue_external(pt_trainer *t, int64_t bs, int64_t neg, const int64_t *bh, const int64_t *bt,
+                            const int64_t *br, float *d_loss, hipStream_t st) {
+    pt::StepParams P = t->P;
+    P.batch_size = bs;
+    P.neg = neg;
+    P.inv_count = 1.0f / (float)(bs * neg);
+    PT_HIP(pt::launch_step(P, pt::DeviceGraph{}, nullptr, 0, 0, 0, bh, bt, br, t->W, d_loss, st));
+    PT_HIP(pt::launch_apply(P, t->W, nullptr, 0, bs, 1 + 2 * neg, d_loss, st));
+    return PT_OK;
+}
+
+static int prepare_sampled(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t steps) {
+    int rc = check_step_args(t->P, s, bs, neg, nullptr);
+    if (rc) return rc;
+    rc = s->g->upload();
+    if (rc) return rc;
+    (void)steps;
+    if (use_csr(neg)) return ensure_csr(t, bs, neg);
     return PT_OK;
 }
 
@@ -257,43 +383,38 @@ extern "C" int pt_trainer_step(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t
                                const int64_t *d_bh, const int64_t *d_bt, const int64_t *d_br, float *d_loss,
                                void *stream) {
     PT_CHECK(t, PT_EINVAL, "null trainer");
-    int rc = check_step_args(t->P, s, bs, neg, d_bh);
-    if (rc) return rc;
-    if (!d_bh) {
-        rc = s->g->upload();
-        if (rc) return rc;
-    } else {
+    if (d_bh) {
         PT_CHECK(d_bt && d_br, PT_EINVAL, "external batch needs h, t and r arrays");
+        PT_CHECK(bs > 0 && neg > 0, PT_EINVAL, "batch_size and neg_ent must be positive");
+        return enqueue_external(t, bs, neg, d_bh, d_bt, d_br, d_loss, (hipStream_t)stream);
     }
-    return enqueue_step(t, s, bs, neg, bern, filter, d_bh, d_bt, d_br, d_loss, (hipStream_t)stream);
+    int rc = prepare_sampled(t, s, bs, neg, 1);
+    if (rc) return rc;
+    return enqueue_run(t, s, bs, neg, bern, filter, 1, d_loss, (hipStream_t)stream);
 }
 
-// One in-kernel-sampled step with HIP events around each of its two kernels on `stream` (measurement
-// hook for bench.py's roofline: the average k_step / k_apply durations). Synchronizes the stream.
-extern "C" int pt_trainer_step_timed(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern,
-                                     int64_t filter, float *d_loss, float *ms_step, float *ms_apply, void *stream) {
-    PT_CHECK(t && ms_step && ms_apply, PT_EINVAL, "pt_trainer_step_timed: null argument");
-    int rc = check_step_args(t->P, s, bs, neg, nullptr);
-    if (rc) return rc;
-    rc = s->g->upload();
+// `steps` in-kernel-sampled steps launched one by one with an event pair around every launch on
+// `stream` (measurement hook for bench.py's roofline). ms4[k] = total duration of kernel kind k
+// (0 sampling, 1 bucket scan, 2 forward/backward, 3 optimizer) divided by `steps`. Synchronizes.
+extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern,
+                                    int64_t filter, int64_t steps, float *d_losses, float *ms4, void *stream) {
+    PT_CHECK(t && ms4 && steps > 0, PT_EINVAL, "pt_trainer_run_timed: bad argument");
+    int rc = prepare_sampled(t, s, bs, neg, steps);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    hipEvent_t ev[3];
-    for (auto &e : ev) PT_HIP(hipEventCreate(&e));
-    pt::StepParams P = t->P;
-    P.batch_size = bs;
-    P.neg = neg;
-    P.inv_count = 1.0f / (float)(bs * neg);
-    PT_HIP(hipEventRecord(ev[0], st));
-    PT_HIP(pt::launch_step(P, s->g->dev, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr, nullptr,
-                           t->W, d_loss, st));
-    PT_HIP(hipEventRecord(ev[1], st));
-    PT_HIP(pt::launch_apply(P, t->W, s->d_states, s->threads, bs, 1 + 2 * neg, d_loss, st));
-    PT_HIP(hipEventRecord(ev[2], st));
-    PT_HIP(hipEventSynchronize(ev[2]));
-    PT_HIP(hipEventElapsedTime(ms_step, ev[0], ev[1]));
-    PT_HIP(hipEventElapsedTime(ms_apply, ev[1], ev[2]));
-    for (auto &e : ev) (void)hipEventDestroy(e);
+    Timing tm;
+    rc = enqueue_run(t, s, bs, neg, bern, filter, steps, d_losses, st, &tm);
+    if (rc) return rc;
+    PT_HIP(hipStreamSynchronize(st));
+    double tot[4] = {0, 0, 0, 0};
+    for (auto &e : tm.ev) {
+        float ms = 0;
+        PT_HIP(hipEventElapsedTime(&ms, std::get<1>(e), std::get<2>(e)));
+        tot[std::get<0>(e)] += ms;
+        (void)hipEventDestroy(std::get<1>(e));
+        (void)hipEventDestroy(std::get<2>(e));
+    }
+    for (int k = 0; k < 4; ++k) ms4[k] = (float)(tot[k] / (double)steps);
     return PT_OK;
 }
 
@@ -301,9 +422,7 @@ extern "C" int pt_trainer_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t 
                               int64_t steps, float *d_losses, void *stream) {
     PT_CHECK(t && d_losses, PT_EINVAL, "pt_trainer_run: null argument");
     PT_CHECK(steps > 0, PT_EINVAL, "steps must be positive");
-    int rc = check_step_args(t->P, s, bs, neg, nullptr);
-    if (rc) return rc;
-    rc = s->g->upload();
+    int rc = prepare_sampled(t, s, bs, neg, steps);
     if (rc) return rc;
     GraphKey key{s, s->g->dev.rec, d_losses, s->d_states, bs, neg, bern, filter, steps};
     auto it = t->graphs.find(key);
@@ -312,8 +431,7 @@ extern "C" int pt_trainer_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t 
         PT_HIP(hipStreamBeginCapture(t->cap, hipStreamCaptureModeThreadLocal));
         int erc = PT_OK;
         if (hipMemsetAsync(d_losses, 0, sizeof(float) * (size_t)steps, t->cap) != hipSuccess) erc = PT_EHIP;
-        for (int64_t i = 0; i < steps && !erc; ++i)
-            erc = enqueue_step(t, s, bs, neg, bern, filter, nullptr, nullptr, nullptr, d_losses + i, t->cap);
+        if (!erc) erc = enqueue_run(t, s, bs, neg, bern, filter, steps, d_losses, t->cap);
         hipError_t ce = hipStreamEndCapture(t->cap, &graph);
         if (erc) return erc;
         PT_HIP(ce);

@@ -23,6 +23,29 @@ struct StepWorkspace {
     int *fent = nullptr, *frel = nullptr, *fnorm = nullptr;      // touched-row flags
 };
 
+// Workspace of the counting-sort (CSR) gradient path for large neg (see k_sample_csr). The sampling
+// and scan passes fill `calls` consecutive steps at once (pos/neg/off/cnt/start are [calls][...]);
+// a per-step view (csr_view) offsets the pointers to one step.
+struct CsrWork {
+    int4 *pos = nullptr;        // [calls][bs] (h, r, t, -)
+    int32_t *neg = nullptr;     // [calls][bs*neg] entity << 1 | tail_side
+    int32_t *off = nullptr;     // [calls][bs*neg] rank inside the entity's bucket
+    int32_t *cnt = nullptr;     // [calls][cnt_stride] bucket sizes (zero between uses)
+    int32_t *start = nullptr;   // [calls][start_stride] exclusive prefix of cnt (E+1 used)
+    float *contrib = nullptr;   // [bs*neg][dim] gradient rows of the corrupted entities (one step)
+    int64_t cnt_stride = 0, start_stride = 0;
+};
+
+inline CsrWork csr_view(const CsrWork &w, int64_t call, int64_t bs, int64_t neg) {
+    CsrWork v = w;
+    v.pos = w.pos + call * bs;
+    v.neg = w.neg + call * bs * neg;
+    v.off = w.off + call * bs * neg;
+    v.cnt = w.cnt + call * w.cnt_stride;
+    v.start = w.start + call * w.start_stride;
+    return v;
+}
+
 struct LpUniverseDev {
     const float *ent, *rel, *normv;
     const int64_t *remap;   // local -> global entity
@@ -37,11 +60,15 @@ bool shape_supported(int64_t dim);
 hipError_t launch_sample(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                          int bern, int filter, int64_t *h, int64_t *t, int64_t *r, float *y, hipStream_t st);
 hipError_t launch_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t dpp, hipStream_t st);
+hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
+                             int bern, int filter, int64_t calls, const CsrWork &w, hipStream_t st);
+hipError_t launch_scan_counts(const CsrWork &w, int64_t n, int64_t calls, uint64_t *states, int64_t threads,
+                              int64_t bs, int64_t dpp, hipStream_t st);
 hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t *states, int64_t threads, int bern,
                        int filter, const int64_t *bh, const int64_t *bt, const int64_t *br, const StepWorkspace &W,
-                       float *loss, hipStream_t st);
+                       float *loss, hipStream_t st, const CsrWork *csr = nullptr);
 hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *states, int64_t threads, int64_t bs,
-                        int64_t dpp, float *loss, hipStream_t st);
+                        int64_t dpp, float *loss, hipStream_t st, const CsrWork *csr = nullptr);
 hipError_t launch_score(const StepParams &P, int mode, const int64_t *h, const int64_t *t, const int64_t *r, int64_t n,
                         float *out, hipStream_t st);
 hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh, const int64_t *qt, const int64_t *qr,

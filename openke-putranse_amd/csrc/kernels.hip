@@ -27,10 +27,30 @@ namespace dev {
 constexpr float kEps = 1e-12f;   // F.normalize eps
 
 // ---------------------------------------------------------------- lane-group vectors -----------
+// All-reduce sum over an aligned group of G lanes, entirely on the VALU: DPP within 16-lane rows
+// (quad_perm xor1, xor2, row_half_mirror, row_mirror), then v_permlane16_swap / v_permlane32_swap
+// across rows (gfx950). Every lane of the group ends with the same value (each step adds a value and
+// its partner's, a commutative pair), which keeps group-uniform branches uniform.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 template <int G>
 __device__ __forceinline__ float gsum(float v) {
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, G);
+    if constexpr (G >= 2) v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+    if constexpr (G >= 4) v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) v += dpp_f<0x141>(v);   // row_half_mirror
+    if constexpr (G >= 16) v += dpp_f<0x140>(v);  // row_mirror
+    if constexpr (G >= 32) {
+        const unsigned x = __float_as_uint(v);
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    if constexpr (G >= 64) {
+        const unsigned x = __float_as_uint(v);
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
     return v;
 }
 
@@ -115,9 +135,9 @@ __device__ __forceinline__ bool vnonzero(const V<G, VEC, KCH> &a) {
 template <int G, int VEC, int KCH>
 __device__ __forceinline__ float vnormalize(const V<G, VEC, KCH> &x, V<G, VEC, KCH> &out) {
     const float n = sqrtf(vdot(x, x));
-    const float den = n > kEps ? n : kEps;
+    const float inv = 1.0f / (n > kEps ? n : kEps);   // one division per row, then multiplies
 #pragma unroll
-    for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = x.x[i] / den;
+    for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = x.x[i] * inv;
     return n;
 }
 
@@ -126,9 +146,10 @@ template <int G, int VEC, int KCH>
 __device__ __forceinline__ void vnormalize_bwd(const V<G, VEC, KCH> &x, float n, const V<G, VEC, KCH> &g,
                                                V<G, VEC, KCH> &out) {
     if (n > kEps) {
-        const float c = vdot(g, x) / (n * n);
+        const float inv = 1.0f / n;
+        const float c = vdot(g, x) * (inv * inv);
 #pragma unroll
-        for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = (g.x[i] - x.x[i] * c) / n;
+        for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = (g.x[i] - x.x[i] * c) * inv;
     } else {
 #pragma unroll
         for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = g.x[i] / kEps;
@@ -182,12 +203,15 @@ __device__ __forceinline__ int64_t corrupt_in_run(const int32_t *__restrict__ va
     return tmp + l - lo + 1;
 }
 
-// state of the sampler stream that produces positive b of this call (Base.cpp:200-207 split)
+// state of the sampler stream that produces positive b of call `call` after the current states
+// (Base.cpp:200-207 split: thread id owns positives [id*per, min((id+1)*per, bs)) of every call)
 __device__ __forceinline__ uint64_t positive_state(const uint64_t *states, int64_t threads, int64_t bs, int64_t b,
-                                                   int64_t dpp) {
+                                                   int64_t dpp, int64_t call = 0) {
     const int64_t per = bs % threads == 0 ? bs / threads : bs / threads + 1;
     const int64_t id = b / per;
-    return lcg_jump(states[id], (uint64_t)((b - id * per) * dpp));
+    int64_t len = bs - id * per;
+    len = len > per ? per : len;
+    return lcg_jump(states[id], (uint64_t)((call * len + (b - id * per)) * dpp));
 }
 
 struct PosDraw {
@@ -198,8 +222,8 @@ struct PosDraw {
 
 // positive b: i = rand_max(trainTotal), trainList[i] (Base.cpp:210-215)
 __device__ __forceinline__ PosDraw draw_positive(const DeviceGraph &g, const uint64_t *states, int64_t threads,
-                                                 int64_t bs, int64_t b, int64_t dpp) {
-    uint64_t s = positive_state(states, threads, bs, b, dpp);
+                                                 int64_t bs, int64_t b, int64_t dpp, int64_t call = 0) {
+    uint64_t s = positive_state(states, threads, bs, b, dpp, call);
     const int64_t i = rand_max(s, g.train_total);
     const int4 *p = reinterpret_cast<const int4 *>(g.rec + i);
     const int4 a = p[0], c = p[1];
@@ -257,6 +281,108 @@ __device__ __forceinline__ void advance_states(uint64_t *states, int64_t threads
 
 __global__ void k_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t dpp) {
     advance_states(states, threads, bs, dpp, (int)threadIdx.x);
+}
+
+// Counting-sort (CSR) sampling pass of the large-negative path: one thread per (positive, negative)
+// slot draws exactly what getBatch draws for it (stream jump to the slot) and reserves the slot's
+// place in its corrupted entity's bucket. Thread k == neg of a positive records the positive.
+using pt::CsrWork;
+
+__global__ __launch_bounds__(256) void k_sample_csr(DeviceGraph g, const uint64_t *__restrict__ states,
+                                                    int64_t threads, int64_t bs, int64_t neg, int bern, int filter,
+                                                    int64_t calls, CsrWork w) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_call = bs * (neg + 1);
+    if (idx >= calls * per_call) return;
+    const int64_t call = idx / per_call, rem = idx - call * per_call;
+    const int64_t b = rem / (neg + 1), k = rem - b * (neg + 1);
+    const PosDraw pd = draw_positive(g, states, threads, bs, b, 1 + 2 * neg, call);
+    if (k == neg) {
+        w.pos[call * bs + b] = make_int4((int)pd.h, (int)pd.r, (int)pd.t, 0);
+        return;
+    }
+    int side;
+    const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
+    const int64_t o = call * bs * neg + b * neg + k;
+    w.neg[o] = (int32_t)((e << 1) | side);
+    w.off[o] = atomicAdd(&w.cnt[call * w.cnt_stride + e], 1);
+}
+
+// exclusive scan of the bucket sizes (one workgroup of 1024 threads, tiles of 16384 counts: 16
+// contiguous counts per thread, wave shuffles for the thread totals, LDS for the 16 wave totals),
+// zeroing the counts for the next step; also advances the sampler streams by this call's draws
+// (the sampling pass was their only reader)
+__global__ __launch_bounds__(1024) void k_scan_counts(int32_t *__restrict__ cnt_all, int32_t *__restrict__ start_all,
+                                                      int64_t n, uint64_t *states, int64_t threads, int64_t bs,
+                                                      int64_t dpp) {
+    __shared__ int32_t wtot[16];
+    __shared__ int32_t carry_s;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // one workgroup per sampled call; workgroup 0 advances the streams by all the calls' draws
+    int32_t *cnt = cnt_all + (int64_t)blockIdx.x * ((n + 3) & ~int64_t(3));        // rows padded to 16 B
+    int32_t *start = start_all + (int64_t)blockIdx.x * ((n + 4) & ~int64_t(3));
+    if (blockIdx.x == 0 && tid < 64 && states) advance_states(states, threads, bs, dpp * (int64_t)gridDim.x, tid);
+    if (tid == 0) carry_s = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < n; base += 16384) {
+        const int64_t lo = base + (int64_t)tid * 16;
+        int32_t v[16];
+        if (lo + 16 <= n) {
+            const int4 *p4 = reinterpret_cast<const int4 *>(cnt + lo);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int4 x = p4[q];
+                v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = lo + q < n ? cnt[lo + q] : 0;
+        }
+        int32_t tsum = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) tsum += v[q];
+        int32_t incl = tsum;   // inclusive wave scan of the thread totals
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wtot[wid] = incl;
+        __syncthreads();
+        int32_t wpre = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            const int32_t t = wtot[w];
+            wpre += w < wid ? t : 0;
+            total += t;
+        }
+        int32_t run = carry_s + wpre + incl - tsum;
+        if (lo + 16 <= n) {
+            int32_t o[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                o[q] = run;
+                run += v[q];
+            }
+            int4 *s4 = reinterpret_cast<int4 *>(start + lo);
+            int4 *c4 = reinterpret_cast<int4 *>(cnt + lo);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                s4[q] = make_int4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+                c4[q] = make_int4(0, 0, 0, 0);
+            }
+        } else {
+            for (int q = 0; q < 16 && lo + q < n; ++q) {
+                start[lo + q] = run;
+                run += v[q];
+                cnt[lo + q] = 0;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) carry_s += total;
+        __syncthreads();
+    }
+    if (tid == 0) start[n] = carry_s;
 }
 
 // ---------------------------------------------------------------- fused step -----------------
@@ -491,128 +617,202 @@ __global__ __launch_bounds__(256) void k_step(StepParams P, const int64_t *__res
     if (lane == 0 && loss) atomicAdd(loss, lsum * P.inv_count);
 }
 
-// Fused step with in-kernel sampling (the Trainer.run hot loop). One lane group per positive; the
-// group's negatives are drawn lane-parallel into LDS, then EVERY row the group needs is loaded
-// before the first gradient atomic is issued (s_waitcnt vmcnt counts loads and atomics in issue
-// order, so a load behind an atomic would wait for it), NCH negative rows held in registers.
-// Rows use the VEC=1 layout so each atomic wave-instruction covers 64 contiguous floats.
-template <int MODEL, int G, int KCH, int NCH>
+// Fused step with in-kernel sampling (the Trainer.run hot loop).
+//
+// A positive is owned by S lane groups ("sub-groups"); sub-group s takes negatives
+// [s*nper, min(neg, (s+1)*nper)). Each sub-group draws its negatives lane-parallel into LDS, then
+// loads EVERY row it needs before its first gradient store/atomic (s_waitcnt vmcnt counts loads,
+// stores and atomics in issue order, so a load queued behind an atomic would wait for it), keeping up
+// to NCH negative rows in registers. The positive's forward is recomputed by every sub-group (its
+// rows are L1/L2 hits); the positive-row gradient partials meet in LDS and sub-group 0 finishes them.
+// Rows use the VEC=1 layout, so each atomic/store wave-instruction covers 64 contiguous floats.
+//
+// CSR = true: the batch was drawn by k_sample_csr; the corrupted entities' gradient rows are written
+// with plain stores to their counting-sort slots (contrib) instead of float atomics.
+template <int MODEL, int G, int KCH, int NCH, int S, bool CSR>
 __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph g, const uint64_t *__restrict__ states,
                                                       int64_t threads, int bern, int filter, GlobalSink sink,
-                                                      float *__restrict__ loss) {
+                                                      float *__restrict__ loss, CsrWork cw) {
     using Vec = V<G, 1, KCH>;
-    constexpr int GPB = 256 / G;
-    extern __shared__ __attribute__((aligned(16))) int64_t s_neg[];   // [GPB][neg] (entity << 1 | tail_side)
+    constexpr int GPB = 256 / G;      // lane groups per block
+    constexpr int PPB = GPB / S;      // positives per block
+    constexpr int RW = KCH * G;       // floats per row slot in the reduction area
+    // LDS: s_neg[PPB*neg] (entity << 1 | tail_side) [, s_dst[PPB*neg]] , then red[GPB][4][RW] + cs[GPB][2]
+    extern __shared__ __attribute__((aligned(16))) int64_t s_neg[];
     const int lane = threadIdx.x % G;
     const int grp = threadIdx.x / G;
+    const int pl = grp / S;            // positive slot in the block
+    const int sub = grp % S;
     const int64_t bs = P.batch_size, neg = P.neg;
-    const int64_t b = (int64_t)blockIdx.x * GPB + grp;
+    const int64_t b = (int64_t)blockIdx.x * PPB + pl;
     const bool active = b < bs;
+    const int64_t nper = (neg + S - 1) / S;
+    const int64_t k_lo = sub * nper < neg ? sub * nper : neg;
+    const int64_t k_hi = k_lo + nper < neg ? k_lo + nper : neg;
+    int64_t *s_dst = s_neg + PPB * neg;
+    float *red = reinterpret_cast<float *>(s_neg + PPB * neg * (CSR ? 2 : 1));
+    float *cs = red + GPB * 4 * RW;
     PosDraw pd{};
     if (active) {
-        pd = draw_positive(g, states, threads, bs, b, 1 + 2 * neg);
-        for (int64_t k = lane; k < neg; k += G) {
-            int side;
-            const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
-            s_neg[grp * neg + k] = (e << 1) | side;
+        if constexpr (!CSR) {
+            pd = draw_positive(g, states, threads, bs, b, 1 + 2 * neg);
+            for (int64_t k = k_lo + lane; k < k_hi; k += G) {
+                int side;
+                const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
+                s_neg[pl * neg + k] = (e << 1) | side;
+            }
+        } else {
+            const int4 q = cw.pos[b];
+            pd.h = q.x; pd.r = q.y; pd.t = q.z;
+            for (int64_t k = k_lo + lane; k < k_hi; k += G) {
+                const int64_t v = cw.neg[b * neg + k];
+                s_neg[pl * neg + k] = v;
+                s_dst[pl * neg + k] = (int64_t)cw.start[v >> 1] + cw.off[b * neg + k];
+            }
         }
     }
     __syncthreads();
-    if (!active) return;
-    const int64_t *mine = s_neg + grp * neg;
     const int D = (int)P.dim;
     const int p = P.p_norm;
     const bool nf = P.norm_flag != 0;
     const int64_t hp = pd.h, rp = pd.r, tp = pd.t;
+    const int64_t *mine = s_neg + pl * neg;
     Vec H, T, Rr, W, nW, hh, th, rh, vpos;
-    vload(H, P.ent + hp * D, D, lane);
-    vload(T, P.ent + tp * D, D, lane);
-    vload(Rr, P.rel + rp * D, D, lane);
-    if constexpr (MODEL == 1) vload(W, P.normv + rp * D, D, lane);
     Vec E[NCH];
-    auto load_chunk = [&](int64_t c0) {
-#pragma unroll
-        for (int k = 0; k < NCH; ++k)
-            if (c0 + k < neg) vload(E[k], P.ent + (mine[c0 + k] >> 1) * D, D, lane);
-    };
-    load_chunk(0);
-    // ---- positive forward
-    Vec Hs = H, Ts = T;
-    float hn = 0, tn = 0, hdot = 0, tdot = 0;
-    if constexpr (MODEL == 1) {
-        vnormalize(W, nW);
-        hdot = vdot(H, nW);
-        tdot = vdot(T, nW);
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            Hs.x[i] = H.x[i] - hdot * nW.x[i];
-            Ts.x[i] = T.x[i] - tdot * nW.x[i];
-        }
-    }
-    if (nf) {
-        hn = vnormalize(Hs, hh);
-        vnormalize(Rr, rh);
-        tn = vnormalize(Ts, th);
-    } else {
-        hh = Hs; rh = Rr; th = Ts;
-    }
-#pragma unroll
-    for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
-    const float ps = vpnorm(vpos, p);
     Vec aH, aT, aR, aW;
     vzero(aH); vzero(aT); vzero(aR); vzero(aW);
     float csum = 0.f, lsum = 0.f;
-    const float m = P.margin, inv = P.inv_count;
-    for (int64_t c0 = 0;;) {
+    Vec Hs, Ts;
+    float hn = 0, tn = 0, hdot = 0, tdot = 0, ps = 0;
+    if (active) {
+        vload(H, P.ent + hp * D, D, lane);
+        vload(T, P.ent + tp * D, D, lane);
+        vload(Rr, P.rel + rp * D, D, lane);
+        if constexpr (MODEL == 1) vload(W, P.normv + rp * D, D, lane);
+        auto load_chunk = [&](int64_t c0) {
 #pragma unroll
-        for (int k = 0; k < NCH; ++k) {
-            if (c0 + k >= neg) break;
-            const int64_t v = mine[c0 + k];
-            const int64_t e = v >> 1;
-            const bool tail_side = v & 1;
-            Vec Es = E[k], eh, vk;
-            float ed = 0.f, en = 0.f;
-            if constexpr (MODEL == 1) {
-                ed = vdot(E[k], nW);
-#pragma unroll
-                for (int i = 0; i < Vec::N; ++i) Es.x[i] = E[k].x[i] - ed * nW.x[i];
-            }
-            if (nf) en = vnormalize(Es, eh); else eh = Es;
-#pragma unroll
-            for (int i = 0; i < Vec::N; ++i)
-                vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - eh.x[i] : (eh.x[i] + rh.x[i]) - th.x[i];
-            const float ns = vpnorm(vk, p);
-            const float a = ps - ns;
-            lsum += a > -m ? a : -m;
-            const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
-            if (c == 0.f) continue;
-            csum += c;
-            Vec gk, gs;
-            vpnorm_bwd(vk, ns, p, -c, gk);
+            for (int k = 0; k < NCH; ++k)
+                if (c0 + k < k_hi) vload(E[k], P.ent + (mine[c0 + k] >> 1) * D, D, lane);
+        };
+        load_chunk(k_lo);
+        // ---- positive forward
+        Hs = H; Ts = T;
+        if constexpr (MODEL == 1) {
+            vnormalize(W, nW);
+            hdot = vdot(H, nW);
+            tdot = vdot(T, nW);
 #pragma unroll
             for (int i = 0; i < Vec::N; ++i) {
-                aR.x[i] += gk.x[i];
-                if (tail_side) aH.x[i] += gk.x[i]; else aT.x[i] -= gk.x[i];
-                gs.x[i] = tail_side ? -gk.x[i] : gk.x[i];   // corrupted tail gets -g, corrupted head +g
-            }
-            if constexpr (MODEL == 0) {
-                sink.ent(e, gs, D, lane);
-            } else {
-                Vec gp, ge;
-                if (nf) vnormalize_bwd(Es, en, gs, gp); else gp = gs;
-                const float ng = vdot(nW, gp);
-#pragma unroll
-                for (int i = 0; i < Vec::N; ++i) {
-                    ge.x[i] = gp.x[i] - nW.x[i] * ng;
-                    aW.x[i] -= ed * gp.x[i] + ng * E[k].x[i];
-                }
-                sink.ent(e, ge, D, lane);
+                Hs.x[i] = H.x[i] - hdot * nW.x[i];
+                Ts.x[i] = T.x[i] - tdot * nW.x[i];
             }
         }
-        c0 += NCH;
-        if (c0 >= neg) break;
-        load_chunk(c0);
+        if (nf) {
+            hn = vnormalize(Hs, hh);
+            vnormalize(Rr, rh);
+            tn = vnormalize(Ts, th);
+        } else {
+            hh = Hs; rh = Rr; th = Ts;
+        }
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
+        ps = vpnorm(vpos, p);
+        const float m = P.margin, inv = P.inv_count;
+        for (int64_t c0 = k_lo; c0 < k_hi;) {
+#pragma unroll
+            for (int k = 0; k < NCH; ++k) {
+                if (c0 + k >= k_hi) break;
+                const int64_t v = mine[c0 + k];
+                const int64_t e = v >> 1;
+                const bool tail_side = v & 1;
+                Vec Es = E[k], eh, vk;
+                float ed = 0.f, en = 0.f;
+                if constexpr (MODEL == 1) {
+                    ed = vdot(E[k], nW);
+#pragma unroll
+                    for (int i = 0; i < Vec::N; ++i) Es.x[i] = E[k].x[i] - ed * nW.x[i];
+                }
+                if (nf) en = vnormalize(Es, eh); else eh = Es;
+#pragma unroll
+                for (int i = 0; i < Vec::N; ++i)
+                    vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - eh.x[i] : (eh.x[i] + rh.x[i]) - th.x[i];
+                const float ns = vpnorm(vk, p);
+                const float a = ps - ns;
+                lsum += a > -m ? a : -m;
+                const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
+                float *dst = nullptr;
+                if constexpr (CSR) dst = cw.contrib + s_dst[pl * neg + c0 + k] * D;
+                if (c == 0.f) {
+                    if constexpr (CSR) {   // the reserved slot must still be defined
+                        Vec z;
+                        vzero(z);
+                        vstore(z, dst, D, lane);
+                    }
+                    continue;
+                }
+                csum += c;
+                Vec gk, gs;
+                vpnorm_bwd(vk, ns, p, -c, gk);
+#pragma unroll
+                for (int i = 0; i < Vec::N; ++i) {
+                    aR.x[i] += gk.x[i];
+                    if (tail_side) aH.x[i] += gk.x[i]; else aT.x[i] -= gk.x[i];
+                    gs.x[i] = tail_side ? -gk.x[i] : gk.x[i];   // corrupted tail gets -g, corrupted head +g
+                }
+                if constexpr (MODEL == 0) {
+                    if constexpr (CSR) vstore(gs, dst, D, lane); else sink.ent(e, gs, D, lane);
+                } else {
+                    Vec gp, ge;
+                    if (nf) vnormalize_bwd(Es, en, gs, gp); else gp = gs;
+                    const float ng = vdot(nW, gp);
+#pragma unroll
+                    for (int i = 0; i < Vec::N; ++i) {
+                        ge.x[i] = gp.x[i] - nW.x[i] * ng;
+                        aW.x[i] -= ed * gp.x[i] + ng * E[k].x[i];
+                    }
+                    if constexpr (CSR) vstore(ge, dst, D, lane); else sink.ent(e, ge, D, lane);
+                }
+            }
+            c0 += NCH;
+            if (c0 >= k_hi) break;
+            load_chunk(c0);
+        }
     }
+    if constexpr (S > 1) {
+        // ---- meet the positive's partials in LDS
+        float *mr = red + grp * 4 * RW;
+#pragma unroll
+        for (int k = 0; k < KCH; ++k) {
+            const int c = k * G + lane;
+            mr[0 * RW + c] = aH.x[k];
+            mr[1 * RW + c] = aT.x[k];
+            mr[2 * RW + c] = aR.x[k];
+            if constexpr (MODEL == 1) mr[3 * RW + c] = aW.x[k];
+        }
+        if (lane == 0) {
+            cs[grp * 2 + 0] = csum;
+            cs[grp * 2 + 1] = lsum;
+        }
+        __syncthreads();
+        if (sub != 0 || !active) return;
+        csum = 0.f;
+        lsum = 0.f;
+        vzero(aH); vzero(aT); vzero(aR); vzero(aW);
+        for (int q = 0; q < S; ++q) {   // fixed order: deterministic
+            const float *qr = red + (grp + q) * 4 * RW;
+#pragma unroll
+            for (int k = 0; k < KCH; ++k) {
+                const int c = k * G + lane;
+                aH.x[k] += qr[0 * RW + c];
+                aT.x[k] += qr[1 * RW + c];
+                aR.x[k] += qr[2 * RW + c];
+                if constexpr (MODEL == 1) aW.x[k] += qr[3 * RW + c];
+            }
+            csum += cs[(grp + q) * 2 + 0];
+            lsum += cs[(grp + q) * 2 + 1];
+        }
+    }
+    if (!active) return;
     // ---- positive backward and the group's on-chip accumulators
     if (csum != 0.f) {
         Vec gv;
@@ -648,7 +848,7 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
             sink.norm(rp, aW, D, lane);
         }
     }
-    if (lane == 0 && loss) atomicAdd(loss, lsum * inv);
+    if (lane == 0 && loss) atomicAdd(loss, lsum * P.inv_count);
 }
 
 // Sparse apply: for every touched row finish the gradient (normalize Jacobian of the pre-step row
@@ -658,6 +858,8 @@ struct ApplyTable {
     int *flag;
     int64_t rows;
     int jacobian;
+    const int *start;       // CSR of extra contribution rows (NULL: none): rows start[r] .. start[r+1]-1
+    const float *contrib;   // [n][dim]
 };
 struct ApplyParams {
     ApplyTable t[3];
@@ -689,11 +891,34 @@ __global__ __launch_bounds__(256) void k_apply(ApplyParams A) {
     }
     if (ti >= A.ntab) return;
     const ApplyTable &T = A.t[ti];
-    if (!T.flag[row]) return;
+    const int flagged = T.flag[row];
+    int c0 = 0, c1 = 0;
+    if (T.start) {
+        c0 = T.start[row];
+        c1 = T.start[row + 1];
+    }
+    if (!flagged && c0 == c1) return;
     const int D = (int)A.dim;
     Vec x, gsum_, g;
     vload(x, T.w + row * D, D, lane);
-    vload(gsum_, T.grad + row * D, D, lane);
+    if (flagged) vload(gsum_, T.grad + row * D, D, lane); else vzero(gsum_);
+    // contributions of this step's corrupted-entity slots (counting-sort order)
+    int j = c0;
+    for (; j + 4 <= c1; j += 4) {
+        Vec c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) vload(c[u], T.contrib + (int64_t)(j + u) * D, D, lane);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) gsum_.x[i] += c[u].x[i];
+    }
+    for (; j < c1; ++j) {
+        Vec c;
+        vload(c, T.contrib + (int64_t)j * D, D, lane);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) gsum_.x[i] += c.x[i];
+    }
     if (T.jacobian) {
         const float n = sqrtf(vdot(x, x));
         vnormalize_bwd(x, n, gsum_, g);
@@ -714,10 +939,12 @@ __global__ __launch_bounds__(256) void k_apply(ApplyParams A) {
         vstore(a, T.acc + row * D, D, lane);
     }
     vstore(x, T.w + row * D, D, lane);
-    Vec z;
-    vzero(z);
-    vstore(z, T.grad + row * D, D, lane);
-    if (lane == 0) T.flag[row] = 0;
+    if (flagged) {
+        Vec z;
+        vzero(z);
+        vstore(z, T.grad + row * D, D, lane);
+        if (lane == 0) T.flag[row] = 0;
+    }
 }
 
 // ---------------------------------------------------------------- scoring ----------------------
@@ -914,13 +1141,18 @@ int pick_nch(int64_t neg, int kch) {
     X(2, 1, 1) X(4, 1, 1) X(8, 1, 1) X(16, 1, 1) X(32, 1, 1) X(64, 1, 1) X(64, 1, 2) X(64, 1, 4)    \
     X(64, 1, 8)
 
-// VEC=1 shapes x NCH of the sampled step kernel
-#define PT_SSHAPES(X)                                                                                 \
-    X(2, 1, 1) X(2, 1, 4) X(2, 1, 8) X(2, 1, 32) X(4, 1, 1) X(4, 1, 4) X(4, 1, 8) X(4, 1, 32)         \
-    X(8, 1, 1) X(8, 1, 4) X(8, 1, 8) X(8, 1, 32) X(16, 1, 1) X(16, 1, 4) X(16, 1, 8) X(16, 1, 32)     \
-    X(32, 1, 1) X(32, 1, 4) X(32, 1, 8) X(32, 1, 32) X(64, 1, 1) X(64, 1, 4) X(64, 1, 8) X(64, 1, 32) \
-    X(64, 2, 1) X(64, 2, 4) X(64, 2, 8) X(64, 2, 32) X(64, 4, 1) X(64, 4, 4) X(64, 4, 8) X(64, 4, 32) \
-    X(64, 8, 1) X(64, 8, 4) X(64, 8, 8)
+// VEC=1 shapes x NCH x S of the sampled step kernel: S = 1 for neg < 8 (NCH covers neg), S = 4 with
+// NCH covering ceil(neg/4) (chunks beyond 32 negatives per sub-group loop)
+#define PT_SSHAPES(X)                                                                                  \
+    X(2, 1, 1, 1) X(2, 1, 4, 1) X(2, 1, 8, 1) X(2, 1, 8, 4) X(2, 1, 32, 4)                             \
+    X(4, 1, 1, 1) X(4, 1, 4, 1) X(4, 1, 8, 1) X(4, 1, 8, 4) X(4, 1, 32, 4)                             \
+    X(8, 1, 1, 1) X(8, 1, 4, 1) X(8, 1, 8, 1) X(8, 1, 8, 4) X(8, 1, 32, 4)                             \
+    X(16, 1, 1, 1) X(16, 1, 4, 1) X(16, 1, 8, 1) X(16, 1, 8, 4) X(16, 1, 32, 4)                        \
+    X(32, 1, 1, 1) X(32, 1, 4, 1) X(32, 1, 8, 1) X(32, 1, 8, 4) X(32, 1, 32, 4)                        \
+    X(64, 1, 1, 1) X(64, 1, 4, 1) X(64, 1, 8, 1) X(64, 1, 8, 4) X(64, 1, 32, 4)                        \
+    X(64, 2, 1, 1) X(64, 2, 4, 1) X(64, 2, 8, 1) X(64, 2, 8, 4) X(64, 2, 32, 4)                        \
+    X(64, 4, 1, 1) X(64, 4, 4, 1) X(64, 4, 8, 1) X(64, 4, 8, 4) X(64, 4, 32, 4)                        \
+    X(64, 8, 1, 1) X(64, 8, 4, 1) X(64, 8, 8, 1) X(64, 8, 8, 4)
 
 }  // namespace
 
@@ -949,9 +1181,24 @@ hipError_t launch_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t
     return hipGetLastError();
 }
 
+hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
+                             int bern, int filter, int64_t calls, const CsrWork &w, hipStream_t st) {
+    const int64_t n = calls * bs * (neg + 1);
+    hipLaunchKernelGGL(dev::k_sample_csr, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, states, threads, bs,
+                       neg, bern, filter, calls, w);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_counts(const CsrWork &w, int64_t n, int64_t calls, uint64_t *states, int64_t threads,
+                              int64_t bs, int64_t dpp, hipStream_t st) {
+    hipLaunchKernelGGL(dev::k_scan_counts, dim3((unsigned)calls), dim3(1024), 0, st, w.cnt, w.start, n, states, threads,
+                       bs, dpp);
+    return hipGetLastError();
+}
+
 hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t *states, int64_t threads, int bern,
                        int filter, const int64_t *bh, const int64_t *bt, const int64_t *br, const StepWorkspace &W,
-                       float *loss, hipStream_t st) {
+                       float *loss, hipStream_t st, const CsrWork *csr) {
     if (P.batch_size <= 0) return hipSuccess;
     dev::GlobalSink sink{W.gent, W.grel, W.gnorm, W.fent, W.frel, W.fnorm};
     if (bh) {   // external batch
@@ -971,18 +1218,33 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
         return hipErrorInvalidValue;
     }
     const Shape s = pick_shape(P.dim, false);
-    const int nch = pick_nch(P.neg, s.KCH);
-    const int64_t gpb = 256 / s.G;
-    const dim3 grid((unsigned)((P.batch_size + gpb - 1) / gpb)), block(256);
-    const size_t lds = (size_t)gpb * (size_t)P.neg * sizeof(int64_t);
-#define PT_SSTEP(G_, K_, N_)                                                                                      \
-    if (s.G == G_ && s.KCH == K_ && nch == N_) {                                                                \
-        if (P.model == 0)                                                                                         \
-            hipLaunchKernelGGL((dev::k_step_sampled<0, G_, K_, N_>), grid, block, lds, st, P, g, states, threads,  \
-                               bern, filter, sink, loss);                                                         \
-        else                                                                                                      \
-            hipLaunchKernelGGL((dev::k_step_sampled<1, G_, K_, N_>), grid, block, lds, st, P, g, states, threads,  \
-                               bern, filter, sink, loss);                                                         \
+    // split a positive's negatives over 4 lane groups when there are enough of them
+    const int S = (P.neg >= 8 && 256 / s.G >= 4) ? 4 : 1;
+    const int64_t nper = (P.neg + S - 1) / S;
+    const int nch = pick_nch(nper, s.KCH);
+    const int64_t gpb = 256 / s.G, ppb = gpb / S;
+    const dim3 grid((unsigned)((P.batch_size + ppb - 1) / ppb)), block(256);
+    size_t lds = (size_t)ppb * (size_t)P.neg * sizeof(int64_t) * (csr ? 2 : 1);
+    if (S > 1) lds += sizeof(float) * ((size_t)gpb * 4 * s.KCH * s.G + (size_t)gpb * 2);
+    if (lds > 64 * 1024) return hipErrorInvalidValue;
+    const CsrWork cw = csr ? *csr : CsrWork{};
+#define PT_SSTEP(G_, K_, N_, S_)                                                                                  \
+    if (s.G == G_ && s.KCH == K_ && nch == N_ && S == S_) {                                                     \
+        if (csr) {                                                                                                \
+            if (P.model == 0)                                                                                     \
+                hipLaunchKernelGGL((dev::k_step_sampled<0, G_, K_, N_, S_, true>), grid, block, lds, st, P, g,     \
+                                   states, threads, bern, filter, sink, loss, cw);                                \
+            else                                                                                                  \
+                hipLaunchKernelGGL((dev::k_step_sampled<1, G_, K_, N_, S_, true>), grid, block, lds, st, P, g,     \
+                                   states, threads, bern, filter, sink, loss, cw);                                \
+        } else {                                                                                                  \
+            if (P.model == 0)                                                                                     \
+                hipLaunchKernelGGL((dev::k_step_sampled<0, G_, K_, N_, S_, false>), grid, block, lds, st, P, g,    \
+                                   states, threads, bern, filter, sink, loss, cw);                                \
+            else                                                                                                  \
+                hipLaunchKernelGGL((dev::k_step_sampled<1, G_, K_, N_, S_, false>), grid, block, lds, st, P, g,    \
+                                   states, threads, bern, filter, sink, loss, cw);                                \
+        }                                                                                                         \
         return hipGetLastError();                                                                                 \
     }
     PT_SSHAPES(PT_SSTEP)
@@ -991,14 +1253,16 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
 }
 
 hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *states, int64_t threads, int64_t bs,
-                        int64_t dpp, float *loss, hipStream_t st) {
+                        int64_t dpp, float *loss, hipStream_t st, const CsrWork *csr) {
     const Shape s = pick_shape(P.dim);
     dev::ApplyParams A{};
     A.ntab = 0;
     const int ent_j = P.model == 0 && P.norm_flag;
-    A.t[A.ntab++] = dev::ApplyTable{P.ent, P.ent_acc, W.gent, W.fent, P.ent_total, ent_j};
-    A.t[A.ntab++] = dev::ApplyTable{P.rel, P.rel_acc, W.grel, W.frel, P.rel_total, P.norm_flag};
-    if (P.model == 1) A.t[A.ntab++] = dev::ApplyTable{P.normv, P.norm_acc, W.gnorm, W.fnorm, P.rel_total, 1};
+    A.t[A.ntab++] = dev::ApplyTable{P.ent, P.ent_acc, W.gent, W.fent, P.ent_total, ent_j,
+                                    csr ? csr->start : nullptr, csr ? csr->contrib : nullptr};
+    A.t[A.ntab++] = dev::ApplyTable{P.rel, P.rel_acc, W.grel, W.frel, P.rel_total, P.norm_flag, nullptr, nullptr};
+    if (P.model == 1)
+        A.t[A.ntab++] = dev::ApplyTable{P.normv, P.norm_acc, W.gnorm, W.fnorm, P.rel_total, 1, nullptr, nullptr};
     A.dim = P.dim;
     A.opt = P.opt;
     A.lr = P.lr;

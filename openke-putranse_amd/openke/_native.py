@@ -66,7 +66,7 @@ SIGNATURES = {
     "pt_trainer_update_desc": (ctypes.c_int, [c_vp, ctypes.POINTER(ModelDesc)]),
     "pt_trainer_step": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "pt_trainer_run": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
-    "pt_trainer_step_timed": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_f32p, c_f32p, c_vp]),
+    "pt_trainer_run_timed": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "pt_score": (ctypes.c_int, [ctypes.POINTER(ModelDesc), c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "pt_score_queries": (ctypes.c_int, [ctypes.POINTER(ModelDesc), c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "pt_lp_metrics": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),

@@ -119,3 +119,21 @@ def assert_tables_close(ours, ref, atol, ill=None, lr=None, max_frac=1e-3):
         assert bad.mean() <= max_frac, "too many ill-conditioned mismatches: %d" % bad.sum()
         return
     assert not bad.any(), "max abs err %g (atol %g) at %d entries" % (err.max(), atol, bad.sum())
+
+
+def assert_close_vs_oracle(ours, ref, orc, atol=1e-5, factor=10.0):
+    """Multi-step Adagrad parity: |ours-ref| <= max(atol, factor*|oracle-ref|) elementwise.
+
+    After a few Adagrad steps the reference's own float32 result is defined only up to the
+    amplification of rounding-order differences (a component whose accumulated gradient cancelled
+    partly turns a 1e-7 relative summation difference into an lr-scaled step difference). The oracle
+    is an independent float32 implementation of the same algorithm; where it also drifts from the
+    reference, the element is sensitive and ours may drift by the same order; everywhere else ours
+    must meet atol."""
+    ours = np.asarray(ours, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    orc = np.asarray(orc, dtype=np.float64)
+    err = np.abs(ours - ref)
+    bound = np.maximum(atol, factor * np.abs(orc - ref))
+    bad = err > bound
+    assert not bad.any(), "max err %g (bound %g) at %d entries" % (err[bad].max(), bound[bad].min(), bad.sum())
