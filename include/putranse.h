@@ -137,18 +137,30 @@ int pt_universe_remaps(const pt_universe *u, int64_t *ent_remap, int64_t *rel_re
 pt_graph *pt_universe_graph(pt_universe *u);      /* the universe's local training graph */
 int pt_universe_seeds(const pt_universe *u, uint64_t *seeds);   /* LCG states after randReset */
 
-/* Train many universes concurrently in one persistent launch (one workgroup per universe). */
+/* Train many universes concurrently: one persistent workgroup per universe runs all its epochs x
+ * nbatches minibatch-synchronous steps (Parallel_Universe_Config.train_embedding_space + Trainer.run,
+ * Parallel_Universe_Config.py:228-258, Trainer.py:90-104), universes of different dims on separate
+ * streams. Tables / accumulators are the caller's device buffers (updated in place). */
 typedef struct {
     const pt_graph *graph;      /* universe-local training graph (from pt_universe_graph) */
-    const uint64_t *seeds;      /* `threads` LCG states */
-    int64_t threads, batch_size, epochs, nbatches;
+    const uint64_t *seeds;      /* host: `threads` LCG states (pt_universe_seeds) */
+    int64_t threads, batch_size, epochs, nbatches, neg;
     float lr, margin;
     float *ent, *rel, *normv;   /* device tables of this universe */
     float *ent_acc, *rel_acc, *norm_acc;
     int64_t dim;
 } pt_universe_job;
+/* prepared set: graphs uploaded, per-universe workspace (LCG states, gradient rows, flags) in HBM */
+typedef struct pt_universe_set pt_universe_set;
+int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm, int32_t norm_flag,
+                           int32_t opt, int64_t bern, int64_t filter, pt_universe_set **out);
+/* run every universe's `epochs` (continuing from the current LCG states); d_losses: NULL or device
+ * [sum of epochs] floats, job-order concatenation of Trainer.run's per-epoch loss sums */
+int pt_universe_set_train(pt_universe_set *s, float *d_losses, void *stream);
+int pt_universe_set_free(pt_universe_set *s);
+/* create + train + free (synchronizes `stream`) */
 int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm, int32_t norm_flag,
-                       int64_t bern, int64_t filter, float *d_losses, void *stream);
+                       int32_t opt, int64_t bern, int64_t filter, float *d_losses, void *stream);
 
 /* ------------------------------------------------------------------ link prediction --------- */
 /* Per-universe all-entity scoring with a float MIN reduction into per-key rows

@@ -16,6 +16,7 @@
 #include "kernels.h"
 #include "rng.h"
 #include "universe.h"
+#include "universes.h"
 
 // ======================================================================== errors =================
 namespace pt {
@@ -558,63 +559,176 @@ extern "C" int pt_universe_seeds(const pt_universe *u, uint64_t *seeds) {
     return PT_OK;
 }
 
-// Train many universes: each universe is an independent chain of epochs*nbatches minibatch-
-// synchronous steps. Chains are issued round-robin on a pool of streams so they run concurrently;
-// each chain's epoch is one replayed hipGraph.
-extern "C" int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm,
-                                  int32_t norm_flag, int64_t bern, int64_t filter, float *d_losses, void *stream) {
-    PT_CHECK(jobs || n == 0, PT_EINVAL, "null jobs");
+// Train many universes with the persistent multi-universe kernel (universes.hip).
+struct pt_universe_set {
+    int32_t model = 0, p_norm = 1, norm_flag = 1, opt = PT_ADAGRAD;
+    int64_t bern = 0, filter = 0, neg = 1;
+    int device = -1;
+    void *arena = nullptr;
+    struct Group {
+        pt::Shape shape;
+        pt::UniverseDev *d_us = nullptr;   // inside the arena
+        int64_t n = 0, list_cap = 0;
+        std::vector<int64_t> loss_off;     // per universe of the group: offset into d_losses
+    };
+    std::vector<Group> groups;
+    std::vector<pt::UniverseDev> host;    // by group, loss pointers patched per train call
+    std::vector<int64_t> host_loss_off;
+    std::vector<hipStream_t> streams;
+    ~pt_universe_set() {
+        for (auto s : streams) (void)hipStreamDestroy(s);
+        if (arena) (void)hipFree(arena);
+    }
+};
+
+extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm,
+                                      int32_t norm_flag, int32_t opt, int64_t bern, int64_t filter,
+                                      pt_universe_set **out) {
+    PT_CHECK(out && (jobs || n == 0), PT_EINVAL, "pt_universe_set_create: null argument");
+    PT_CHECK(model == 0 || model == 1, PT_EINVAL, "model must be 0 (TransE) or 1 (TransH)");
+    PT_CHECK(p_norm == 1 || p_norm == 2, PT_EINVAL, "p_norm must be 1 or 2");
+    PT_CHECK(opt == PT_SGD || opt == PT_ADAGRAD, PT_EINVAL, "opt must be PT_SGD or PT_ADAGRAD");
+    auto set = std::make_unique<pt_universe_set>();
+    set->model = model; set->p_norm = p_norm; set->norm_flag = norm_flag; set->opt = opt;
+    set->bern = bern; set->filter = filter;
+    PT_HIP(hipGetDevice(&set->device));
+    int64_t neg = -1;
+    // layout of the per-universe workspace in one arena
+    auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
+    struct Slot {
+        int64_t states, grad, flags;
+    };
+    std::vector<Slot> slots((size_t)n);
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const pt_universe_job &J = jobs[i];
+        PT_CHECK(J.graph && J.seeds && J.ent && J.rel, PT_EINVAL, "universe job: null graph / seeds / tables");
+        PT_CHECK(model == 0 || J.normv, PT_EINVAL, "TransH universe job needs normv");
+        PT_CHECK(opt == PT_SGD || (J.ent_acc && J.rel_acc && (model == 0 || J.norm_acc)), PT_EINVAL,
+                 "Adagrad universe job needs accumulators");
+        PT_CHECK(J.threads > 0 && J.threads <= 64, PT_EINVAL, "universe job: threads must be in [1, 64]");
+        PT_CHECK(J.dim > 0 && pt::shape_supported(J.dim), PT_EINVAL, "universe job: unsupported dim");
+        PT_CHECK(J.batch_size >= 0 && J.epochs >= 0 && J.nbatches >= 0, PT_EINVAL, "universe job: negative sizes");
+        PT_CHECK(neg < 0 || J.neg == neg, PT_EINVAL, "universe jobs must share neg");
+        PT_CHECK(J.neg >= 1, PT_EINVAL, "universe job: neg must be >= 1");
+        neg = J.neg;
+        const pt::Graph &g = reinterpret_cast<const pt_graph *>(J.graph)->g;
+        PT_CHECK(g.train_total > 0 || J.batch_size == 0, PT_EINVAL, "universe job: empty graph");
+        PT_CHECK(J.batch_size * (4 + J.neg) <= 16384, PT_EINVAL, "universe job: batch too large for the LDS work list");
+        const int64_t rows = g.ent_total + g.rel_total * (model == 1 ? 2 : 1);
+        slots[i].states = total; total += al(8 * J.threads);
+        slots[i].grad = total;   total += al(4 * rows * J.dim);
+        slots[i].flags = total;  total += al(4 * (g.ent_total + 2 * g.rel_total));
+    }
+    set->neg = neg < 0 ? 1 : neg;
+    const int64_t us_off = total;
+    total += al((int64_t)sizeof(pt::UniverseDev) * std::max<int64_t>(n, 1));
+    PT_HIP(hipMalloc(&set->arena, (size_t)total));
+    char *base = (char *)set->arena;
+    PT_HIP(hipMemset(base, 0, (size_t)us_off));
+    // group by row shape
+    std::map<std::tuple<int, int, int>, std::vector<int64_t>> by_shape;
+    for (int64_t i = 0; i < n; ++i) {
+        const pt::Shape s = pt::pick_shape(jobs[i].dim);
+        by_shape[std::make_tuple(s.G, s.VEC, s.KCH)].push_back(i);
+    }
+    set->host.reserve((size_t)n);
+    int64_t loss_off = 0;
+    std::vector<int64_t> loss_of((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        loss_of[i] = loss_off;
+        loss_off += jobs[i].epochs;
+    }
+    std::vector<uint64_t> states_h;
+    for (auto &kv : by_shape) {
+        pt_universe_set::Group grp;
+        grp.shape = pt::Shape{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first)};
+        grp.d_us = (pt::UniverseDev *)(base + us_off) + set->host.size();
+        grp.n = (int64_t)kv.second.size();
+        for (int64_t i : kv.second) {
+            const pt_universe_job &J = jobs[i];
+            pt::Graph &g = const_cast<pt::Graph &>(reinterpret_cast<const pt_graph *>(J.graph)->g);
+            int rc = g.upload();
+            if (rc) return rc;
+            pt::UniverseDev U{};
+            U.g = g.dev;
+            U.states = (uint64_t *)(base + slots[i].states);
+            PT_HIP(hipMemcpy(U.states, J.seeds, 8 * J.threads, hipMemcpyHostToDevice));
+            U.ent = J.ent; U.rel = J.rel; U.normv = J.normv;
+            U.ent_acc = J.ent_acc; U.rel_acc = J.rel_acc; U.norm_acc = J.norm_acc;
+            float *gr = (float *)(base + slots[i].grad);
+            U.gent = gr;
+            U.grel = gr + g.ent_total * J.dim;
+            U.gnorm = model == 1 ? U.grel + g.rel_total * J.dim : nullptr;
+            int32_t *fl = (int32_t *)(base + slots[i].flags);
+            U.fent = fl;
+            U.frel = fl + g.ent_total;
+            U.fnorm = U.frel + g.rel_total;
+            U.losses = nullptr;
+            U.threads = J.threads; U.bs = J.batch_size; U.nbatches = J.nbatches; U.epochs = J.epochs; U.dim = J.dim;
+            U.lr = J.lr; U.margin = J.margin;
+            set->host.push_back(U);
+            set->host_loss_off.push_back(loss_of[i]);
+            grp.list_cap = std::max(grp.list_cap, std::max<int64_t>(J.batch_size * (4 + J.neg), 1));
+        }
+        set->groups.push_back(std::move(grp));
+    }
+    for (size_t i = 0; i < set->groups.size(); ++i) {
+        hipStream_t s;
+        PT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        set->streams.push_back(s);
+    }
+    *out = set.release();
+    return PT_OK;
+}
+
+extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void *stream) {
+    PT_CHECK(set, PT_EINVAL, "null universe set");
+    if (set->host.empty()) return PT_OK;
     hipStream_t user = (hipStream_t)stream;
-    const int NS = 16;
-    hipStream_t ss[NS];
-    for (int i = 0; i < NS; ++i) PT_HIP(hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking));
+    for (size_t i = 0; i < set->host.size(); ++i)
+        set->host[i].losses = d_losses ? d_losses + set->host_loss_off[i] : nullptr;
+    PT_HIP(hipMemcpyAsync(set->groups[0].d_us, set->host.data(), sizeof(pt::UniverseDev) * set->host.size(),
+                          hipMemcpyHostToDevice, user));
     hipEvent_t start;
     PT_HIP(hipEventCreateWithFlags(&start, hipEventDisableTiming));
     PT_HIP(hipEventRecord(start, user));
-    for (int i = 0; i < NS; ++i) PT_HIP(hipStreamWaitEvent(ss[i], start, 0));
-    std::vector<std::unique_ptr<pt_trainer>> trainers;
-    std::vector<std::unique_ptr<pt_sampler>> samplers;
     int rc = PT_OK;
-    int64_t loss_off = 0;
-    for (int64_t i = 0; i < n && !rc; ++i) {
-        const pt_universe_job &J = jobs[i];
-        pt::Graph *g = const_cast<pt::Graph *>(reinterpret_cast<const pt::Graph *>(J.graph));
-        pt_model_desc m{};
-        m.model = model; m.p_norm = p_norm; m.norm_flag = norm_flag; m.opt = PT_ADAGRAD;
-        m.lr = J.lr; m.margin = J.margin;
-        m.ent_total = g->ent_total; m.rel_total = g->rel_total; m.dim = J.dim;
-        m.ent = J.ent; m.rel = J.rel; m.normv = J.normv;
-        m.ent_acc = J.ent_acc; m.rel_acc = J.rel_acc; m.norm_acc = J.norm_acc;
-        pt_trainer *t = nullptr;
-        rc = pt_trainer_create(&m, &t);
-        if (rc) break;
-        trainers.emplace_back(t);
-        auto s = std::make_unique<pt_sampler>();
-        rc = sampler_init(s.get(), g, J.threads, J.seeds);
-        if (rc) break;
-        const int64_t bs = J.batch_size;
-        if (bs <= 0 || J.epochs <= 0) {
-            samplers.push_back(std::move(s));
-            continue;
-        }
-        for (int64_t e = 0; e < J.epochs && !rc; ++e)
-            rc = pt_trainer_run(t, s.get(), bs, 1, bern, filter, J.nbatches, d_losses + loss_off, ss[i % NS]);
-        loss_off += J.nbatches;
-        samplers.push_back(std::move(s));
+    for (size_t k = 0; k < set->groups.size() && !rc; ++k) {
+        const auto &G = set->groups[k];
+        hipStream_t s = set->streams[k];
+        if (hipStreamWaitEvent(s, start, 0) != hipSuccess) { rc = pt::fail(PT_EHIP, "hipStreamWaitEvent"); break; }
+        const hipError_t e = pt::launch_universes(G.d_us, G.n, G.shape, set->model, set->p_norm, set->norm_flag,
+                                                  set->opt, set->neg, (int)set->bern, (int)set->filter, G.list_cap, s);
+        if (e != hipSuccess) rc = pt::fail(PT_EHIP, std::string("launch_universes: ") + hipGetErrorString(e));
     }
-    for (int i = 0; i < NS; ++i) {
+    for (size_t k = 0; k < set->groups.size(); ++k) {
         hipEvent_t done;
         (void)hipEventCreateWithFlags(&done, hipEventDisableTiming);
-        (void)hipEventRecord(done, ss[i]);
+        (void)hipEventRecord(done, set->streams[k]);
         (void)hipStreamWaitEvent(user, done, 0);
         (void)hipEventDestroy(done);
     }
-    // trainers/samplers own device workspace used by the queued work: wait before freeing
-    (void)hipStreamSynchronize(user);
-    trainers.clear();
-    samplers.clear();
-    for (int i = 0; i < NS; ++i) (void)hipStreamDestroy(ss[i]);
     (void)hipEventDestroy(start);
+    return rc;
+}
+
+extern "C" int pt_universe_set_free(pt_universe_set *set) {
+    if (set) (void)hipDeviceSynchronize();
+    delete set;
+    return PT_OK;
+}
+
+extern "C" int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm,
+                                  int32_t norm_flag, int32_t opt, int64_t bern, int64_t filter, float *d_losses,
+                                  void *stream) {
+    pt_universe_set *set = nullptr;
+    int rc = pt_universe_set_create(jobs, n, model, p_norm, norm_flag, opt, bern, filter, &set);
+    if (rc) return rc;
+    rc = pt_universe_set_train(set, d_losses, stream);
+    const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    pt_universe_set_free(set);
+    if (!rc && e != hipSuccess) rc = pt::fail(PT_EHIP, std::string("pt_universes_train: ") + hipGetErrorString(e));
     return rc;
 }
 

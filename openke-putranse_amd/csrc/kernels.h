@@ -56,6 +56,32 @@ struct LpPair {
     int32_t key, universe, anchor, rel, side;   // local anchor entity / relation ids
 };
 
+// lane-group shape of a row of D floats: G lanes x KCH chunks of VEC floats (kernels.hip header)
+struct Shape {
+    int G, VEC, KCH;
+};
+
+inline Shape pick_shape(int64_t D, bool vec4 = true) {
+    const int VEC = vec4 && D % 4 == 0 ? 4 : 1;
+    const int64_t chunks = D / VEC;
+    int G = 1;
+    while (G < chunks && G < 64) G <<= 1;
+    if (G < 2) G = 2;
+    int KCH = (int)((chunks + G - 1) / G);
+    if (VEC == 1) {   // VEC=1 instantiations exist for power-of-two chunk counts
+        int k = 1;
+        while (k < KCH) k <<= 1;
+        KCH = k;
+    }
+    return Shape{G, VEC, KCH};
+}
+
+// instantiated (G, VEC, KCH) row shapes
+#define PT_SHAPES(X)                                                                                  \
+    X(2, 4, 1) X(4, 4, 1) X(8, 4, 1) X(16, 4, 1) X(32, 4, 1) X(64, 4, 1) X(64, 4, 2)                 \
+    X(2, 1, 1) X(4, 1, 1) X(8, 1, 1) X(16, 1, 1) X(32, 1, 1) X(64, 1, 1) X(64, 1, 2) X(64, 1, 4)    \
+    X(64, 1, 8)
+
 bool shape_supported(int64_t dim);
 hipError_t launch_sample(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                          int bern, int filter, int64_t *h, int64_t *t, int64_t *r, float *y, hipStream_t st);

@@ -17,237 +17,13 @@
 
 #include <cstdint>
 
+#include "device.h"
 #include "graph.h"
 #include "kernels.h"
 #include "rng.h"
 
 namespace pt {
 namespace dev {
-
-constexpr float kEps = 1e-12f;   // F.normalize eps
-
-// ---------------------------------------------------------------- lane-group vectors -----------
-// All-reduce sum over an aligned group of G lanes, entirely on the VALU: DPP within 16-lane rows
-// (quad_perm xor1, xor2, row_half_mirror, row_mirror), then v_permlane16_swap / v_permlane32_swap
-// across rows (gfx950). Every lane of the group ends with the same value (each step adds a value and
-// its partner's, a commutative pair), which keeps group-uniform branches uniform.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-template <int G>
-__device__ __forceinline__ float gsum(float v) {
-    if constexpr (G >= 2) v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
-    if constexpr (G >= 4) v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
-    if constexpr (G >= 8) v += dpp_f<0x141>(v);   // row_half_mirror
-    if constexpr (G >= 16) v += dpp_f<0x140>(v);  // row_mirror
-    if constexpr (G >= 32) {
-        const unsigned x = __float_as_uint(v);
-        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-        v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-    }
-    if constexpr (G >= 64) {
-        const unsigned x = __float_as_uint(v);
-        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-        v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-    }
-    return v;
-}
-
-template <int G, int VEC, int KCH>
-struct V {
-    static constexpr int N = VEC * KCH;
-    float x[N];
-};
-
-template <int G, int VEC, int KCH>
-__device__ __forceinline__ void vload(V<G, VEC, KCH> &o, const float *__restrict__ row, int D, int lane) {
-#pragma unroll
-    for (int k = 0; k < KCH; ++k) {
-        const int c = k * G + lane;
-        if (c * VEC < D) {
-            if constexpr (VEC == 4) {
-                const float4 f = *reinterpret_cast<const float4 *>(row + c * 4);
-                o.x[k * 4 + 0] = f.x; o.x[k * 4 + 1] = f.y; o.x[k * 4 + 2] = f.z; o.x[k * 4 + 3] = f.w;
-            } else {
-#pragma unroll
-                for (int q = 0; q < VEC; ++q) o.x[k * VEC + q] = row[c * VEC + q];
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) o.x[k * VEC + q] = 0.f;
-        }
-    }
-}
-
-template <int G, int VEC, int KCH>
-__device__ __forceinline__ void vstore(const V<G, VEC, KCH> &o, float *__restrict__ row, int D, int lane) {
-#pragma unroll
-    for (int k = 0; k < KCH; ++k) {
-        const int c = k * G + lane;
-        if (c * VEC < D) {
-            if constexpr (VEC == 4) {
-                *reinterpret_cast<float4 *>(row + c * 4) =
-                    make_float4(o.x[k * 4 + 0], o.x[k * 4 + 1], o.x[k * 4 + 2], o.x[k * 4 + 3]);
-            } else {
-#pragma unroll
-                for (int q = 0; q < VEC; ++q) row[c * VEC + q] = o.x[k * VEC + q];
-            }
-        }
-    }
-}
-
-template <int G, int VEC, int KCH>
-__device__ __forceinline__ void vatomic(const V<G, VEC, KCH> &o, float *__restrict__ row, int D, int lane) {
-#pragma unroll
-    for (int k = 0; k < KCH; ++k) {
-        const int c = k * G + lane;
-        if (c * VEC < D) {
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) atomicAdd(row + c * VEC + q, o.x[k * VEC + q]);
-        }
-    }
-}
-
-template <int G, int VEC, int KCH>
-__device__ __forceinline__ float vdot(const V<G, VEC, KCH> &a, const V<G, VEC, KCH> &b) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < V<G, VEC, KCH>::N; ++i) s += a.x[i] * b.x[i];
-    return gsum<G>(s);
-}
-
-template <int G, int VEC, int KCH>
-__device__ __forceinline__ void vzero(V<G, VEC, KCH> &a) {
-#pragma unroll
-    for (int i = 0; i < V<G, VEC, KCH>::N; ++i) a.x[i] = 0.f;
-}
-
-template <int G, int VEC, int KCH>
-__device__ __forceinline__ bool vnonzero(const V<G, VEC, KCH> &a) {
-    int nz = 0;
-#pragma unroll
-    for (int i = 0; i < V<G, VEC, KCH>::N; ++i) nz |= a.x[i] != 0.f;
-    return gsum<G>((float)nz) != 0.f;
-}
-
-// F.normalize(x, 2, -1): out = x / max(||x||, eps); returns ||x||
-template <int G, int VEC, int KCH>
-__device__ __forceinline__ float vnormalize(const V<G, VEC, KCH> &x, V<G, VEC, KCH> &out) {
-    const float n = sqrtf(vdot(x, x));
-    const float inv = 1.0f / (n > kEps ? n : kEps);   // one division per row, then multiplies
-#pragma unroll
-    for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = x.x[i] * inv;
-    return n;
-}
-
-// backward of F.normalize at raw x with norm n: (g - x (x.g)/n^2) / n   (clamp_min branch: g / eps)
-template <int G, int VEC, int KCH>
-__device__ __forceinline__ void vnormalize_bwd(const V<G, VEC, KCH> &x, float n, const V<G, VEC, KCH> &g,
-                                               V<G, VEC, KCH> &out) {
-    if (n > kEps) {
-        const float inv = 1.0f / n;
-        const float c = vdot(g, x) * (inv * inv);
-#pragma unroll
-        for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = (g.x[i] - x.x[i] * c) * inv;
-    } else {
-#pragma unroll
-        for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = g.x[i] / kEps;
-    }
-}
-
-// ||v||_p for p in {1,2}
-template <int G, int VEC, int KCH>
-__device__ __forceinline__ float vpnorm(const V<G, VEC, KCH> &v, int p) {
-    float s = 0.f;
-    if (p == 1) {
-#pragma unroll
-        for (int i = 0; i < V<G, VEC, KCH>::N; ++i) s += fabsf(v.x[i]);
-        return gsum<G>(s);
-    }
-#pragma unroll
-    for (int i = 0; i < V<G, VEC, KCH>::N; ++i) s += v.x[i] * v.x[i];
-    return sqrtf(gsum<G>(s));
-}
-
-// ds * d||v||_p/dv : p=1 sgn(v)*ds (sgn 0 = 0), p=2 v*(ds/||v||) masked at ||v|| = 0
-template <int G, int VEC, int KCH>
-__device__ __forceinline__ void vpnorm_bwd(const V<G, VEC, KCH> &v, float nv, int p, float ds, V<G, VEC, KCH> &g) {
-    if (p == 1) {
-#pragma unroll
-        for (int i = 0; i < V<G, VEC, KCH>::N; ++i) g.x[i] = v.x[i] > 0.f ? ds : (v.x[i] < 0.f ? -ds : 0.f);
-    } else {
-        const float k = nv == 0.f ? 0.f : ds / nv;
-#pragma unroll
-        for (int i = 0; i < V<G, VEC, KCH>::N; ++i) g.x[i] = v.x[i] * k;
-    }
-}
-
-// ---------------------------------------------------------------- sampler --------------------
-__device__ __forceinline__ int64_t rand_max(uint64_t &s, int64_t x) { return (int64_t)(lcg_next(s) % (uint64_t)x); }
-
-// Filtered corruption (Corrupt.h:27-56 / :75-104): `vals` is the searched column of the sorted list
-// (trainHead[].t for corrupt_head, trainTail[].h for corrupt_tail) and [lo, hi] the run of known
-// partners of the positive's (entity, relation) - the [ll, rr] of the reference's two binary searches,
-// precomputed per triple (TripleRec). The draw and the final search are the reference's.
-__device__ __forceinline__ int64_t corrupt_in_run(const int32_t *__restrict__ vals, int64_t lo, int64_t hi, int64_t E,
-                                                  uint64_t &s) {
-    const int64_t tmp = rand_max(s, E - (hi - lo + 1));
-    if (tmp < vals[lo]) return tmp;
-    if (tmp > vals[hi] - hi + lo - 1) return tmp + hi - lo + 1;
-    int64_t l = lo, r = hi + 1;
-    while (l + 1 < r) {
-        const int64_t mid = (l + r) >> 1;
-        if (vals[mid] - mid + lo - 1 < tmp) l = mid; else r = mid;
-    }
-    return tmp + l - lo + 1;
-}
-
-// state of the sampler stream that produces positive b of call `call` after the current states
-// (Base.cpp:200-207 split: thread id owns positives [id*per, min((id+1)*per, bs)) of every call)
-__device__ __forceinline__ uint64_t positive_state(const uint64_t *states, int64_t threads, int64_t bs, int64_t b,
-                                                   int64_t dpp, int64_t call = 0) {
-    const int64_t per = bs % threads == 0 ? bs / threads : bs / threads + 1;
-    const int64_t id = b / per;
-    int64_t len = bs - id * per;
-    len = len > per ? per : len;
-    return lcg_jump(states[id], (uint64_t)((call * len + (b - id * per)) * dpp));
-}
-
-struct PosDraw {
-    int64_t h, r, t;
-    int32_t hr_lo, hr_hi, tr_lo, tr_hi;
-    uint64_t s1;   // stream state after the positive's index draw
-};
-
-// positive b: i = rand_max(trainTotal), trainList[i] (Base.cpp:210-215)
-__device__ __forceinline__ PosDraw draw_positive(const DeviceGraph &g, const uint64_t *states, int64_t threads,
-                                                 int64_t bs, int64_t b, int64_t dpp, int64_t call = 0) {
-    uint64_t s = positive_state(states, threads, bs, b, dpp, call);
-    const int64_t i = rand_max(s, g.train_total);
-    const int4 *p = reinterpret_cast<const int4 *>(g.rec + i);
-    const int4 a = p[0], c = p[1];
-    return PosDraw{a.x, a.y, a.z, a.w, c.x, c.y, c.z, s};
-}
-
-// negative k of a positive (stream offsets 1+2k coin, 2+2k corruption; Base.cpp:217-232): returns the
-// corrupted entity, *tail_side = 1 when the tail was replaced (corrupt_head), 0 when the head was
-__device__ __forceinline__ int64_t draw_negative(const DeviceGraph &g, const PosDraw &p, int64_t k, int bern,
-                                                 int filter, int *tail_side) {
-    uint64_t s = lcg_jump(p.s1, (uint64_t)(2 * k));
-    const float prob = bern ? g.bern_prob[p.r] : 500.f;
-    const int64_t E = g.ent_total;
-    if ((float)(lcg_next(s) % 1000ULL) < prob) {
-        *tail_side = 1;
-        if (filter) return corrupt_in_run(g.head_t, p.hr_lo, p.hr_hi, E, s);
-        const int64_t tmp = rand_max(s, E - 1);   // skips the passed entity h (Corrupt.h:18-25)
-        return tmp < p.h ? tmp : tmp + 1;
-    }
-    *tail_side = 0;
-    if (filter) return corrupt_in_run(g.tail_h, p.tr_lo, p.tr_hi, E, s);
-    const int64_t tmp = rand_max(s, E - 1);       // skips t (Corrupt.h:68-74)
-    return tmp < p.t ? tmp : tmp + 1;
-}
 
 // sampling() into arrays (one thread per positive); the stream advance is a separate kernel
 __global__ void k_sample(DeviceGraph g, const uint64_t *__restrict__ states, int64_t threads, int64_t bs, int64_t neg,
@@ -267,15 +43,6 @@ __global__ void k_sample(DeviceGraph g, const uint64_t *__restrict__ states, int
         ot[o] = tail_side ? e : tp;
         orr[o] = rp;
         if (oy) oy[o] = -1.f;
-    }
-}
-
-__device__ __forceinline__ void advance_states(uint64_t *states, int64_t threads, int64_t bs, int64_t dpp, int lane) {
-    if (lane < threads) {
-        const int64_t per = bs % threads == 0 ? bs / threads : bs / threads + 1;
-        int64_t len = bs - lane * per;
-        len = len < 0 ? 0 : (len > per ? per : len);
-        states[lane] = lcg_jump(states[lane], (uint64_t)(len * dpp));
     }
 }
 
@@ -314,7 +81,7 @@ __global__ __launch_bounds__(256) void k_sample_csr(DeviceGraph g, const uint64_
 // (the sampling pass was their only reader)
 __global__ __launch_bounds__(1024) void k_scan_counts(int32_t *__restrict__ cnt_all, int32_t *__restrict__ start_all,
                                                       int64_t n, uint64_t *states, int64_t threads, int64_t bs,
-                                                      int64_t dpp) {
+                                                      int64_t dpp, CsrWork w, int64_t slots) {
     __shared__ int32_t wtot[16];
     __shared__ int32_t carry_s;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -383,6 +150,12 @@ __global__ __launch_bounds__(1024) void k_scan_counts(int32_t *__restrict__ cnt_
         __syncthreads();
     }
     if (tid == 0) start[n] = carry_s;
+    __syncthreads();
+    // resolve every slot's destination row in the contribution buffer: start[e] + rank (the step kernel
+    // then needs no dependent lookup). off[] is overwritten in place by the destination.
+    const int32_t *neg = w.neg + (int64_t)blockIdx.x * slots;
+    int32_t *off = w.off + (int64_t)blockIdx.x * slots;
+    for (int64_t i = tid; i < slots; i += 1024) off[i] = start[neg[i] >> 1] + off[i];
 }
 
 // ---------------------------------------------------------------- fused step -----------------
@@ -407,194 +180,6 @@ struct GlobalSink {
         if (lane == 0) fnorm[row] = 1;
     }
 };
-
-// One positive group: forward + MarginLoss + backward for the positive and its `neg` negatives.
-// Gradient conventions per table (the apply pass finishes them):
-//   TransE: ent and rel gradients in normalized space (the apply pass multiplies by the normalize
-//           Jacobian of the pre-step row; sum-then-Jacobian == Jacobian-then-sum, it is linear);
-//   TransH: ent gradients raw (their projection/normalize Jacobians depend on the relation, so they are
-//           applied here), rel in normalized space, norm_vector in normalized (n-hat) space.
-// Negatives are given by `get_neg(k, &h, &t, &r)`; rows equal to the positive's reuse its registers
-// and accumulate on chip, other rows go straight to the sink.
-template <int MODEL, int G, int VEC, int KCH, typename Sink, typename NegFn>
-__device__ __forceinline__ float group_step(const StepParams &P, int64_t hp, int64_t rp, int64_t tp, int64_t neg,
-                                            NegFn get_neg, const Sink &sink, int lane) {
-    using Vec = V<G, VEC, KCH>;
-    const int D = (int)P.dim;
-    const int p = P.p_norm;
-    const bool nf = P.norm_flag != 0;
-    // ---- positive
-    Vec H, T, Rr, W, nW, hh, th, rh, vpos;
-    float hn = 0, tn = 0, hdot = 0, tdot = 0;
-    vload(H, P.ent + hp * D, D, lane);
-    vload(T, P.ent + tp * D, D, lane);
-    vload(Rr, P.rel + rp * D, D, lane);
-    Vec Hs = H, Ts = T;   // scored entity vectors (projected for TransH)
-    if constexpr (MODEL == 1) {
-        vload(W, P.normv + rp * D, D, lane);
-        vnormalize(W, nW);
-        hdot = vdot(H, nW);
-        tdot = vdot(T, nW);
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            Hs.x[i] = H.x[i] - hdot * nW.x[i];
-            Ts.x[i] = T.x[i] - tdot * nW.x[i];
-        }
-    }
-    if (nf) {
-        hn = vnormalize(Hs, hh);
-        vnormalize(Rr, rh);
-        tn = vnormalize(Ts, th);
-    } else {
-        hh = Hs; rh = Rr; th = Ts;
-    }
-#pragma unroll
-    for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
-    const float ps = vpnorm(vpos, p);
-
-    Vec aH, aT, aR, aW;   // on-chip accumulators of the positive's rows
-    vzero(aH); vzero(aT); vzero(aR); vzero(aW);
-    float csum = 0.f, lsum = 0.f;
-    const float m = P.margin;
-    const float inv = P.inv_count;
-
-    for (int64_t k = 0; k < neg; ++k) {
-        int64_t hk, tk, rk;
-        get_neg(k, hk, tk, rk);
-        const bool same_r = rk == rp;
-        // relation row of the negative
-        Vec Rk, rkh, Wk, nWk;
-        if (same_r) {
-            rkh = rh;
-            if constexpr (MODEL == 1) { nWk = nW; Wk = W; }
-        } else {
-            vload(Rk, P.rel + rk * D, D, lane);
-            if (nf) vnormalize(Rk, rkh); else rkh = Rk;
-            if constexpr (MODEL == 1) {
-                vload(Wk, P.normv + rk * D, D, lane);
-                vnormalize(Wk, nWk);
-            }
-        }
-        // entity rows of the negative: reuse the positive's when the (row, relation) matches
-        Vec Ek[2], Eks[2], ekh[2];
-        float ekn[2], ekdot[2];
-        int role[2];   // 0: row hp, 1: row tp, -1: other
-        const int64_t ids[2] = {hk, tk};
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int64_t e = ids[s];
-            role[s] = !same_r ? -1 : (e == hp ? 0 : (e == tp ? 1 : -1));
-            if (role[s] == 0) {
-                Ek[s] = H; Eks[s] = Hs; ekh[s] = hh; ekn[s] = hn; ekdot[s] = hdot;
-            } else if (role[s] == 1) {
-                Ek[s] = T; Eks[s] = Ts; ekh[s] = th; ekn[s] = tn; ekdot[s] = tdot;
-            } else {
-                vload(Ek[s], P.ent + e * D, D, lane);
-                Eks[s] = Ek[s];
-                ekdot[s] = 0.f;
-                if constexpr (MODEL == 1) {
-                    ekdot[s] = vdot(Ek[s], nWk);
-#pragma unroll
-                    for (int i = 0; i < Vec::N; ++i) Eks[s].x[i] = Ek[s].x[i] - ekdot[s] * nWk.x[i];
-                }
-                if (nf) ekn[s] = vnormalize(Eks[s], ekh[s]); else { ekh[s] = Eks[s]; ekn[s] = 0.f; }
-            }
-        }
-        Vec vk;
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) vk.x[i] = (ekh[0].x[i] + rkh.x[i]) - ekh[1].x[i];
-        const float ns = vpnorm(vk, p);
-        const float a = ps - ns;
-        lsum += a > -m ? a : -m;
-        const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
-        if (c == 0.f) continue;
-        csum += c;
-        Vec g;
-        vpnorm_bwd(vk, ns, p, -c, g);   // d loss / d v_k
-        // relation (normalized space)
-        if (same_r) {
-#pragma unroll
-            for (int i = 0; i < Vec::N; ++i) aR.x[i] += g.x[i];
-        } else {
-            sink.rel(rk, g, D, lane);
-        }
-        Vec gw;   // TransH: d/d n-hat of this negative's relation
-        if constexpr (MODEL == 1) vzero(gw);
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            Vec gs;   // d/d(normalized scored entity): +g for the head, -g for the tail
-#pragma unroll
-            for (int i = 0; i < Vec::N; ++i) gs.x[i] = s == 0 ? g.x[i] : -g.x[i];
-            if (role[s] >= 0) {
-                Vec &acc = role[s] == 0 ? aH : aT;
-#pragma unroll
-                for (int i = 0; i < Vec::N; ++i) acc.x[i] += gs.x[i];
-                continue;
-            }
-            if constexpr (MODEL == 0) {
-                sink.ent(ids[s], gs, D, lane);
-            } else {
-                Vec gp;   // through normalize of the projected vector
-                if (nf) vnormalize_bwd(Eks[s], ekn[s], gs, gp); else gp = gs;
-                const float ng = vdot(nWk, gp);
-                Vec ge;
-#pragma unroll
-                for (int i = 0; i < Vec::N; ++i) {
-                    ge.x[i] = gp.x[i] - nWk.x[i] * ng;
-                    gw.x[i] -= ekdot[s] * gp.x[i] + ng * Ek[s].x[i];
-                }
-                sink.ent(ids[s], ge, D, lane);
-            }
-        }
-        if constexpr (MODEL == 1) {
-            if (same_r) {
-#pragma unroll
-                for (int i = 0; i < Vec::N; ++i) aW.x[i] += gw.x[i];
-            } else if (vnonzero(gw)) {
-                sink.norm(rk, gw, D, lane);
-            }
-        }
-    }
-    // ---- positive backward
-    if (csum != 0.f) {
-        Vec g;
-        vpnorm_bwd(vpos, ps, p, csum, g);
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            aH.x[i] += g.x[i];
-            aR.x[i] += g.x[i];
-            aT.x[i] -= g.x[i];
-        }
-    }
-    if (vnonzero(aR)) sink.rel(rp, aR, D, lane);
-    if constexpr (MODEL == 0) {
-        if (vnonzero(aH)) sink.ent(hp, aH, D, lane);
-        if (vnonzero(aT)) sink.ent(tp, aT, D, lane);
-    } else {
-        // positive-row accumulators are in normalized-projected space: finish them once
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            Vec &acc = s == 0 ? aH : aT;
-            if (!vnonzero(acc)) continue;
-            const Vec &E = s == 0 ? H : T;
-            const Vec &Es = s == 0 ? Hs : Ts;
-            const float en = s == 0 ? hn : tn;
-            const float edot = s == 0 ? hdot : tdot;
-            Vec gp;
-            if (nf) vnormalize_bwd(Es, en, acc, gp); else gp = acc;
-            const float ng = vdot(nW, gp);
-            Vec ge;
-#pragma unroll
-            for (int i = 0; i < Vec::N; ++i) {
-                ge.x[i] = gp.x[i] - nW.x[i] * ng;
-                aW.x[i] -= edot * gp.x[i] + ng * E.x[i];
-            }
-            sink.ent(s == 0 ? hp : tp, ge, D, lane);
-        }
-        if (vnonzero(aW)) sink.norm(rp, aW, D, lane);
-    }
-    return lsum;
-}
 
 // General step on an externally given batch (Trainer.train_one_step): any (h, r, t) per slot.
 template <int MODEL, int G, int VEC, int KCH>
@@ -653,31 +238,39 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
     float *red = reinterpret_cast<float *>(s_neg + PPB * neg * (CSR ? 2 : 1));
     float *cs = red + GPB * 4 * RW;
     PosDraw pd{};
+    const int D = (int)P.dim;
+    Vec H, T, Rr, W, nW, hh, th, rh, vpos;
     if (active) {
         if constexpr (!CSR) {
             pd = draw_positive(g, states, threads, bs, b, 1 + 2 * neg);
+        } else {
+            const int4 q = cw.pos[b];
+            pd.h = q.x; pd.r = q.y; pd.t = q.z;
+        }
+        pd.h = uni<G>((int32_t)pd.h); pd.r = uni<G>((int32_t)pd.r); pd.t = uni<G>((int32_t)pd.t);
+        // the positive's rows are in flight while the negatives are drawn / fetched
+        vload(H, P.ent + pd.h * D, D, lane);
+        vload(T, P.ent + pd.t * D, D, lane);
+        vload(Rr, P.rel + pd.r * D, D, lane);
+        if constexpr (MODEL == 1) vload(W, P.normv + pd.r * D, D, lane);
+        if constexpr (!CSR) {
             for (int64_t k = k_lo + lane; k < k_hi; k += G) {
                 int side;
                 const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
                 s_neg[pl * neg + k] = (e << 1) | side;
             }
         } else {
-            const int4 q = cw.pos[b];
-            pd.h = q.x; pd.r = q.y; pd.t = q.z;
             for (int64_t k = k_lo + lane; k < k_hi; k += G) {
-                const int64_t v = cw.neg[b * neg + k];
-                s_neg[pl * neg + k] = v;
-                s_dst[pl * neg + k] = (int64_t)cw.start[v >> 1] + cw.off[b * neg + k];
+                s_neg[pl * neg + k] = cw.neg[b * neg + k];
+                s_dst[pl * neg + k] = cw.off[b * neg + k];   // resolved destination (k_scan_counts)
             }
         }
     }
     __syncthreads();
-    const int D = (int)P.dim;
     const int p = P.p_norm;
     const bool nf = P.norm_flag != 0;
     const int64_t hp = pd.h, rp = pd.r, tp = pd.t;
     const int64_t *mine = s_neg + pl * neg;
-    Vec H, T, Rr, W, nW, hh, th, rh, vpos;
     Vec E[NCH];
     Vec aH, aT, aR, aW;
     vzero(aH); vzero(aT); vzero(aR); vzero(aW);
@@ -685,10 +278,6 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
     Vec Hs, Ts;
     float hn = 0, tn = 0, hdot = 0, tdot = 0, ps = 0;
     if (active) {
-        vload(H, P.ent + hp * D, D, lane);
-        vload(T, P.ent + tp * D, D, lane);
-        vload(Rr, P.rel + rp * D, D, lane);
-        if constexpr (MODEL == 1) vload(W, P.normv + rp * D, D, lane);
         auto load_chunk = [&](int64_t c0) {
 #pragma unroll
             for (int k = 0; k < NCH; ++k)
@@ -698,7 +287,7 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
         // ---- positive forward
         Hs = H; Ts = T;
         if constexpr (MODEL == 1) {
-            vnormalize(W, nW);
+            vnormalize<true>(W, nW);
             hdot = vdot(H, nW);
             tdot = vdot(T, nW);
 #pragma unroll
@@ -708,21 +297,21 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
             }
         }
         if (nf) {
-            hn = vnormalize(Hs, hh);
-            vnormalize(Rr, rh);
-            tn = vnormalize(Ts, th);
+            hn = vnormalize<true>(Hs, hh);
+            vnormalize<true>(Rr, rh);
+            tn = vnormalize<true>(Ts, th);
         } else {
             hh = Hs; rh = Rr; th = Ts;
         }
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
-        ps = vpnorm(vpos, p);
+        ps = vpnorm<true>(vpos, p);
         const float m = P.margin, inv = P.inv_count;
         for (int64_t c0 = k_lo; c0 < k_hi;) {
 #pragma unroll
             for (int k = 0; k < NCH; ++k) {
                 if (c0 + k >= k_hi) break;
-                const int64_t v = mine[c0 + k];
+                const int32_t v = uni<G>((int32_t)mine[c0 + k]);
                 const int64_t e = v >> 1;
                 const bool tail_side = v & 1;
                 Vec Es = E[k], eh, vk;
@@ -732,16 +321,16 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
 #pragma unroll
                     for (int i = 0; i < Vec::N; ++i) Es.x[i] = E[k].x[i] - ed * nW.x[i];
                 }
-                if (nf) en = vnormalize(Es, eh); else eh = Es;
+                if (nf) en = vnormalize<true>(Es, eh); else eh = Es;
 #pragma unroll
                 for (int i = 0; i < Vec::N; ++i)
                     vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - eh.x[i] : (eh.x[i] + rh.x[i]) - th.x[i];
-                const float ns = vpnorm(vk, p);
-                const float a = ps - ns;
+                const float ns = vpnorm<true>(vk, p);
+                const float a = uni<G>(ps - ns);
                 lsum += a > -m ? a : -m;
                 const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
                 float *dst = nullptr;
-                if constexpr (CSR) dst = cw.contrib + s_dst[pl * neg + c0 + k] * D;
+                if constexpr (CSR) dst = cw.contrib + (int64_t)uni<G>((int32_t)s_dst[pl * neg + c0 + k]) * D;
                 if (c == 0.f) {
                     if constexpr (CSR) {   // the reserved slot must still be defined
                         Vec z;
@@ -752,7 +341,7 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
                 }
                 csum += c;
                 Vec gk, gs;
-                vpnorm_bwd(vk, ns, p, -c, gk);
+                vpnorm_bwd<true>(vk, ns, p, -c, gk);
 #pragma unroll
                 for (int i = 0; i < Vec::N; ++i) {
                     aR.x[i] += gk.x[i];
@@ -763,7 +352,7 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
                     if constexpr (CSR) vstore(gs, dst, D, lane); else sink.ent(e, gs, D, lane);
                 } else {
                     Vec gp, ge;
-                    if (nf) vnormalize_bwd(Es, en, gs, gp); else gp = gs;
+                    if (nf) vnormalize_bwd<true>(Es, en, gs, gp); else gp = gs;
                     const float ng = vdot(nW, gp);
 #pragma unroll
                     for (int i = 0; i < Vec::N; ++i) {
@@ -814,9 +403,9 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
     }
     if (!active) return;
     // ---- positive backward and the group's on-chip accumulators
-    if (csum != 0.f) {
+    if (uni<G>(csum) != 0.f) {
         Vec gv;
-        vpnorm_bwd(vpos, ps, p, csum, gv);
+        vpnorm_bwd<true>(vpos, ps, p, csum, gv);
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) {
             aH.x[i] += gv.x[i];
@@ -836,7 +425,7 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
                 const float enn = s2 == 0 ? hn : tn;
                 const float edd = s2 == 0 ? hdot : tdot;
                 Vec gp, ge;
-                if (nf) vnormalize_bwd(Esv, enn, acc, gp); else gp = acc;
+                if (nf) vnormalize_bwd<true>(Esv, enn, acc, gp); else gp = acc;
                 const float ng = vdot(nW, gp);
 #pragma unroll
                 for (int i = 0; i < Vec::N; ++i) {
@@ -1105,25 +694,6 @@ __global__ __launch_bounds__(256) void k_lp_min(const LpUniverseDev *__restrict_
 // ==================================================================== host launchers ===========
 namespace {
 
-struct Shape {
-    int G, VEC, KCH;
-};
-
-Shape pick_shape(int64_t D, bool vec4 = true) {
-    const int VEC = vec4 && D % 4 == 0 ? 4 : 1;
-    const int64_t chunks = D / VEC;
-    int G = 1;
-    while (G < chunks && G < 64) G <<= 1;
-    if (G < 2) G = 2;
-    int KCH = (int)((chunks + G - 1) / G);
-    if (VEC == 1) {   // VEC=1 instantiations exist for power-of-two chunk counts
-        int k = 1;
-        while (k < KCH) k <<= 1;
-        KCH = k;
-    }
-    return Shape{G, VEC, KCH};
-}
-
 // negatives held in registers per chunk: smallest of {1,4,8,32} >= neg, at most 128 VGPRs of rows
 int pick_nch(int64_t neg, int kch) {
     static const int opts[4] = {1, 4, 8, 32};
@@ -1135,11 +705,6 @@ int pick_nch(int64_t neg, int kch) {
     }
     return best;
 }
-
-#define PT_SHAPES(X)                                                                                  \
-    X(2, 4, 1) X(4, 4, 1) X(8, 4, 1) X(16, 4, 1) X(32, 4, 1) X(64, 4, 1) X(64, 4, 2)                 \
-    X(2, 1, 1) X(4, 1, 1) X(8, 1, 1) X(16, 1, 1) X(32, 1, 1) X(64, 1, 1) X(64, 1, 2) X(64, 1, 4)    \
-    X(64, 1, 8)
 
 // VEC=1 shapes x NCH x S of the sampled step kernel: S = 1 for neg < 8 (NCH covers neg), S = 4 with
 // NCH covering ceil(neg/4) (chunks beyond 32 negatives per sub-group loop)
@@ -1192,7 +757,7 @@ hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64
 hipError_t launch_scan_counts(const CsrWork &w, int64_t n, int64_t calls, uint64_t *states, int64_t threads,
                               int64_t bs, int64_t dpp, hipStream_t st) {
     hipLaunchKernelGGL(dev::k_scan_counts, dim3((unsigned)calls), dim3(1024), 0, st, w.cnt, w.start, n, states, threads,
-                       bs, dpp);
+                       bs, dpp, w, bs * ((dpp - 1) / 2));
     return hipGetLastError();
 }
 

@@ -33,7 +33,7 @@ class ModelDesc(ctypes.Structure):
 
 class UniverseJob(ctypes.Structure):
     _fields_ = [("graph", c_vp), ("seeds", c_vp), ("threads", c_i64), ("batch_size", c_i64), ("epochs", c_i64),
-                ("nbatches", c_i64), ("lr", c_f32), ("margin", c_f32), ("ent", c_vp), ("rel", c_vp),
+                ("nbatches", c_i64), ("neg", c_i64), ("lr", c_f32), ("margin", c_f32), ("ent", c_vp), ("rel", c_vp),
                 ("normv", c_vp), ("ent_acc", c_vp), ("rel_acc", c_vp), ("norm_acc", c_vp), ("dim", c_i64)]
 
 
@@ -79,8 +79,12 @@ SIGNATURES = {
     "pt_universe_remaps": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "pt_universe_graph": (c_vp, [c_vp]),
     "pt_universe_seeds": (ctypes.c_int, [c_vp, c_vp]),
-    "pt_universes_train": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i64, c_i64,
-                                          c_vp, c_vp]),
+    "pt_universe_set_create": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32,
+                                              c_i64, c_i64, ctypes.POINTER(c_vp)]),
+    "pt_universe_set_train": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "pt_universe_set_free": (ctypes.c_int, [c_vp]),
+    "pt_universes_train": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
+                                          c_i64, c_vp, c_vp]),
     "pt_lp_min_scores": (ctypes.c_int, [ctypes.POINTER(LpUniverse), c_i64, c_i32, c_i32, c_i32,
                                         ctypes.POINTER(LpPair), c_i64, c_i64, c_vp, c_vp]),
     "pt_known_create": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(c_vp)]),
