@@ -87,6 +87,121 @@ def cpu_baseline(path, wl, seconds=15.0):
                       "oracle/oracle.c single thread, %.1f s" % (steps, bs, neg, dim, el)}
 
 
+def universe_draws(k, seed0=4):
+    """Python-RNG hyperparameters of universe k exactly as Parallel_Universe_Config draws them
+    (:157-161, :210-236) with the PuTransE WN18 experiment's ranges
+    (experiments/static_experiment_PuTransE_on_WN18.py:67-88)."""
+    import random
+    rs = random.Random(seed0 + k)
+    tc = rs.randrange(500, 2000)
+    bal = round(rs.uniform(0.25, 0.5), 2)
+    margin = rs.randrange(1, 4)
+    epochs = rs.randrange(50, 200)
+    lr = round(rs.uniform(0.001, 0.1), 3)
+    return tc, bal, margin, epochs, lr
+
+
+def run_universes(args, ws, rank, dev, n_univ=512):
+    """C3: PuTransE on WN18-shaped data, 512 universes with D ~ U{20..100}, Adagrad, neg 1, bern 0,
+    filter 0, nbatches 20, 8 sampler threads; universe k on rank k % N (strong scaling, no collective).
+    One step = every universe's full training run (all its epochs) in one persistent launch per shape."""
+    import synth_kg
+    from openke import _native
+    L = _native.lib()
+    path = synth_kg.ensure_dataset(os.path.join(args.data_dir, "rank%d" % rank), "wn18")
+    g = ctypes.c_void_p()
+    _native.check(L.pt_graph_load(path.encode(), ctypes.byref(g)))
+    own = [k for k in range(n_univ) if k % ws == rank]
+    draws = [universe_draws(k) for k in own]
+    dims = [int(np.random.default_rng(1000 + k).integers(20, 101)) for k in own]
+    seeds = np.array([4 + k for k in own], dtype=np.int64)
+    tcs = np.array([d[0] for d in draws], dtype=np.int64)
+    bals = np.array([d[1] for d in draws], dtype=np.float32)
+    handles = (ctypes.c_void_p * max(len(own), 1))()
+    t0 = time.perf_counter()
+    _native.check(L.pt_universe_build_many(g, len(own), seeds.ctypes.data, 8, tcs.ctypes.data, bals.ctypes.data, 0,
+                                           handles))
+    build_s = time.perf_counter() - t0
+    jobs, keep = [], []
+    slots_step, bytes_step = 0, 0
+    for i, k in enumerate(own):
+        h = handles[i]
+        E, R, N = L.pt_universe_ent_total(h), L.pt_universe_rel_total(h), L.pt_universe_train_total(h)
+        D = dims[i]
+        rng = np.random.default_rng(k)
+        b = np.sqrt(6.0 / (E + D))
+        ent = torch.from_numpy(rng.uniform(-b, b, (E, D)).astype(np.float32)).to(dev)
+        b = np.sqrt(6.0 / (R + D))
+        rel = torch.from_numpy(rng.uniform(-b, b, (R, D)).astype(np.float32)).to(dev)
+        accs = (torch.zeros_like(ent), torch.zeros_like(rel))
+        st = np.zeros(8, dtype=np.uint64)
+        _native.check(L.pt_universe_seeds(h, st.ctypes.data))
+        tc, bal, margin, epochs, lr = draws[i]
+        bs = N // 20
+        j = _native.UniverseJob()
+        j.graph = L.pt_universe_graph(h)
+        j.seeds = st.ctypes.data
+        j.threads, j.batch_size, j.epochs, j.nbatches, j.neg = 8, bs, epochs, 20, 1
+        j.lr, j.margin = lr, margin
+        j.ent, j.rel, j.normv = ent.data_ptr(), rel.data_ptr(), None
+        j.ent_acc, j.rel_acc, j.norm_acc = accs[0].data_ptr(), accs[1].data_ptr(), None
+        j.dim = D
+        jobs.append(j)
+        keep.append((st, ent, rel, accs))
+        slots = epochs * 20 * bs * 2
+        slots_step += slots
+        bytes_step += slots * algorithmic_bytes_per_slot("TransE", "adagrad", D)
+    arr = (_native.UniverseJob * max(len(jobs), 1))(*jobs)
+    uset = ctypes.c_void_p()
+    _native.check(L.pt_universe_set_create(arr, len(jobs), 0, 1, 1, _native.PT_ADAGRAD, 0, 0, ctypes.byref(uset)))
+    total_epochs = sum(int(j.epochs) for j in jobs)
+    losses = torch.zeros(max(total_epochs, 1), device=dev)
+    stream = _native.stream()
+    for _ in range(args.c3_warmup):
+        _native.check(L.pt_universe_set_train(uset, _native.ptr(losses), stream))
+    torch.cuda.synchronize()
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.c3_steps):
+        _native.check(L.pt_universe_set_train(uset, _native.ptr(losses), stream))
+    torch.cuda.synchronize()
+    barrier(ws)
+    el = time.perf_counter() - t0
+    tot = torch.tensor([el, float(slots_step), float(bytes_step)], dtype=torch.float64, device=dev)
+    if ws > 1:
+        import torch.distributed as dist
+        mx = tot[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        el = float(mx.item())
+    slots_all, bytes_all = float(tot[1].item()), float(tot[2].item())
+    assert torch.isfinite(losses).all(), "non-finite universe loss"
+    if os.environ.get("PT_UNI_PROF") == "1":
+        prof = np.zeros(4 * max(len(jobs), 1), dtype=np.uint64)
+        _native.check(L.pt_universe_set_profile(uset, prof.ctypes.data))
+        prof = prof.reshape(-1, 4).astype(np.float64)
+        order = np.argsort(-prof[:, 3])
+        for i in order[:5]:
+            steps = max(prof[i, 3], 1)
+            print("universe-prof steps %d  cycles/step: presample %.0f  A %.0f  B %.0f" %
+                  (steps, prof[i, 0] / steps, prof[i, 1] / steps, prof[i, 2] / steps), file=sys.stderr)
+        tot = prof[:, :3].sum(axis=0) / max(prof[:, 3].sum(), 1)
+        print("universe-prof all: cycles/step presample %.0f A %.0f B %.0f" % tuple(tot), file=sys.stderr)
+    _native.check(L.pt_universe_set_free(uset))
+    for i in range(len(own)):
+        L.pt_universe_free(handles[i])
+    L.pt_graph_free(g)
+    achieved = bytes_all * args.c3_steps / el / 1e9 / max(ws, 1)
+    return {"workload": "C3 PuTransE wn18-shaped, %d universes, D~U{20..100}, tc~U[500,2000), epochs~U[50,200), "
+                        "Adagrad, neg 1, nbatches 20" % n_univ,
+            "value": slots_all * args.c3_steps / el, "unit": "triples/s", "scaling": "strong",
+            "steps": args.c3_steps, "warmup": args.c3_warmup, "s_per_step": el / args.c3_steps,
+            "universes_per_gpu": len(own), "host_universe_build_s": build_s,
+            "roofline": {"bound": "latency (per-universe dependent step chain)", "achieved_per_gpu": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}}
+
+
 def load_traffic(tag):
     """Per-launch HBM bytes of k_step + k_apply from a committed rocprofv3 --pmc summary, if present."""
     f = os.path.join(HERE, "profiles", "pmc_%s.json" % tag)
@@ -103,13 +218,32 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS) + ["c3"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "putranse_bench"))
+    ap.add_argument("--no-c3", action="store_true", help="skip the PuTransE universe workload (C3) field")
+    ap.add_argument("--c3-steps", type=int, default=2)
+    ap.add_argument("--c3-warmup", type=int, default=1)
     args = ap.parse_args()
 
     ws, rank, local = dist_setup()
+    if args.workload == "c3":
+        dev = torch.device("cuda", torch.cuda.current_device())
+        args.c3_steps, args.c3_warmup = args.steps, args.warmup
+        c3 = run_universes(args, ws, rank, dev)
+        if rank == 0:
+            rec = {"metric": "training triples/sec (pos+neg)", "value": c3["value"], "unit": "triples/s",
+                   "n_gpus": ws, "steps": args.steps, "warmup": args.warmup, "ms_per_step": c3["s_per_step"] * 1e3,
+                   "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+                   "data": "synthetic wn18-shaped graph (tools/synth_kg.py, seed 0), xavier-uniform tables",
+                   "config": {"workload": c3["workload"], "parallelism": "universes sharded k %% %d" % ws},
+                   "roofline": c3["roofline"], "universes_per_gpu": c3["universes_per_gpu"]}
+            print(json.dumps(rec), flush=True)
+        if ws > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
     wl = WORKLOADS[args.workload]
     shape, model, dim, p, opt, lr, margin, bs, neg, bern, filt = wl
 
@@ -176,6 +310,7 @@ def main():
     bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
     achieved = bytes_step / (sum(per_kernel.values()) * 1e-3) / 1e9
 
+    c3 = None if args.no_c3 else run_universes(args, ws, rank, dev)
     if rank != 0:
         if ws > 1:
             import torch.distributed as dist
@@ -207,6 +342,8 @@ def main():
                      "algorithmic_bytes_per_step": bytes_step},
         "loss_last_step": loss_last,
     }
+    if c3 is not None:
+        rec["pu_c3"] = c3
     if ws == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(path, wl, args.cpu_seconds)
     print(json.dumps(rec), flush=True)

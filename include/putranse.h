@@ -158,6 +158,9 @@ int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, int32_t model
  * [sum of epochs] floats, job-order concatenation of Trainer.run's per-epoch loss sums */
 int pt_universe_set_train(pt_universe_set *s, float *d_losses, void *stream);
 int pt_universe_set_free(pt_universe_set *s);
+/* diagnostics of a set created with PT_UNI_PROF=1 in the environment: per universe (in the set's
+ * launch order) shader-clock cycles spent in epoch presampling, phase A, phase B, and the step count */
+int pt_universe_set_profile(pt_universe_set *s, uint64_t *out);
 /* create + train + free (synchronizes `stream`) */
 int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm, int32_t norm_flag,
                        int32_t opt, int64_t bern, int64_t filter, float *d_losses, void *stream);
@@ -167,7 +170,8 @@ int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, in
  * (obtain_embedding_space_score + transmit_max_scores, Parallel_Universe_Config.py:446-465, :516-543).
  * d_key_rows: [n_keys][global_ent_total] fp32 device buffer (init +inf). A pair names one universe
  * holding both the key's anchor entity and relation: every local entity e of that universe is scored
- * as the missing side (side 0: tail prediction, (anchor, r, e); side 1: head prediction, (e, r, anchor))
+ * as the missing side (side 0: head prediction, (e, r, anchor); side 1: tail prediction, (anchor, r, e);
+ * the same side convention as pt_rank_queries / pt_known_partners)
  * and MIN-reduced into row `key` at column ent_remap[e]. Universes of different dims may be mixed. */
 typedef struct {
     const float *ent, *rel, *normv;        /* device tables of the universe */
@@ -179,7 +183,19 @@ typedef struct {
 } pt_lp_pair;
 int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, int32_t model, int32_t p_norm,
                      int32_t norm_flag, const pt_lp_pair *pairs, int64_t n_pairs, int64_t global_ent_total,
-                     float *d_key_rows, void *stream);
+                     float *d_key_rows, float *d_key_tuple, void *stream);
+/* d_key_tuple (optional, [n_keys], init +inf): MIN over the pairs' universes of the null_vector score
+ * _calc(anchor, 0, r) / _calc(0, anchor, r) on the raw anchor row (calc_tuple_score,
+ * Parallel_Universe_Config.py:405-416, transmit_tuple_max_score :494-514) */
+
+/* Ranks straight from global-order score rows (device): query q is ranked on row d_row_of[q] with
+ * truth entity d_truth[q]; +inf entries are replaced by d_repl[q] when d_repl is non-NULL
+ * (missing_embedding_handling = 'null_vector'); d_part_off/d_part = CSR of the known partners of the
+ * query's (anchor, r) (pt_known_partners). Same raw / filtered counts as testHead/testTail on the
+ * candidate-order vector (Test.h:118-359) and validHead/validTail (Valid.h:117-240). */
+int pt_rank_rows(const float *d_rows, int64_t ent_total, const int64_t *d_row_of, const int64_t *d_truth,
+                 const float *d_repl, const int64_t *d_part_off, const int64_t *d_part, int64_t n, int64_t *d_raw,
+                 int64_t *d_filt, void *stream);
 
 /* Filtered / raw ranks (testHead/testTail, Test.h:118-359) for many queries at once on host threads:
  * con rows [n][ent_total] in candidate order, anchors per query. Known-triple set from
@@ -187,6 +203,10 @@ int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, int32_t mode
 typedef struct pt_known pt_known;
 int pt_known_create(const int64_t *h, const int64_t *t, const int64_t *r, int64_t n, pt_known **out);
 int pt_known_free(pt_known *k);
+/* CSR of the known partners of (anchor[q], rel[q]): side 0 = heads h of known (h, anchor, r), side 1 =
+ * tails t of known (anchor, t, r). off has n + 1 entries; with list == NULL only the offsets are filled. */
+int pt_known_partners(const pt_known *k, int32_t side, int64_t n, const int64_t *anchor, const int64_t *rel,
+                      int64_t *off, int64_t *list);
 int pt_rank_queries(const pt_known *k, int64_t ent_total, const int64_t *h, const int64_t *t, const int64_t *r,
                     int64_t n, int32_t side, const float *con, int64_t *raw, int64_t *filt, int64_t n_workers);
 
@@ -199,6 +219,8 @@ int64_t pt_legacy_bern(void);
  * count, fills the arrays when non-NULL. The known-triple set used by the filtered rank. */
 int64_t pt_legacy_eval_triples(int32_t valid, int64_t *h, int64_t *t, int64_t *r);
 const pt_known *pt_legacy_known(void);
+/* the global context's full training graph (importTrainFiles), e.g. for pt_universe_build_many */
+pt_graph *pt_legacy_graph(void);
 
 /* ------------------------------------------------------------------ B: Base.so-compatible ---- */
 /* Same names and semantics as the reference (see file:line per symbol in DESIGN.md §Boundary). */

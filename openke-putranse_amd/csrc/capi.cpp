@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -565,19 +566,15 @@ struct pt_universe_set {
     int64_t bern = 0, filter = 0, neg = 1;
     int device = -1;
     void *arena = nullptr;
-    struct Group {
-        pt::Shape shape;
-        pt::UniverseDev *d_us = nullptr;   // inside the arena
-        int64_t n = 0, list_cap = 0;
-        std::vector<int64_t> loss_off;     // per universe of the group: offset into d_losses
-    };
-    std::vector<Group> groups;
-    std::vector<pt::UniverseDev> host;    // by group, loss pointers patched per train call
+    pt::UniverseDev *d_us = nullptr;      // inside the arena, longest-first order
+    int *d_counter = nullptr;             // work-queue counter (inside the arena)
+    pt::UniverseLaunch cfg;
+    std::vector<pt::UniverseDev> host;    // same order; loss pointers patched per train call
     std::vector<int64_t> host_loss_off;
-    std::vector<hipStream_t> streams;
+    uint64_t *prof = nullptr;             // PT_UNI_PROF=1: [n][4] cycle counters (device)
     ~pt_universe_set() {
-        for (auto s : streams) (void)hipStreamDestroy(s);
         if (arena) (void)hipFree(arena);
+        if (prof) (void)hipFree(prof);
     }
 };
 
@@ -592,11 +589,17 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     set->model = model; set->p_norm = p_norm; set->norm_flag = norm_flag; set->opt = opt;
     set->bern = bern; set->filter = filter;
     PT_HIP(hipGetDevice(&set->device));
+    if (const char *v = getenv("PT_UNI_PROF")) {
+        if (atoi(v) && n > 0) {
+            PT_HIP(hipMalloc((void **)&set->prof, 32 * (size_t)n));
+            PT_HIP(hipMemset(set->prof, 0, 32 * (size_t)n));
+        }
+    }
     int64_t neg = -1;
     // layout of the per-universe workspace in one arena
     auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
     struct Slot {
-        int64_t states, grad, flags;
+        int64_t states, contrib, grad, flags;
     };
     std::vector<Slot> slots((size_t)n);
     int64_t total = 0;
@@ -607,7 +610,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         PT_CHECK(opt == PT_SGD || (J.ent_acc && J.rel_acc && (model == 0 || J.norm_acc)), PT_EINVAL,
                  "Adagrad universe job needs accumulators");
         PT_CHECK(J.threads > 0 && J.threads <= 64, PT_EINVAL, "universe job: threads must be in [1, 64]");
-        PT_CHECK(J.dim > 0 && pt::shape_supported(J.dim), PT_EINVAL, "universe job: unsupported dim");
+        PT_CHECK(J.dim > 0 && pt::universe_shape_supported(J.dim), PT_EINVAL, "universe job: unsupported dim");
         PT_CHECK(J.batch_size >= 0 && J.epochs >= 0 && J.nbatches >= 0, PT_EINVAL, "universe job: negative sizes");
         PT_CHECK(neg < 0 || J.neg == neg, PT_EINVAL, "universe jobs must share neg");
         PT_CHECK(J.neg >= 1, PT_EINVAL, "universe job: neg must be >= 1");
@@ -617,21 +620,33 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         PT_CHECK(J.batch_size * (4 + J.neg) <= 16384, PT_EINVAL, "universe job: batch too large for the LDS work list");
         const int64_t rows = g.ent_total + g.rel_total * (model == 1 ? 2 : 1);
         slots[i].states = total; total += al(8 * J.threads);
+        slots[i].contrib = total; total += al(4 * J.batch_size * (2 + J.neg) * J.dim);
         slots[i].grad = total;   total += al(4 * rows * J.dim);
         slots[i].flags = total;  total += al(4 * (g.ent_total + 2 * g.rel_total));
     }
     set->neg = neg < 0 ? 1 : neg;
     const int64_t us_off = total;
     total += al((int64_t)sizeof(pt::UniverseDev) * std::max<int64_t>(n, 1));
+    const int64_t counter_off = total;
+    total += al(sizeof(int));
     PT_HIP(hipMalloc(&set->arena, (size_t)total));
     char *base = (char *)set->arena;
     PT_HIP(hipMemset(base, 0, (size_t)us_off));
-    // group by row shape
-    std::map<std::tuple<int, int, int>, std::vector<int64_t>> by_shape;
-    for (int64_t i = 0; i < n; ++i) {
-        const pt::Shape s = pt::pick_shape(jobs[i].dim);
-        by_shape[std::make_tuple(s.G, s.VEC, s.KCH)].push_back(i);
-    }
+    // LDS budget per universe workgroup: the device's per-workgroup limit, at most half a CU (so two
+    // universes share a CU), minus the kernel's static LDS
+    int max_lds = 64 << 10;
+    (void)hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, set->device);
+    const int64_t lds_budget = std::min<int64_t>(max_lds, 80 << 10) - 1024;
+    // one persistent launch over all universes, longest dependent step chain first (the work queue
+    // then approximates longest-processing-time scheduling over the CUs)
+    std::vector<int64_t> order((size_t)n);
+    for (int64_t i = 0; i < n; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+        return jobs[a].epochs * jobs[a].nbatches * std::max<int64_t>(jobs[a].batch_size, 1) >
+               jobs[b].epochs * jobs[b].nbatches * std::max<int64_t>(jobs[b].batch_size, 1);
+    });
+    set->d_us = (pt::UniverseDev *)(base + us_off);
+    set->d_counter = (int *)(base + counter_off);
     set->host.reserve((size_t)n);
     int64_t loss_off = 0;
     std::vector<int64_t> loss_of((size_t)n);
@@ -639,45 +654,77 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         loss_of[i] = loss_off;
         loss_off += jobs[i].epochs;
     }
-    std::vector<uint64_t> states_h;
-    for (auto &kv : by_shape) {
-        pt_universe_set::Group grp;
-        grp.shape = pt::Shape{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first)};
-        grp.d_us = (pt::UniverseDev *)(base + us_off) + set->host.size();
-        grp.n = (int64_t)kv.second.size();
-        for (int64_t i : kv.second) {
-            const pt_universe_job &J = jobs[i];
-            pt::Graph &g = const_cast<pt::Graph &>(reinterpret_cast<const pt_graph *>(J.graph)->g);
-            int rc = g.upload();
-            if (rc) return rc;
-            pt::UniverseDev U{};
-            U.g = g.dev;
-            U.states = (uint64_t *)(base + slots[i].states);
-            PT_HIP(hipMemcpy(U.states, J.seeds, 8 * J.threads, hipMemcpyHostToDevice));
-            U.ent = J.ent; U.rel = J.rel; U.normv = J.normv;
-            U.ent_acc = J.ent_acc; U.rel_acc = J.rel_acc; U.norm_acc = J.norm_acc;
-            float *gr = (float *)(base + slots[i].grad);
-            U.gent = gr;
-            U.grel = gr + g.ent_total * J.dim;
-            U.gnorm = model == 1 ? U.grel + g.rel_total * J.dim : nullptr;
-            int32_t *fl = (int32_t *)(base + slots[i].flags);
-            U.fent = fl;
-            U.frel = fl + g.ent_total;
-            U.fnorm = U.frel + g.rel_total;
-            U.losses = nullptr;
-            U.threads = J.threads; U.bs = J.batch_size; U.nbatches = J.nbatches; U.epochs = J.epochs; U.dim = J.dim;
-            U.lr = J.lr; U.margin = J.margin;
-            set->host.push_back(U);
-            set->host_loss_off.push_back(loss_of[i]);
-            grp.list_cap = std::max(grp.list_cap, std::max<int64_t>(J.batch_size * (4 + J.neg), 1));
-        }
-        set->groups.push_back(std::move(grp));
+    int64_t max_bs = 0, max_flags = 0, max_relg = 0, max_ent = 0, max_rel = 0, max_seq = 0, max_nb = 0;
+    for (int64_t i : order) {
+        const pt_universe_job &J = jobs[i];
+        pt::Graph &g = const_cast<pt::Graph &>(reinterpret_cast<const pt_graph *>(J.graph)->g);
+        int rc = g.upload();
+        if (rc) return rc;
+        pt::UniverseDev U{};
+        U.g = g.dev;
+        U.states = (uint64_t *)(base + slots[i].states);
+        PT_HIP(hipMemcpy(U.states, J.seeds, 8 * J.threads, hipMemcpyHostToDevice));
+        U.ent = J.ent; U.rel = J.rel; U.normv = J.normv;
+        U.ent_acc = J.ent_acc; U.rel_acc = J.rel_acc; U.norm_acc = J.norm_acc;
+        float *gr = (float *)(base + slots[i].grad);
+        U.gent = gr;
+        U.grel = gr + g.ent_total * J.dim;
+        U.gnorm = model == 1 ? U.grel + g.rel_total * J.dim : nullptr;
+        int32_t *fl = (int32_t *)(base + slots[i].flags);
+        U.fent = fl;
+        U.frel = fl + g.ent_total;
+        U.fnorm = U.frel + g.rel_total;
+        U.contrib = (float *)(base + slots[i].contrib);
+        U.losses = nullptr;
+        U.prof = set->prof ? set->prof + 4 * (int64_t)set->host.size() : nullptr;
+        U.threads = J.threads; U.bs = J.batch_size; U.nbatches = J.nbatches; U.epochs = J.epochs; U.dim = J.dim;
+        U.lr = J.lr; U.margin = J.margin;
+        U.shape = pt::universe_shape_id(J.dim);
+        set->host.push_back(U);
+        set->host_loss_off.push_back(loss_of[i]);
+        max_bs = std::max(max_bs, J.batch_size);
+        max_flags = std::max(max_flags, g.ent_total + 2 * g.rel_total);
+        max_relg = std::max(max_relg, g.rel_total * J.dim);
+        max_ent = std::max(max_ent, g.ent_total);
+        max_rel = std::max(max_rel, g.rel_total);
+        max_seq = std::max(max_seq, J.batch_size * (1 + J.neg));
+        max_nb = std::max(max_nb, J.nbatches);
     }
-    for (size_t i = 0; i < set->groups.size(); ++i) {
-        hipStream_t s;
-        PT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        set->streams.push_back(s);
-    }
+    // LDS plan (within the device's per-workgroup limit and half a CU): the work list is required;
+    // then, each if it still fits, the relation gradient rows (the contended rows of the scatter), the
+    // entity contribution lists (replace the entity float atomics), the touched flags, and as many
+    // presampled batches as fit
+    auto &C = set->cfg;
+    C.list_cap = std::max<int64_t>(max_bs * (4 + set->neg), 1);
+    auto a4 = [](int64_t v) { return 4 * ((v + 3) & ~int64_t(3)); };
+    const int64_t list_b = a4(C.list_cap);
+    const int64_t relg_b = 4 * max_relg * (model == 1 ? 2 : 1);
+    const int64_t contrib_b = a4(max_ent) + a4(max_bs * (2 + set->neg));
+    int64_t used = list_b;
+    auto env_on = [](const char *name) {
+        const char *v = getenv(name);
+        return !v || atoi(v) != 0;
+    };
+    PT_CHECK(used <= lds_budget, PT_EINVAL, "universe batch too large for the LDS work list");
+    C.lds_relgrad = used + relg_b <= lds_budget && env_on("PT_UNI_RELGRAD");
+    used += C.lds_relgrad ? relg_b : 0;
+    C.contrib = used + contrib_b + a4(2 * max_rel) <= lds_budget && env_on("PT_UNI_CONTRIB");
+    used += C.contrib ? contrib_b : 0;
+    const int64_t flags_b = C.contrib ? a4(2 * max_rel) : a4(max_flags);
+    C.lds_flags = used + flags_b <= lds_budget && env_on("PT_UNI_LDSFLAGS");
+    used += C.lds_flags ? flags_b : 0;
+    const int64_t per_batch = 12 * max_seq;
+    C.pchunk = env_on("PT_UNI_PRESAMPLE") && per_batch > 0 ? std::min<int64_t>(max_nb, (lds_budget - used) / per_batch)
+                                                            : 0;
+    if (C.pchunk < 0) C.pchunk = 0;
+    used += C.pchunk * per_batch;
+    C.lds_bytes = used;
+    // agent-scope fences only while some gradient row is a global float atomic
+    C.agent_fence = !(C.contrib && C.lds_relgrad && C.lds_flags);
+    if (const char *v = getenv("PT_UNI_FENCE")) C.agent_fence = C.agent_fence || atoi(v) != 0;
+    C.threads = 512;
+    // tuning overrides (benchmarks): PT_UNI_RELGRAD / CONTRIB / LDSFLAGS / PRESAMPLE = 0 disable the
+    // LDS placements above, PT_UNI_FENCE=1 forces agent-scope fences
     *out = set.release();
     return PT_OK;
 }
@@ -685,32 +732,27 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
 extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void *stream) {
     PT_CHECK(set, PT_EINVAL, "null universe set");
     if (set->host.empty()) return PT_OK;
-    hipStream_t user = (hipStream_t)stream;
+    hipStream_t st = (hipStream_t)stream;
     for (size_t i = 0; i < set->host.size(); ++i)
         set->host[i].losses = d_losses ? d_losses + set->host_loss_off[i] : nullptr;
-    PT_HIP(hipMemcpyAsync(set->groups[0].d_us, set->host.data(), sizeof(pt::UniverseDev) * set->host.size(),
-                          hipMemcpyHostToDevice, user));
-    hipEvent_t start;
-    PT_HIP(hipEventCreateWithFlags(&start, hipEventDisableTiming));
-    PT_HIP(hipEventRecord(start, user));
-    int rc = PT_OK;
-    for (size_t k = 0; k < set->groups.size() && !rc; ++k) {
-        const auto &G = set->groups[k];
-        hipStream_t s = set->streams[k];
-        if (hipStreamWaitEvent(s, start, 0) != hipSuccess) { rc = pt::fail(PT_EHIP, "hipStreamWaitEvent"); break; }
-        const hipError_t e = pt::launch_universes(G.d_us, G.n, G.shape, set->model, set->p_norm, set->norm_flag,
-                                                  set->opt, set->neg, (int)set->bern, (int)set->filter, G.list_cap, s);
-        if (e != hipSuccess) rc = pt::fail(PT_EHIP, std::string("launch_universes: ") + hipGetErrorString(e));
-    }
-    for (size_t k = 0; k < set->groups.size(); ++k) {
-        hipEvent_t done;
-        (void)hipEventCreateWithFlags(&done, hipEventDisableTiming);
-        (void)hipEventRecord(done, set->streams[k]);
-        (void)hipStreamWaitEvent(user, done, 0);
-        (void)hipEventDestroy(done);
-    }
-    (void)hipEventDestroy(start);
-    return rc;
+    PT_HIP(hipMemcpyAsync(set->d_us, set->host.data(), sizeof(pt::UniverseDev) * set->host.size(),
+                          hipMemcpyHostToDevice, st));
+    const hipError_t e = pt::launch_universes(set->d_us, (int64_t)set->host.size(), set->d_counter, set->model,
+                                              set->p_norm, set->norm_flag, set->opt, set->neg, (int)set->bern,
+                                              (int)set->filter, set->cfg, st);
+    if (e != hipSuccess) return pt::fail(PT_EHIP, std::string("launch_universes: ") + hipGetErrorString(e));
+    // the host array must outlive the async copy: this call returns only after it has been consumed
+    PT_HIP(hipStreamSynchronize(st));
+    return PT_OK;
+}
+
+// PT_UNI_PROF diagnostics: per universe (set order) cycles in presampling / phase A / phase B and steps
+extern "C" int pt_universe_set_profile(pt_universe_set *set, uint64_t *out) {
+    PT_CHECK(set && out, PT_EINVAL, "null argument");
+    PT_CHECK(set->prof, PT_ESTATE, "set created without PT_UNI_PROF=1");
+    PT_HIP(hipDeviceSynchronize());
+    PT_HIP(hipMemcpy(out, set->prof, 32 * set->host.size(), hipMemcpyDeviceToHost));
+    return PT_OK;
 }
 
 extern "C" int pt_universe_set_free(pt_universe_set *set) {
@@ -735,7 +777,7 @@ extern "C" int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_
 // ======================================================================== link prediction =======
 extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, int32_t model, int32_t p_norm,
                                 int32_t norm_flag, const pt_lp_pair *pairs, int64_t n_pairs,
-                                int64_t global_ent_total, float *d_key_rows, void *stream) {
+                                int64_t global_ent_total, float *d_key_rows, float *d_key_tuple, void *stream) {
     PT_CHECK((us && pairs && d_key_rows) || n_pairs == 0, PT_EINVAL, "pt_lp_min_scores: null argument");
     if (n_pairs == 0) return PT_OK;
     hipStream_t st = (hipStream_t)stream;
@@ -767,12 +809,23 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
             PT_HIP(hipMallocAsync((void **)&dp, sizeof(pt::LpPair) * cnt, st));
             PT_HIP(hipMemcpyAsync(dp, v.data() + off, sizeof(pt::LpPair) * cnt, hipMemcpyHostToDevice, st));
             PT_HIP(pt::launch_lp_min(du, dp, (int64_t)cnt, kv.first, max_ent[kv.first], model, p_norm, norm_flag,
-                                     global_ent_total, d_key_rows, st));
+                                     global_ent_total, d_key_rows, d_key_tuple, st));
             PT_HIP(hipFreeAsync(dp, st));
         }
     }
     PT_HIP(hipFreeAsync(du, st));
     PT_HIP(hipStreamSynchronize(st));   // host vectors above must outlive the async copies
+    return PT_OK;
+}
+
+extern "C" int pt_rank_rows(const float *d_rows, int64_t ent_total, const int64_t *d_row_of, const int64_t *d_truth,
+                            const float *d_repl, const int64_t *d_part_off, const int64_t *d_part, int64_t n,
+                            int64_t *d_raw, int64_t *d_filt, void *stream) {
+    if (n == 0) return PT_OK;
+    PT_CHECK(d_rows && d_row_of && d_truth && d_part_off && d_raw && d_filt && ent_total > 0, PT_EINVAL,
+             "pt_rank_rows: null argument");
+    PT_HIP(pt::launch_rank_rows(d_rows, ent_total, d_row_of, d_truth, d_repl, d_part_off, d_part, n, d_raw, d_filt,
+                                (hipStream_t)stream));
     return PT_OK;
 }
 
@@ -956,6 +1009,10 @@ extern "C" int64_t pt_legacy_eval_triples(int32_t valid, int64_t *h, int64_t *t,
     return (int64_t)v.size();
 }
 extern "C" const pt_known *pt_legacy_known(void) { return L().known; }
+extern "C" pt_graph *pt_legacy_graph(void) {
+    // the full training graph of importTrainFiles (never the swapped universe): pt_graph wraps pt::Graph
+    return reinterpret_cast<pt_graph *>(L().train.get());
+}
 
 extern "C" void getParallelUniverse(int64_t tc, float balance) {
     Legacy &l = L();

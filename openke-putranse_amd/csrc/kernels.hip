@@ -637,10 +637,12 @@ __global__ __launch_bounds__(256) void k_score_queries(StepParams P, int side, c
 // ---------------------------------------------------------------- universe link prediction ------
 // For a (key, universe) pair: score every local entity of the universe as the missing side and MIN
 // it into the key's global score row (scores are norms >= 0, so float order == int order).
+// side 0 = head prediction (anchor is the tail: e + (r - anchor)), side 1 = tail prediction
+// (anchor is the head: (anchor + r) - e).
 template <int MODEL, int G, int VEC, int KCH>
 __global__ __launch_bounds__(256) void k_lp_min(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
                                                 int64_t n_pairs, int p_norm, int norm_flag, int64_t global_E,
-                                                float *__restrict__ rows) {
+                                                float *__restrict__ rows, float *__restrict__ tuple_min) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = 256 / G;
     const int lane = threadIdx.x % G;
@@ -654,6 +656,22 @@ __global__ __launch_bounds__(256) void k_lp_min(const LpUniverseDev *__restrict_
     vload(A, U.ent + (int64_t)pr.anchor * D, D, lane);
     vload(R, U.rel + (int64_t)pr.rel * D, D, lane);
     float adot = 0.f;
+    if (tuple_min && blockIdx.x == 0 && grp == 0) {
+        // null_vector fallback score of the key in this universe: _calc on the RAW anchor row against a
+        // zero vector, ||a^ + r^ - 0|| (tail side) or ||0 + r^ - a^|| (head side)
+        // (Parallel_Universe_Config.py:405-416 calc_tuple_score, :545-554)
+        Vec an, rn, v;
+        if (norm_flag) {
+            vnormalize(A, an);
+            vnormalize(R, rn);
+        } else {
+            an = A; rn = R;
+        }
+#pragma unroll
+        for (int k = 0; k < Vec::N; ++k) v.x[k] = pr.side == 0 ? rn.x[k] - an.x[k] : an.x[k] + rn.x[k];
+        const float s = vpnorm(v, p_norm);
+        if (lane == 0) atomicMin(reinterpret_cast<int *>(tuple_min + pr.key), __float_as_int(s));
+    }
     if constexpr (MODEL == 1) {
         Vec W;
         vload(W, U.normv + (int64_t)pr.rel * D, D, lane);
@@ -671,7 +689,7 @@ __global__ __launch_bounds__(256) void k_lp_min(const LpUniverseDev *__restrict_
     // head prediction: score = e + (r - t); tail prediction: (h + r) - e   (TransE.py:56-59)
     Vec base;
 #pragma unroll
-    for (int k = 0; k < Vec::N; ++k) base.x[k] = pr.side == 1 ? rh.x[k] - ah.x[k] : ah.x[k] + rh.x[k];
+    for (int k = 0; k < Vec::N; ++k) base.x[k] = pr.side == 0 ? rh.x[k] - ah.x[k] : ah.x[k] + rh.x[k];
     float *out = rows + (int64_t)pr.key * global_E;
     for (int64_t e = (int64_t)blockIdx.x * GPB + grp; e < U.ent_total; e += (int64_t)gridDim.x * GPB) {
         Vec X, xh, v;
@@ -683,7 +701,7 @@ __global__ __launch_bounds__(256) void k_lp_min(const LpUniverseDev *__restrict_
         }
         if (norm_flag) vnormalize(X, xh); else xh = X;
 #pragma unroll
-        for (int k = 0; k < Vec::N; ++k) v.x[k] = pr.side == 1 ? xh.x[k] + base.x[k] : base.x[k] - xh.x[k];
+        for (int k = 0; k < Vec::N; ++k) v.x[k] = pr.side == 0 ? xh.x[k] + base.x[k] : base.x[k] - xh.x[k];
         const float s = vpnorm(v, p_norm);
         if (lane == 0) atomicMin(reinterpret_cast<int *>(out + U.remap[e]), __float_as_int(s));
     }
@@ -894,7 +912,8 @@ hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh
 }
 
 hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, int64_t dim, int64_t max_ent,
-                         int model, int p_norm, int norm_flag, int64_t global_E, float *rows, hipStream_t st) {
+                         int model, int p_norm, int norm_flag, int64_t global_E, float *rows, float *tuple_min,
+                         hipStream_t st) {
     if (n_pairs <= 0) return hipSuccess;
     const Shape s = pick_shape(dim);
     const int64_t gpb = 256 / s.G;
@@ -906,10 +925,10 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
     if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                                              \
         if (model == 0)                                                                                           \
             hipLaunchKernelGGL((dev::k_lp_min<0, G_, V_, K_>), grid, block, 0, st, us, pairs, n_pairs, p_norm,    \
-                               norm_flag, global_E, rows);                                                        \
+                               norm_flag, global_E, rows, tuple_min);                                             \
         else                                                                                                      \
             hipLaunchKernelGGL((dev::k_lp_min<1, G_, V_, K_>), grid, block, 0, st, us, pairs, n_pairs, p_norm,    \
-                               norm_flag, global_E, rows);                                                        \
+                               norm_flag, global_E, rows, tuple_min);                                             \
         return hipGetLastError();                                                                               \
     }
     PT_SHAPES(PT_LP)

@@ -2,8 +2,11 @@
 // with the known-triple filter (_find over tripleList, Corrupt.h:188-199) as a hash set.
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <unordered_set>
+#include <utility>
 #include <vector>
 
 #include "common.h"
@@ -27,6 +30,25 @@ struct KeyHash {
 struct pt_known {
     std::unordered_set<Key, KeyHash> set;
     bool has(int64_t h, int64_t t, int64_t r) const { return set.count(Key{h, t, r}) != 0; }
+    // (anchor, r) -> partner entities, per side (0: heads of (t, r); 1: tails of (h, r)); built on first use
+    struct PairHash {
+        size_t operator()(const std::pair<int64_t, int64_t> &p) const {
+            const uint64_t x = (uint64_t)p.first * 0x9E3779B97F4A7C15ULL ^ (uint64_t)p.second * 0xC2B2AE3D27D4EB4FULL;
+            return (size_t)(x ^ (x >> 29));
+        }
+    };
+    mutable std::mutex mu;
+    mutable bool indexed = false;
+    mutable std::unordered_map<std::pair<int64_t, int64_t>, std::vector<int64_t>, PairHash> by_side[2];
+    void index() const {
+        std::lock_guard<std::mutex> g(mu);
+        if (indexed) return;
+        for (const Key &k : set) {
+            by_side[0][{k.t, k.r}].push_back(k.h);
+            by_side[1][{k.h, k.r}].push_back(k.t);
+        }
+        indexed = true;
+    }
 };
 
 namespace pt {
@@ -87,5 +109,29 @@ extern "C" int pt_rank_queries(const pt_known *k, int64_t E, const int64_t *h, c
     for (int64_t w = 1; w < n_workers; ++w) pool.emplace_back(work);
     work();
     for (auto &th : pool) th.join();
+    return PT_OK;
+}
+
+// CSR of the known partners of many (anchor, r) queries: side 0 (head prediction, anchor = t) lists the
+// h with (h, t, r) known; side 1 (tail prediction, anchor = h) lists the t with (h, t, r) known.
+// off[n + 1]; when list is NULL only off is filled (off[n] = total).
+extern "C" int pt_known_partners(const pt_known *k, int32_t side, int64_t n, const int64_t *anchor, const int64_t *rel,
+                                 int64_t *off, int64_t *list) {
+    if (!k || (n > 0 && (!anchor || !rel)) || !off || (side != 0 && side != 1))
+        return pt::fail(PT_EINVAL, "pt_known_partners: bad argument");
+    k->index();
+    const auto &m = k->by_side[side];
+    off[0] = 0;
+    for (int64_t q = 0; q < n; ++q) {
+        const auto it = m.find({anchor[q], rel[q]});
+        int64_t c = 0;
+        if (it != m.end()) {
+            for (int64_t e : it->second) {
+                if (list) list[off[q] + c] = e;
+                ++c;
+            }
+        }
+        off[q + 1] = off[q] + c;
+    }
     return PT_OK;
 }

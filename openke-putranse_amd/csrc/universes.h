@@ -17,14 +17,35 @@ struct UniverseDev {
     float *ent_acc, *rel_acc, *norm_acc;            // Adagrad accumulators (same shapes)
     float *gent, *grel, *gnorm;                     // gradient rows, zero between steps
     int32_t *fent, *frel, *fnorm;                   // touched-row flags, zero between steps
+    float *contrib;                                 // [bs*(2+neg)][dim] entity-row gradient contributions
     float *losses;                                  // [epochs] Trainer.run's per-epoch loss sum (or null)
+    uint64_t *prof;                                 // null, or [4] cycle counters (presample, A, B, steps)
     int64_t threads, bs, nbatches, epochs, dim;
     float lr, margin;
+    int32_t shape;                                  // universe_shape_id(dim)
 };
 
-// n universes of one row shape `s` in one launch (one workgroup each); list_cap = LDS work-list entries
-// (>= bs * (4 + neg) for every universe of the launch)
-hipError_t launch_universes(const UniverseDev *d_us, int64_t n, const Shape &s, int model, int p_norm, int norm_flag,
-                            int opt, int64_t neg, int bern, int filter, int64_t list_cap, hipStream_t st);
+// launch configuration of one group of universes (host-chosen for the largest universe of the group)
+struct UniverseLaunch {
+    int threads = 512;          // workgroup size
+    int64_t list_cap = 1;       // LDS work-list entries (>= bs * (4 + neg))
+    int lds_flags = 0;          // touched-row flags in LDS instead of the global flag arrays
+    int contrib = 0;            // entity gradients as LDS-linked contribution slots (needs head[E] + next[ccap])
+    int64_t pchunk = 0;         // batches drawn into LDS at a time (0: sample inside each step)
+    int lds_relgrad = 0;        // relation / norm_vector gradient rows in LDS (R x D floats, x2 for TransH)
+    int agent_fence = 1;        // agent-scope fences around the phase barriers (global atomics in use)
+    int64_t lds_bytes = 0;      // dynamic LDS per workgroup
+};
+
+// lane-group shape of the universe kernel for dim D (narrower groups than pick_shape) and its id in
+// the kernel's shape switch (-1: unsupported)
+Shape pick_universe_shape(int64_t D);
+int universe_shape_id(int64_t D);
+bool universe_shape_supported(int64_t D);
+
+// all n universes in one persistent launch: workgroups pull universes from *counter (device int,
+// reset by the launch) in array order (the host sorts longest-first)
+hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, int model, int p_norm, int norm_flag,
+                            int opt, int64_t neg, int bern, int filter, const UniverseLaunch &cfg, hipStream_t st);
 
 }  // namespace pt

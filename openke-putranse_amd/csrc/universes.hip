@@ -7,18 +7,23 @@
 // kernel, with two workgroup barriers per step that give the reference's minibatch-synchronous
 // semantics (every gradient of a step sees the pre-step tables):
 //
-//   phase A  each lane group takes positives b = grp, grp + GPB, ... of the step: draws the positive
-//            and its negatives exactly as sampling() would (per-universe LCG streams kept in LDS),
-//            runs group_step (forward, MarginLoss, backward) and adds the gradient rows into the
-//            universe's gradient buffer with float atomics; the first touch of a row appends it to
-//            an LDS work list;
-//   phase B  the lane groups walk the work list: normalize Jacobian of the pre-step row where the
-//            table's gradient is in normalized space, then the Adagrad (or SGD) row update, and
-//            re-zero the gradient row / flag; the sampler streams advance by the step's draws.
+//   sample   every `pchunk` steps the next pchunk batches (TrainDataLoader.sampling() calls) are drawn
+//            at once into LDS, lane-parallel (stream jumps, rng.h);
+//   phase A  each lane group takes positives b = grp, grp + GPB, ... of the step and runs group_step
+//            (forward, MarginLoss, backward). Gradient rows leave it through the sink:
+//              entity rows  -> written with plain stores to a per-universe contribution slot and
+//                              linked into the row's LDS list (no float atomics: 512 universes x
+//                              ~40 K row-element atomics per step saturate the L2 atomic units);
+//              relation / norm_vector rows -> LDS float atomics into LDS gradient rows (a universe
+//                              has few relations, and every positive of a step hits its relation);
+//            the first touch of a row appends it to an LDS work list;
+//   phase B  lane groups walk the work list, RB rows at a time: sum the row's contributions, normalize
+//            Jacobian of the pre-step row where the gradient is in normalized space, Adagrad (or SGD)
+//            update, reset the row's LDS state.
 //
-// Universes are independent, so thousands run concurrently (one per workgroup, several per CU) and
-// universes of different embedding dims run as separate launches on separate streams. The tables
-// stay in HBM (a universe's rows are re-read every step, so they live in L2 / Infinity Cache).
+// Whatever does not fit the LDS budget falls back to global memory (atomic gradient rows, flag arrays,
+// per-step sampling). Universes are independent, so thousands run concurrently (one per workgroup,
+// several per CU); universes of different row shapes run as separate launches on separate streams.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -32,26 +37,52 @@ namespace dev {
 
 // release / acquire at agent scope around the workgroup barrier: stores of one phase are visible to
 // loads of the next phase from any wave (L1 invalidated), independent of L1 write policy
-__device__ __forceinline__ void phase_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+// (needed while gradient rows are float atomics performed at L2: a later plain load must not hit a
+// stale L1 line). Without global atomics in the step (contribution lists + LDS relation rows + LDS
+// flags) every cross-wave exchange is plain stores / loads or LDS within the workgroup, which the
+// workgroup barrier alone orders (all waves of a workgroup share the CU's L1).
+__device__ __forceinline__ void phase_barrier(bool agent) {
+    if (agent) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    } else {
+        __syncthreads();
+    }
 }
 
-// Gradient sink of one universe: float atomics into the gradient rows, first touch of a row appends
-// (row << 2 | table) to the LDS work list.
+// Gradient sink of one universe.
+//   contrib != null: entity rows go to contribution slots (plain stores) linked per row in LDS
+//   (head[row] -> c -> next[c] -> ... -> -1); otherwise float atomics into gent.
+//   grel / gnorm point to LDS gradient rows or to global ones (float atomics either way).
 struct UniverseSink {
     float *gent, *grel, *gnorm;
     int32_t *fent, *frel, *fnorm;
     int32_t *list;
     int *count;
+    float *contrib;     // [ccap][D] (global) or null
+    int32_t *head;      // [E] LDS
+    int32_t *next;      // [ccap] LDS
+    int *ccount;        // LDS counter of contribution slots
     __device__ __forceinline__ void touch(int32_t *flag, int64_t row, int table) const {
         if (atomicExch(flag + row, 1) == 0) list[atomicAdd(count, 1)] = (int32_t)(row << 2) | table;
     }
     template <int G, int VEC, int KCH>
     __device__ __forceinline__ void ent(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
-        vatomic(g, gent + row * D, D, lane);
-        if (lane == 0) touch(fent, row, 0);
+        if (contrib) {
+            int c = 0;
+            if (lane == 0) c = atomicAdd(ccount, 1);
+            c = __shfl(c, 0, G);
+            vstore(g, contrib + (int64_t)c * D, D, lane);
+            if (lane == 0) {
+                const int32_t prev = atomicExch(head + row, c);
+                next[c] = prev;
+                if (prev < 0) list[atomicAdd(count, 1)] = (int32_t)(row << 2);
+            }
+        } else {
+            vatomic(g, gent + row * D, D, lane);
+            if (lane == 0) touch(fent, row, 0);
+        }
     }
     template <int G, int VEC, int KCH>
     __device__ __forceinline__ void rel(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
@@ -65,131 +96,447 @@ struct UniverseSink {
     }
 };
 
-template <int MODEL, int G, int VEC, int KCH>
-__global__ __launch_bounds__(256) void k_universes(const UniverseDev *__restrict__ us, int p_norm, int norm_flag,
-                                                   int opt, int64_t neg, int bern, int filter) {
+// TransE step of one positive whose negatives each replace ONE side with entity e (the sampler's
+// structure, Base.cpp:217-232): the same forward / MarginLoss / backward as group_step with a smaller
+// live set (normalized rows kept in place, no per-negative row-role bookkeeping), so the universe
+// kernel stays under 128 VGPRs. get_neg(k, &e, &tail_side). Gradients in normalized space, like
+// group_step for TransE; a corrupted row equal to a positive row is simply a separate contribution.
+template <int G, int VEC, int KCH, typename Sink, typename NegFn>
+__device__ __forceinline__ float transe_step(const StepParams &P, int64_t hp, int64_t rp, int64_t tp, int64_t neg,
+                                             NegFn get_neg, const Sink &sink, int lane) {
     using Vec = V<G, VEC, KCH>;
-    constexpr int GPB = 256 / G;
-    extern __shared__ int32_t s_list[];
-    __shared__ uint64_t s_states[64];
-    __shared__ int s_count;
-    __shared__ float s_loss;
-    const UniverseDev U = us[blockIdx.x];
+    const int D = (int)P.dim;
+    const int p = P.p_norm;
+    const bool nf = P.norm_flag != 0;
+    Vec hh, th, rh, vpos;
+    vload(hh, P.ent + hp * D, D, lane);
+    vload(th, P.ent + tp * D, D, lane);
+    vload(rh, P.rel + rp * D, D, lane);
+    if (nf) {
+        vnormalize(hh, hh);
+        vnormalize(rh, rh);
+        vnormalize(th, th);
+    }
+#pragma unroll
+    for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
+    const float ps = vpnorm(vpos, p);
+    Vec aH, aT, aR;
+    vzero(aH); vzero(aT); vzero(aR);
+    float csum = 0.f, lsum = 0.f;
+    const float m = P.margin, inv = P.inv_count;
+    for (int64_t k = 0; k < neg; ++k) {
+        int64_t e;
+        bool tail_side;
+        get_neg(k, e, tail_side);
+        Vec x;
+        vload(x, P.ent + e * D, D, lane);
+        if (nf) vnormalize(x, x);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) x.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - x.x[i] : (x.x[i] + rh.x[i]) - th.x[i];
+        const float ns = vpnorm(x, p);
+        const float a = ps - ns;
+        lsum += a > -m ? a : -m;
+        const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
+        if (c == 0.f) continue;
+        csum += c;
+        vpnorm_bwd(x, ns, p, -c, x);   // x := d loss / d v_k
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            aR.x[i] += x.x[i];
+            if (tail_side) aH.x[i] += x.x[i]; else aT.x[i] -= x.x[i];
+        }
+        if (tail_side) {
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) x.x[i] = -x.x[i];
+        }
+        sink.ent(e, x, D, lane);   // corrupted tail gets -g, corrupted head +g
+    }
+    if (csum != 0.f) {
+        vpnorm_bwd(vpos, ps, p, csum, vpos);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            aH.x[i] += vpos.x[i];
+            aR.x[i] += vpos.x[i];
+            aT.x[i] -= vpos.x[i];
+        }
+    }
+    if (vnonzero(aR)) sink.rel(rp, aR, D, lane);
+    if (vnonzero(aH)) sink.ent(hp, aH, D, lane);
+    if (vnonzero(aT)) sink.ent(tp, aT, D, lane);
+    return lsum;
+}
+
+// Dynamic LDS layout (int32 units; the host sizes it for the largest universe of the launch):
+//   list[list_cap] | flags[E + 2R] or [2R] | head[E] + next[ccap] (contrib) |
+//   batch h, r, t [3][pchunk * bs * (1 + neg)] (pchunk > 0) | rel (+ norm) gradient rows [R][D] floats
+// LDS state of a universe workgroup that is not in the dynamic area (declared once by the kernel)
+struct UniShared {
+    int32_t *dyn;
+    uint64_t *states;   // [64]
+    int *count, *ccount;
+    float *loss;
+};
+
+// One universe's whole training run (all epochs x nbatches steps) by the calling workgroup.
+template <int MODEL, int G, int VEC, int KCH, int NT>
+__device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, int norm_flag, int opt, int64_t neg,
+                                             int bern, int filter, const UniverseLaunch &cfg, const UniShared &S) {
+    using Vec = V<G, VEC, KCH>;
+    constexpr int GPB = NT / G;
+    int32_t *s_dyn = S.dyn;
+    uint64_t *s_states = S.states;
+    int &s_count = *S.count;
+    int &s_ccount = *S.ccount;
+    float &s_loss = *S.loss;
     const int tid = threadIdx.x, lane = tid % G, grp = tid / G;
     const int64_t bs = U.bs, threads = U.threads, D = U.dim;
+    const int64_t E = U.g.ent_total, R = U.g.rel_total;
+    const bool contrib = cfg.contrib && U.contrib;
+    const int64_t seq = bs * (1 + neg), ccap = bs * (2 + neg);
+    const int64_t pchunk = cfg.pchunk < U.nbatches ? cfg.pchunk : U.nbatches;
+    // carve the LDS
+    int32_t *p = s_dyn;
+    int32_t *s_list = p;
+    p += cfg.list_cap;
+    int32_t *s_flags = p;   // [E (atomic mode only)][R][R]
+    const int64_t nflags = cfg.lds_flags ? (contrib ? 2 * R : E + 2 * R) : 0;
+    p += (nflags + 3) & ~int64_t(3);
+    int32_t *s_head = p;
+    int32_t *s_next = p + ((E + 3) & ~int64_t(3));
+    if (contrib) p += ((E + 3) & ~int64_t(3)) + ((ccap + 3) & ~int64_t(3));
+    int32_t *s_bh = p, *s_br = p + pchunk * seq, *s_bt = p + 2 * pchunk * seq;
+    p += 3 * pchunk * seq;
+    float *s_grel = reinterpret_cast<float *>(p);
+    const int64_t nrelg = cfg.lds_relgrad ? R * D * (MODEL == 1 ? 2 : 1) : 0;
+
     if (tid < threads) s_states[tid] = U.states[tid];
+    for (int64_t i = tid; i < nflags; i += NT) s_flags[i] = 0;
+    if (contrib)
+        for (int64_t i = tid; i < E; i += NT) s_head[i] = -1;
+    for (int64_t i = tid; i < nrelg; i += NT) s_grel[i] = 0.f;
     StepParams P{};
     P.model = MODEL; P.p_norm = p_norm; P.norm_flag = norm_flag; P.opt = opt;
     P.lr = U.lr; P.margin = U.margin;
-    P.ent_total = U.g.ent_total; P.rel_total = U.g.rel_total; P.dim = D;
+    P.ent_total = E; P.rel_total = R; P.dim = D;
     P.ent = U.ent; P.rel = U.rel; P.normv = U.normv;
     P.ent_acc = U.ent_acc; P.rel_acc = U.rel_acc; P.norm_acc = U.norm_acc;
     P.batch_size = bs; P.neg = neg;
     P.inv_count = 1.0f / (float)(bs * neg);
-    const UniverseSink sink{U.gent, U.grel, U.gnorm, U.fent, U.frel, U.fnorm, s_list, &s_count};
+    UniverseSink sink{U.gent, U.grel, U.gnorm, U.fent, U.frel, U.fnorm, s_list, &s_count,
+                      contrib ? U.contrib : nullptr, s_head, s_next, &s_ccount};
+    if (cfg.lds_flags) {
+        int32_t *f = s_flags;
+        if (!contrib) {
+            sink.fent = f;
+            f += E;
+        }
+        sink.frel = f;
+        sink.fnorm = f + R;
+    }
+    if (cfg.lds_relgrad) {
+        sink.grel = s_grel;
+        sink.gnorm = s_grel + R * D;
+    }
     const int64_t dpp = 1 + 2 * neg;
     const DeviceGraph &g = U.g;
+    const int64_t per = bs % threads == 0 ? bs / threads : bs / threads + 1;
     float epoch_loss = 0.f;
+    uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0;
+    __syncthreads();
     for (int64_t epoch = 0; epoch < U.epochs; ++epoch) {
         for (int64_t step = 0; step < U.nbatches; ++step) {
-            if (tid == 0) {
-                s_count = 0;
-                s_loss = 0.f;
-            }
-            phase_barrier();
-            // ---- phase A: sample + forward + backward of the step's positives
-            for (int64_t b = grp; b < bs; b += GPB) {
-                const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp);
-                const float lsum = group_step<MODEL, G, VEC, KCH>(
-                    P, pd.h, pd.r, pd.t, neg,
-                    [&](int64_t k, int64_t &h, int64_t &t, int64_t &r) {
+            if (U.prof) t0 = clock64();
+            const int64_t cs = pchunk > 0 ? step % pchunk : 0;
+            if (pchunk > 0 && cs == 0) {
+                // the next min(pchunk, left) batches drawn at once into LDS: batch j of the chunk is
+                // sampler call j after the chunk-start stream states
+                const int64_t nb = U.nbatches - step < pchunk ? U.nbatches - step : pchunk;
+                for (int64_t q = tid; q < nb * bs; q += NT) {
+                    const int64_t s = q / bs, b = q - s * bs;
+                    const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp, s);
+                    int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
+                    bh[b] = (int32_t)pd.h; br[b] = (int32_t)pd.r; bt[b] = (int32_t)pd.t;
+                    for (int64_t k = 0; k < neg; ++k) {
                         int side;
                         const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
-                        h = side ? pd.h : e;
-                        t = side ? e : pd.t;
-                        r = pd.r;
-                    },
-                    sink, lane);
+                        const int64_t o = (k + 1) * bs + b;
+                        bh[o] = (int32_t)(side ? pd.h : e);
+                        bt[o] = (int32_t)(side ? e : pd.t);
+                        br[o] = (int32_t)pd.r;
+                    }
+                }
+                __syncthreads();
+                if (tid < threads) {   // the chunk consumed nb calls of the streams
+                    int64_t len = bs - tid * per;
+                    len = len < 0 ? 0 : (len > per ? per : len);
+                    s_states[tid] = lcg_jump(s_states[tid], (uint64_t)(len * dpp * nb));
+                }
+            }
+            if (tid == 0) {
+                s_count = 0;
+                s_ccount = 0;
+                s_loss = 0.f;
+            }
+            phase_barrier(cfg.agent_fence);
+            if (U.prof) {
+                const uint64_t t1 = clock64();
+                t_pre += t1 - t0;
+                t0 = t1;
+            }
+            // ---- phase A: forward + backward of the step's positives
+            for (int64_t b = grp; b < bs; b += GPB) {
+                float lsum;
+                if (pchunk > 0) {
+                    const int32_t *bh = s_bh + cs * seq, *br = s_br + cs * seq, *bt = s_bt + cs * seq;
+                    const int64_t hp = bh[b], rp = br[b], tp = bt[b];
+                    if constexpr (MODEL == 0) {
+                        // a negative shares one side with its positive: the head when the tail was
+                        // corrupted (if both sides match, the negative equals the positive and either
+                        // reading gives the same gradients)
+                        lsum = transe_step<G, VEC, KCH>(
+                            P, hp, rp, tp, neg,
+                            [&](int64_t k, int64_t &e, bool &tail_side) {
+                                const int64_t o = (k + 1) * bs + b;
+                                tail_side = bh[o] == hp;
+                                e = tail_side ? bt[o] : bh[o];
+                            },
+                            sink, lane);
+                    } else {
+                        lsum = group_step<MODEL, G, VEC, KCH>(
+                            P, hp, rp, tp, neg,
+                            [&](int64_t k, int64_t &h, int64_t &t, int64_t &r) {
+                                const int64_t o = (k + 1) * bs + b;
+                                h = bh[o]; t = bt[o]; r = br[o];
+                            },
+                            sink, lane);
+                    }
+                } else {
+                    const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp);
+                    if constexpr (MODEL == 0) {
+                        lsum = transe_step<G, VEC, KCH>(
+                            P, pd.h, pd.r, pd.t, neg,
+                            [&](int64_t k, int64_t &e, bool &tail_side) {
+                                int side;
+                                e = draw_negative(g, pd, k, bern, filter, &side);
+                                tail_side = side != 0;
+                            },
+                            sink, lane);
+                    } else {
+                        lsum = group_step<MODEL, G, VEC, KCH>(
+                            P, pd.h, pd.r, pd.t, neg,
+                            [&](int64_t k, int64_t &h, int64_t &t, int64_t &r) {
+                                int side;
+                                const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
+                                h = side ? pd.h : e;
+                                t = side ? e : pd.t;
+                                r = pd.r;
+                            },
+                            sink, lane);
+                    }
+                }
                 if (lane == 0) atomicAdd(&s_loss, lsum);
             }
-            phase_barrier();
-            // ---- phase B: row updates of the touched rows
-            const int n = s_count;
-            for (int i = grp; i < n; i += GPB) {
-                const int32_t code = s_list[i];
-                const int table = code & 3;
-                const int64_t row = code >> 2;
-                float *w = table == 0 ? U.ent : (table == 1 ? U.rel : U.normv);
-                float *acc = table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc);
-                float *gr = table == 0 ? U.gent : (table == 1 ? U.grel : U.gnorm);
-                int32_t *fl = table == 0 ? U.fent : (table == 1 ? U.frel : U.fnorm);
-                // ent rows of TransE and every rel / norm_vector row carry normalized-space gradients
-                const bool jac = table == 0 ? (MODEL == 0 && norm_flag) : (table == 1 ? norm_flag != 0 : true);
-                Vec x, gs, gg;
-                vload(x, w + row * D, (int)D, lane);
-                vload(gs, gr + row * D, (int)D, lane);
-                if (jac) {
-                    const float nx = sqrtf(vdot(x, x));
-                    vnormalize_bwd(x, nx, gs, gg);
-                } else {
-                    gg = gs;
-                }
-                if (opt == 0) {
-#pragma unroll
-                    for (int j = 0; j < Vec::N; ++j) x.x[j] = x.x[j] + (-U.lr) * gg.x[j];
-                } else {
-                    Vec a;
-                    vload(a, acc + row * D, (int)D, lane);
-#pragma unroll
-                    for (int j = 0; j < Vec::N; ++j) {
-                        a.x[j] = a.x[j] + gg.x[j] * gg.x[j];
-                        x.x[j] = x.x[j] + (-U.lr) * gg.x[j] / (sqrtf(a.x[j]) + 1e-10f);
-                    }
-                    vstore(a, acc + row * D, (int)D, lane);
-                }
-                vstore(x, w + row * D, (int)D, lane);
-                Vec z;
-                vzero(z);
-                vstore(z, gr + row * D, (int)D, lane);
-                if (lane == 0) fl[row] = 0;
+            phase_barrier(cfg.agent_fence);
+            if (U.prof) {
+                const uint64_t t1 = clock64();
+                t_a += t1 - t0;
+                t0 = t1;
             }
-            if (tid < threads) {   // the step consumed bs positives x dpp draws (Base.cpp:200-207 split)
-                const int64_t per = bs % threads == 0 ? bs / threads : bs / threads + 1;
+            // ---- phase B: row updates of the touched rows, RB rows per lane group at a time (all their
+            // loads in flight together: the pass is a chain of dependent memory round trips otherwise)
+            const int n = s_count;
+            constexpr int RB = VEC * KCH > 4 ? 2 : 4;
+            for (int i0 = grp * RB; i0 < n; i0 += GPB * RB) {
+                Vec x[RB], gs[RB], a[RB];
+                float *wp[RB], *ap[RB];
+                int32_t code[RB];
+#pragma unroll
+                for (int u = 0; u < RB; ++u) {
+                    if (i0 + u >= n) break;
+                    code[u] = s_list[i0 + u];
+                    const int table = code[u] & 3;
+                    const int64_t row = code[u] >> 2;
+                    wp[u] = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
+                    ap[u] = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
+                    vload(x[u], wp[u], (int)D, lane);
+                    if (opt != 0) vload(a[u], ap[u], (int)D, lane);
+                    if (table == 0 && contrib) {
+                        // the row's contributions (linked in LDS), summed in list order
+                        int32_t c = s_head[row];
+                        vload(gs[u], U.contrib + (int64_t)c * D, (int)D, lane);
+                        for (c = s_next[c]; c >= 0; c = s_next[c]) {
+                            Vec y;
+                            vload(y, U.contrib + (int64_t)c * D, (int)D, lane);
+#pragma unroll
+                            for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y.x[j];
+                        }
+                    } else {
+                        vload(gs[u], (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D,
+                              (int)D, lane);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < RB; ++u) {
+                    if (i0 + u >= n) break;
+                    const int table = code[u] & 3;
+                    const int64_t row = code[u] >> 2;
+                    // ent rows of TransE and every rel / norm_vector row carry normalized-space gradients
+                    const bool jac = table == 0 ? (MODEL == 0 && norm_flag) : (table == 1 ? norm_flag != 0 : true);
+                    Vec gg;
+                    if (jac) {
+                        const float nx = sqrtf(vdot(x[u], x[u]));
+                        vnormalize_bwd(x[u], nx, gs[u], gg);
+                    } else {
+                        gg = gs[u];
+                    }
+                    if (opt == 0) {
+#pragma unroll
+                        for (int j = 0; j < Vec::N; ++j) x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j];
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < Vec::N; ++j) {
+                            a[u].x[j] = a[u].x[j] + gg.x[j] * gg.x[j];
+                            x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j] / (sqrtf(a[u].x[j]) + 1e-10f);
+                        }
+                        vstore(a[u], ap[u], (int)D, lane);
+                    }
+                    vstore(x[u], wp[u], (int)D, lane);
+                    if (table == 0 && contrib) {
+                        if (lane == 0) s_head[row] = -1;
+                    } else {
+                        Vec z;
+                        vzero(z);
+                        vstore(z, (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D, (int)D,
+                               lane);
+                        if (lane == 0) (table == 0 ? sink.fent : (table == 1 ? sink.frel : sink.fnorm))[row] = 0;
+                    }
+                }
+            }
+            if (pchunk == 0 && tid < threads) {   // the step consumed bs positives x dpp draws
                 int64_t len = bs - tid * per;
                 len = len < 0 ? 0 : (len > per ? per : len);
                 s_states[tid] = lcg_jump(s_states[tid], (uint64_t)(len * dpp));
             }
             if (tid == 0) epoch_loss += s_loss * P.inv_count + U.margin;
+            if (U.prof) {
+                const uint64_t t1 = clock64();
+                t_b += t1 - t0;
+            }
         }
-        if (tid == 0 && U.losses) {
-            U.losses[epoch] = epoch_loss;
-        }
+        if (tid == 0 && U.losses) U.losses[epoch] = epoch_loss;
         epoch_loss = 0.f;
     }
-    phase_barrier();
+    phase_barrier(cfg.agent_fence);
+    if (U.prof && tid == 0) {
+        U.prof[0] = t_pre;
+        U.prof[1] = t_a;
+        U.prof[2] = t_b;
+        U.prof[3] = (uint64_t)U.epochs * U.nbatches;
+    }
     if (tid < threads) U.states[tid] = s_states[tid];
+}
+
+// row shapes of the universe kernel: narrower lane groups than the single-model kernels (2 x VEC=4
+// or 4 x VEC=1 chunks per lane) so a step's ~25-100 positives and ~100-300 touched rows take few rounds
+#define PT_USHAPES(X)                                                                                  \
+    X(0, 2, 4, 1) X(1, 2, 4, 2) X(2, 4, 4, 2) X(3, 8, 4, 2) X(4, 16, 4, 2) X(5, 32, 4, 2) X(6, 64, 4, 2) \
+    X(7, 2, 1, 1) X(8, 2, 1, 2) X(9, 2, 1, 4) X(10, 4, 1, 4) X(11, 8, 1, 4) X(12, 16, 1, 4)              \
+    X(13, 32, 1, 4) X(14, 64, 1, 4) X(15, 64, 1, 8)
+
+// Persistent work-queue kernel: a workgroup takes universes in the host's longest-first order from an
+// atomic counter until the queue is empty (greedy longest-processing-time list scheduling over the
+// CUs, whatever the mix of universe sizes and row shapes), every universe with its shape's code path.
+template <int MODEL, int NT, int WPE>
+__global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__restrict__ us, int64_t n,
+                                                       int *__restrict__ next_universe, int p_norm, int norm_flag,
+                                                       int opt, int64_t neg, int bern, int filter,
+                                                       UniverseLaunch cfg) {
+    extern __shared__ int32_t s_dyn[];
+    __shared__ uint64_t s_states[64];
+    __shared__ int s_count, s_ccount, s_u;
+    __shared__ float s_loss;
+    const UniShared S{s_dyn, s_states, &s_count, &s_ccount, &s_loss};
+    for (;;) {
+        if (threadIdx.x == 0) s_u = atomicAdd(next_universe, 1);
+        __syncthreads();
+        const int64_t u = s_u;
+        __syncthreads();
+        if (u >= n) break;   // every wave of the workgroup reads the same u: the whole group exits
+        const UniverseDev U = us[u];
+        switch (U.shape) {
+#define PT_URUN(ID_, G_, V_, K_)                                                                   \
+    case ID_:                                                                                      \
+        universe_run<MODEL, G_, V_, K_, NT>(U, p_norm, norm_flag, opt, neg, bern, filter, cfg, S); \
+        break;
+            PT_USHAPES(PT_URUN)
+#undef PT_URUN
+            default:
+                break;
+        }
+        __syncthreads();
+    }
 }
 
 }  // namespace dev
 
-hipError_t launch_universes(const UniverseDev *d_us, int64_t n, const Shape &s, int model, int p_norm, int norm_flag,
-                            int opt, int64_t neg, int bern, int filter, int64_t list_cap, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    const dim3 grid((unsigned)n), block(256);
-    const size_t lds = (size_t)list_cap * sizeof(int32_t);
-#define PT_UNI(G_, V_, K_)                                                                                    \
-    if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                                          \
-        if (model == 0)                                                                                       \
-            hipLaunchKernelGGL((dev::k_universes<0, G_, V_, K_>), grid, block, lds, st, d_us, p_norm,        \
-                               norm_flag, opt, neg, bern, filter);                                            \
-        else                                                                                                  \
-            hipLaunchKernelGGL((dev::k_universes<1, G_, V_, K_>), grid, block, lds, st, d_us, p_norm,        \
-                               norm_flag, opt, neg, bern, filter);                                            \
-        return hipGetLastError();                                                                           \
+Shape pick_universe_shape(int64_t D) {
+    const int VEC = D % 4 == 0 ? 4 : 1;
+    const int64_t chunks = (D + VEC - 1) / VEC;
+    const int64_t per_lane = VEC == 4 ? 2 : 4;
+    int G = 2;
+    while (G < 64 && (int64_t)G * per_lane < chunks) G <<= 1;
+    int KCH = 1;
+    while ((int64_t)G * KCH < chunks) KCH <<= 1;
+    return Shape{G, VEC, KCH};
+}
+
+int universe_shape_id(int64_t D) {
+    if (D <= 0) return -1;
+    const Shape s = pick_universe_shape(D);
+#define PT_USUP(ID_, G_, V_, K_) \
+    if (s.G == G_ && s.VEC == V_ && s.KCH == K_) return ID_;
+    PT_USHAPES(PT_USUP)
+#undef PT_USUP
+    return -1;
+}
+
+bool universe_shape_supported(int64_t D) { return universe_shape_id(D) >= 0; }
+
+namespace {
+template <int MODEL, int WPE>
+hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int p_norm, int norm_flag, int opt, int64_t neg,
+                    int bern, int filter, const UniverseLaunch &cfg, hipStream_t st) {
+    constexpr int NT = 512;
+    auto kern = dev::k_universes<MODEL, NT, WPE>;
+    if (cfg.lds_bytes > (64 << 10)) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)cfg.lds_bytes);
+        if (e != hipSuccess) return e;
     }
-    PT_SHAPES(PT_UNI)
-#undef PT_UNI
-    return hipErrorInvalidValue;
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kern), NT,
+                                                         (size_t)cfg.lds_bytes);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1) per_cu = 1;
+    int64_t grid = (int64_t)cus * per_cu;
+    if (grid > n) grid = n;
+    if (grid < 1) grid = 1;
+    e = hipMemsetAsync(counter, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), (size_t)cfg.lds_bytes, st, d_us, n, counter, p_norm,
+                       norm_flag, opt, neg, bern, filter, cfg);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, int model, int p_norm, int norm_flag,
+                            int opt, int64_t neg, int bern, int filter, const UniverseLaunch &cfg, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    return model == 0 ? launch_q<0, 1>(d_us, n, counter, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
+                      : launch_q<1, 1>(d_us, n, counter, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
 }
 
 }  // namespace pt

@@ -83,15 +83,19 @@ SIGNATURES = {
                                               c_i64, c_i64, ctypes.POINTER(c_vp)]),
     "pt_universe_set_train": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "pt_universe_set_free": (ctypes.c_int, [c_vp]),
+    "pt_universe_set_profile": (ctypes.c_int, [c_vp, c_vp]),
     "pt_universes_train": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
                                           c_i64, c_vp, c_vp]),
     "pt_lp_min_scores": (ctypes.c_int, [ctypes.POINTER(LpUniverse), c_i64, c_i32, c_i32, c_i32,
-                                        ctypes.POINTER(LpPair), c_i64, c_i64, c_vp, c_vp]),
+                                        ctypes.POINTER(LpPair), c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "pt_rank_rows": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "pt_known_partners": (ctypes.c_int, [c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "pt_known_create": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(c_vp)]),
     "pt_known_free": (ctypes.c_int, [c_vp]),
     "pt_rank_queries": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64]),
     "pt_legacy_sampler": (c_vp, []),
     "pt_legacy_bern": (c_i64, []),
+    "pt_legacy_graph": (c_vp, []),
     "pt_legacy_eval_triples": (c_i64, [c_i32, c_vp, c_vp, c_vp]),
     "pt_legacy_known": (c_vp, []),
     # Base.so surface (argument types as the reference's loaders declare them)

@@ -1,7 +1,764 @@
-# placeholder replaced below
+# coding:utf-8
+"""PuTransE / PuTransH driver (mirror of openke/config/Parallel_Universe_Config.py).
+
+Same constructor, attributes, per-universe protocol and outputs as the reference; the work is
+re-organised for the GPU:
+
+* Training. The reference builds and trains universes one at a time (train_parallel_universes,
+  :316-367). Universe k is a pure function of seed0 + k (set_random_seed, :157-161), so here a WAVE of
+  universes is prepared at once - the Python draws of every universe in the reference's order
+  (randrange(tc), uniform(balance), randrange(margin), randrange(epochs), uniform(lr); :210-236), the
+  universe construction on host threads (pt_universe_build_many; getParallelUniverse), the torch init
+  of every universe's tables after torch.manual_seed(seed0 + k) (the model factory, :169-177) - and
+  the whole wave trains in ONE persistent GPU launch (pt_universes_train: one workgroup per universe
+  runs all of its epochs x nbatches Adagrad steps, :238-258). The universes are then committed one by
+  one in id order with the reference's validation / early-stopping / checkpoint schedule; universes a
+  wave trained beyond an early stop are discarded, so the committed result is the reference's.
+* Multi-GPU. With torch.distributed initialised (one process per GPU), universe k trains on rank
+  k % world_size (universes are independent: no data-path collective). Link-prediction score rows
+  are MIN-combined across ranks with one all_reduce(MIN) over RCCL.
+* Global energy estimation. The per-(entity, relation) score dictionaries (:446-465, :516-554) are
+  device rows [n_keys][entTotal] filled by pt_lp_min_scores (score every entity of every universe
+  holding the key, MIN into the key row); ranks come from pt_rank_rows on those rows (the same counts
+  as testHead/testTail and validHead/validTail on the candidate-order vectors), metrics from
+  pt_lp_metrics.
+"""
+import ctypes
+import os
+import random
+import time
+from collections import defaultdict
+from copy import deepcopy
+from random import randrange, uniform, seed
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..data import TestDataLoader
+from ..module.loss import MarginLoss
+from ..module.model.Model import Model
+from ..module.strategy import NegativeSampling
 from .Tester import Tester
 
 
+def get_string_key(entity, relation):
+    return '{},{}'.format(entity, relation)
+
+
+def defaultdict_int(innerfactory=int):
+    return defaultdict(innerfactory)
+
+
+def float_default():
+    return float("inf")
+
+
+def to_tensor(x, use_gpu):
+    if use_gpu:
+        return torch.tensor([x]).cuda()
+    return torch.tensor([x])
+
+
+def _dist():
+    """(world_size, rank) of an initialised torch.distributed group, else (1, 0)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+class _KeyStore(object):
+    """Device score rows of one evaluation split: one row per (side, anchor, relation) key.
+
+    side 0 = head prediction, anchor = tail (evaluation_tail2head_triple_score_dict, key 't,r');
+    side 1 = tail prediction, anchor = head (evaluation_head2tail_triple_score_dict, key 'h,r') - the
+    side convention of every native entry point (pt_lp_min_scores, pt_rank_rows, pt_known_partners)."""
+
+    def __init__(self, h, t, r, ent_tot, device):
+        self.h, self.t, self.r = h, t, r
+        self.E = ent_tot
+        keys = {}
+        self.q_row = [np.zeros(len(h), dtype=np.int64), np.zeros(len(h), dtype=np.int64)]
+        for q in range(len(h)):
+            for side, anchor in ((0, int(t[q])), (1, int(h[q]))):
+                k = (side, anchor, int(r[q]))
+                idx = keys.get(k)
+                if idx is None:
+                    idx = keys[k] = len(keys)
+                self.q_row[side][q] = idx
+        self.keys = keys
+        n = len(keys)
+        self.key_side = np.array([k[0] for k in keys], dtype=np.int64)
+        self.key_anchor = np.array([k[1] for k in keys], dtype=np.int64)
+        self.key_rel = np.array([k[2] for k in keys], dtype=np.int64)
+        self.rows = torch.full((max(n, 1), max(ent_tot, 1)), float("inf"), dtype=torch.float32, device=device)
+        self.tuple = torch.full((max(n, 1),), float("inf"), dtype=torch.float32, device=device)
+        self.folded = 0   # universes [0, folded) are MIN-ed into the rows
+
+    def row(self, side, anchor, rel):
+        idx = self.keys.get((side, int(anchor), int(rel)))
+        return None if idx is None else idx
+
+
 class Parallel_Universe_Config(Tester):
-    def __init__(self, *a, **k):
-        raise NotImplementedError
+    def __init__(self,
+                 train_dataloader=None, training_identifier='', valid_dataloader=None, test_dataloader=None,
+                 initial_num_universes=5000,
+                 min_margin=1, max_margin=4, min_lr=0.01, max_lr=0.1, min_num_epochs=50, max_num_epochs=200,
+                 const_num_epochs=None, min_triple_constraint=500, max_triple_constraint=2000, min_balance=0.25,
+                 max_balance=0.5, embedding_model=None, embedding_model_param=None,
+                 missing_embedding_handling='last_rank',
+                 save_steps=5, checkpoint_dir='./checkpoint/', valid_steps=5, early_stopping_patience=5,
+                 training_setting="static",
+                 incremental_strategy="normal",
+                 universe_wave_size=None):
+        super(Parallel_Universe_Config, self).__init__(data_loader=test_dataloader, use_gpu=torch.cuda.is_available())
+        if training_setting != "static":
+            raise NotImplementedError("the incremental setting is outside the accelerated path")
+
+        """ Train data + variables"""
+        self.train_dataloader = train_dataloader
+        self.ent_tot = train_dataloader.entTotal
+        self.rel_tot = train_dataloader.relTotal
+        self.training_identifier = training_identifier
+
+        """ "-constant traininghyper parameters" """
+        self.embedding_model = embedding_model
+        self.embedding_model_param = embedding_model_param
+
+        """ Parallel Universe data structures """
+        self.initial_num_universes = initial_num_universes
+        self.next_universe_id = 0
+
+        self.trained_embedding_spaces = defaultdict(Model)  # universe_id -> embedding_space
+        self.entity_id_mappings = defaultdict(defaultdict_int)  # universe_id -> global entity_id -> local id
+        self.relation_id_mappings = defaultdict(defaultdict_int)  # universe_id -> global relation_id -> local id
+
+        self.entity_universes = defaultdict(set)  # entity_id -> universe_id
+        self.relation_universes = defaultdict(set)  # relation_id -> universe_id
+
+        self.initial_random_seed = self.train_dataloader.lib.getRandomSeed()
+
+        """Parallel Universe spans for randomizing embedding space hyper parameters"""
+        self.min_margin = min_margin
+        self.max_margin = max_margin
+        self.min_lr = min_lr
+        self.max_lr = max_lr
+        self.min_num_epochs = min_num_epochs
+        self.max_num_epochs = max_num_epochs
+        self.const_num_epochs = const_num_epochs
+        self.min_triple_constraint = min_triple_constraint
+        self.max_triple_constraint = max_triple_constraint
+        self.min_balance = min_balance
+        self.max_balance = max_balance
+
+        """ saving """
+        self.save_steps = save_steps
+        self.checkpoint_dir = checkpoint_dir
+
+        """ Eval """
+        self.missing_embedding_handling = missing_embedding_handling  # "last_rank" | "null_vector"
+
+        """ ""Valid"" """
+        self.valid_dataloader = valid_dataloader if valid_dataloader is not None else TestDataLoader(
+            train_dataloader.in_path,
+            sampling_mode="link",
+            mode='valid')
+
+        self.valid_steps = valid_steps
+        self.early_stopping_patience = early_stopping_patience
+        self.early_stopping_patience_const = early_stopping_patience
+        self.bad_counts = 0
+        self.best_hit10 = 0
+        self.best_state = None
+
+        """Global Energy Estimation data structures"""
+        self.current_tested_universes = 0
+        self.current_validated_universes = 0
+        # the reference's score dictionaries are device rows here (see _KeyStore); these stay empty
+        self.evaluation_head2tail_triple_score_dict = {}
+        self.evaluation_tail2head_triple_score_dict = {}
+        self.evaluation_head2rel_tuple_score_dict = {}
+        self.evaluation_tail2rel_tuple_score_dict = {}
+        self.default_scores = None   # the reference's [inf] * entTotal template, not needed with device rows
+
+        self.training_setting = training_setting
+        self.incremental_strategy = incremental_strategy
+
+        """ MI355X build """
+        self.universe_wave_size = universe_wave_size
+        self.last_universe_losses = {}    # universe_id -> per-epoch loss sums of Trainer.run
+        self.universe_hparams = {}        # universe_id -> tc, balance, margin, epochs, lr, batch_size
+        self._stores = {}                 # 'test' / 'valid' -> _KeyStore
+        self._remap_cache = {}            # universe_id -> (ent_remap, rel_remap, sorted helpers)
+        self._dev_remaps = {}             # universe_id -> device int64 local -> global entity map
+
+    # ------------------------------------------------------------------ reference API -----------
+    def get_default_value_list(self):
+        return [float("inf") for i in range(self.ent_tot)]
+
+    def set_min_max_triple_constraint(self, min, max):
+        self.min_triple_constraint = min
+        self.max_triple_constraint = max
+
+    def set_random_seed(self, rand_seed):
+        self.train_dataloader.lib.setRandomSeed(rand_seed)
+        self.train_dataloader.lib.randReset()
+        seed(rand_seed)
+        torch.manual_seed(rand_seed)
+
+    def set_valid_dataloader(self, valid_dataloader):
+        self.valid_dataloader = valid_dataloader
+        self._stores.pop('valid', None)
+
+    def set_test_dataloader(self, test_dataloader):
+        self.data_loader = test_dataloader
+        self._stores.pop('test', None)
+
+    def embedding_model_factory(self, ent_tot, rel_tot, margin):
+        embedding_method = self.embedding_model(ent_tot, rel_tot, **self.embedding_model_param)
+        return NegativeSampling(
+            model=embedding_method,
+            loss=MarginLoss(margin=margin),
+            batch_size=self.train_dataloader.batch_size
+        )
+
+    def reset_valid_variables(self):
+        self.early_stopping_patience = self.early_stopping_patience_const
+        self.best_state = {}
+        self.best_hit10 = 0
+        self.bad_counts = 0
+
+    def add_embedding_space(self, embedding_space):
+        for param in embedding_space.parameters():
+            param.requires_grad = False
+        self.trained_embedding_spaces[self.next_universe_id] = embedding_space
+
+    # ------------------------------------------------------------------ training ----------------
+    def _check_setup(self):
+        dl = self.train_dataloader
+        if dl.sampling_mode != "normal":
+            raise NotImplementedError("PuTransE trains with sampling_mode='normal' (TrainDataLoader.sampling)")
+        if dl.negative_rel != 0:
+            raise NotImplementedError("neg_rel > 0 is outside the accelerated path")
+        if self.embedding_model is None or getattr(self.embedding_model, "native_model", None) is None:
+            raise NotImplementedError("embedding_model must be openke.module.model.TransE or TransH")
+        _native.require_gpu()
+
+    def _universe_draws(self, uid):
+        """Python-RNG draws of universe uid in the reference's order (:210-236), after set_random_seed."""
+        self.set_random_seed(self.initial_random_seed + uid)
+        tc = randrange(self.min_triple_constraint, self.max_triple_constraint)
+        balance = round(uniform(self.min_balance, self.max_balance), 2)
+        margin = randrange(self.min_margin, self.max_margin)
+        epochs = self.const_num_epochs if self.const_num_epochs is not None \
+            else randrange(self.min_num_epochs, self.max_num_epochs)
+        lr = round(uniform(self.min_lr, self.max_lr), len(str(self.min_lr).split('.')[1]))
+        return tc, balance, margin, epochs, lr
+
+    def _train_wave(self, ids):
+        """Build and train universes `ids` (this rank's share on the GPU); returns records in id order."""
+        L = _native.lib()
+        dl = self.train_dataloader
+        world, rank = _dist()
+        n = len(ids)
+        draws = [self._universe_draws(uid) for uid in ids]
+        seeds = np.array([self.initial_random_seed + uid for uid in ids], dtype=np.int64)
+        tcs = np.array([d[0] for d in draws], dtype=np.int64)
+        bals = np.array([d[1] for d in draws], dtype=np.float32)
+        handles = (ctypes.c_void_p * max(n, 1))()
+        graph = L.pt_legacy_graph()
+        if not graph:
+            raise RuntimeError("no training graph imported (TrainDataLoader.read() imports it)")
+        _native.check(L.pt_universe_build_many(graph, n, seeds.ctypes.data, dl.work_threads, tcs.ctypes.data,
+                                               bals.ctypes.data, 0, handles))
+        recs, jobs, keep = [], [], []
+        dev = torch.device("cuda", torch.cuda.current_device())
+        try:
+            for i, uid in enumerate(ids):
+                tc, balance, margin, epochs, lr = draws[i]
+                h = handles[i]
+                E_u, R_u = L.pt_universe_ent_total(h), L.pt_universe_rel_total(h)
+                N_u = L.pt_universe_train_total(h)
+                em = np.zeros(max(E_u, 1), dtype=np.int64)
+                rm = np.zeros(max(R_u, 1), dtype=np.int64)
+                _native.check(L.pt_universe_remaps(h, em.ctypes.data, rm.ctypes.data))
+                bs = N_u // dl.nbatches
+                # the model factory after torch.manual_seed(seed0 + uid) (set_random_seed, :157-161)
+                torch.manual_seed(self.initial_random_seed + uid)
+                kge = self.embedding_model(E_u, R_u, **self.embedding_model_param)
+                rec = {"id": uid, "kge": kge, "ent_remap": em[:E_u], "rel_remap": rm[:R_u], "tc": tc,
+                       "balance": balance, "margin": margin, "epochs": epochs, "lr": lr, "batch_size": bs,
+                       "train_total": N_u, "losses": None}
+                recs.append(rec)
+                if uid % world != rank:
+                    continue   # trained on another rank
+                kge.to(dev)
+                ent, rel, nv = kge.tables()
+                accs = tuple(torch.zeros_like(x) if x is not None else None for x in (ent, rel, nv))
+                st = np.zeros(dl.work_threads, dtype=np.uint64)
+                _native.check(L.pt_universe_seeds(h, st.ctypes.data))
+                j = _native.UniverseJob()
+                j.graph = L.pt_universe_graph(h)
+                j.seeds = st.ctypes.data
+                j.threads = dl.work_threads
+                j.batch_size = bs
+                j.epochs = epochs if bs > 0 else 0
+                j.nbatches = dl.nbatches
+                j.neg = dl.negative_ent
+                j.lr = lr
+                j.margin = margin
+                j.ent, j.rel, j.normv = (x.data_ptr() if x is not None else None for x in (ent, rel, nv))
+                j.ent_acc, j.rel_acc, j.norm_acc = (x.data_ptr() if x is not None else None for x in accs)
+                j.dim = ent.shape[1]
+                jobs.append(j)
+                keep.append((st, accs, rec))
+            if jobs:
+                kge0 = keep[0][2]["kge"]
+                total_epochs = sum(int(j.epochs) for j in jobs)
+                losses = torch.zeros(max(total_epochs, 1), dtype=torch.float32, device=dev)
+                arr = (_native.UniverseJob * len(jobs))(*jobs)
+                _native.check(L.pt_universes_train(arr, len(jobs), kge0.native_model, int(kge0.p_norm),
+                                                   1 if kge0.norm_flag else 0, _native.PT_ADAGRAD,
+                                                   int(dl.bern), int(dl.filter), _native.ptr(losses),
+                                                   _native.stream()))
+                lh = losses.cpu().numpy()
+                off = 0
+                for j, (_, _, rec) in zip(jobs, keep):
+                    rec["losses"] = lh[off:off + int(j.epochs)].copy()
+                    off += int(j.epochs)
+        finally:
+            for i in range(n):
+                if handles[i]:
+                    L.pt_universe_free(handles[i])
+        return recs
+
+    def add_universe(self, embedding_space, ent_remap, rel_remap):
+        """Register a trained universe as id next_universe_id: add_embedding_space +
+        process_universe_mappings (:179-207) from its local -> global entity / relation maps.
+        embedding_space is None for a universe trained on another rank."""
+        uid = self.next_universe_id
+        em = np.ascontiguousarray(ent_remap, dtype=np.int64)
+        rm = np.ascontiguousarray(rel_remap, dtype=np.int64)
+        emap = self.entity_id_mappings[uid]
+        for local, g in enumerate(em.tolist()):
+            self.entity_universes[g].add(uid)
+            emap[g] = local
+        rmap = self.relation_id_mappings[uid]
+        for local, g in enumerate(rm.tolist()):
+            self.relation_universes[g].add(uid)
+            rmap[g] = local
+        if embedding_space is not None:
+            self.add_embedding_space(embedding_space)
+        self._remap_cache[uid] = self._remaps_from_arrays(em, rm)
+        self.next_universe_id += 1
+        return uid
+
+    def _commit(self, rec):
+        assert rec["id"] == self.next_universe_id
+        world, rank = _dist()
+        uid = self.add_universe(rec["kge"] if rec["id"] % world == rank else None, rec["ent_remap"],
+                                rec["rel_remap"])
+        if rec["losses"] is not None:
+            self.last_universe_losses[uid] = rec["losses"]
+        self.universe_hparams[uid] = {k: rec[k] for k in ("tc", "balance", "margin", "epochs", "lr", "batch_size",
+                                                         "train_total")}
+
+    def train_parallel_universes(self, num_of_embedding_spaces):
+        self._check_setup()
+        training_duration = 0.0
+        done = 0
+        stop = False
+        while done < num_of_embedding_spaces and not stop:
+            wave = num_of_embedding_spaces - done
+            if self.universe_wave_size:
+                wave = min(wave, int(self.universe_wave_size))
+            ids = list(range(self.next_universe_id, self.next_universe_id + wave))
+            t0 = time.time()
+            recs = self._train_wave(ids)
+            per_universe = (time.time() - t0) / max(len(recs), 1)
+            print("trained universes %d..%d on the GPU (%.3f s)" % (ids[0], ids[-1], per_universe * len(recs)))
+            for rec in recs:
+                universe_id = done
+                self._commit(rec)
+                training_duration += per_universe
+                if (universe_id + 1) % self.valid_steps == 0:
+                    print("Universe %d has finished, validating..." % (self.next_universe_id - 1))
+                    self.eval_universes(eval_mode='valid')
+                    hit10 = self.valid()
+                    print("Current hit@10: {}".format(hit10))
+                    if hit10 > self.best_hit10:
+                        self.best_hit10 = hit10
+                        print("Best model | hit@10 of valid set is %f" % self.best_hit10)
+                        print('Save model at universe %d.' % self.next_universe_id)
+                        self.save_model("Best_model_Pu{}_{}.ckpt".format(self.embedding_model.__name__,
+                                                                         self.training_identifier))
+                        self.bad_counts = 0
+                    else:
+                        print("Hit@10 of valid set is %f | bad count is %d" % (hit10, self.bad_counts))
+                        self.bad_counts += 1
+                    if self.bad_counts == self.early_stopping_patience:
+                        print("Early stopping at universe {}".format(self.next_universe_id - 1))
+                        self.get_best_state()
+                        stop = True
+                        break
+                if self.save_steps and self.checkpoint_dir and (universe_id + 1) % self.save_steps == 0:
+                    print('Save model at universe %d.' % self.next_universe_id)
+                    self.save_model()
+                done += 1
+        print('Time took for creation of embedding spaces: {:5.3f}s'.format(training_duration), end='\n')
+
+    # ------------------------------------------------------------------ global energy estimation -
+    @staticmethod
+    def _remaps_from_arrays(em, rm):
+        eo = np.argsort(em, kind="stable")
+        ro = np.argsort(rm, kind="stable")
+        return em, rm, em[eo], eo, rm[ro], ro
+
+    def _remaps(self, uid):
+        c = self._remap_cache.get(uid)
+        if c is None:
+            emap, rmap = self.entity_id_mappings[uid], self.relation_id_mappings[uid]
+            em = np.zeros(len(emap), dtype=np.int64)
+            for g, l in emap.items():
+                em[l] = g
+            rm = np.zeros(len(rmap), dtype=np.int64)
+            for g, l in rmap.items():
+                rm[l] = g
+            c = self._remap_cache[uid] = self._remaps_from_arrays(em, rm)
+        return c
+
+    @staticmethod
+    def _lookup(sorted_g, order, q):
+        """local ids of global ids q in a universe (-1 where absent)."""
+        if len(sorted_g) == 0:
+            return np.full(len(q), -1, dtype=np.int64)
+        pos = np.searchsorted(sorted_g, q)
+        pos = np.minimum(pos, len(sorted_g) - 1)
+        hit = sorted_g[pos] == q
+        return np.where(hit, order[pos], -1)
+
+    def _store(self, eval_mode):
+        st = self._stores.get(eval_mode)
+        if st is None:
+            loader = self.data_loader if eval_mode == 'test' else self.valid_dataloader
+            h, t, r = loader.eval_triples()
+            dev = torch.device("cuda", torch.cuda.current_device())
+            st = self._stores[eval_mode] = _KeyStore(h, t, r, self.ent_tot, dev)
+        return st
+
+    def _fold(self, st, universes):
+        """MIN the scores of `universes` (this rank's trained ones) into the store's rows."""
+        L = _native.lib()
+        world, rank = _dist()
+        local = [u for u in universes if u in self.trained_embedding_spaces]
+        lp_us, pairs = [], []
+        model_id = p_norm = norm_flag = None
+        for slot, u in enumerate(local):
+            kge = self.trained_embedding_spaces[u]
+            if not next(kge.parameters()).is_cuda:
+                kge.cuda()
+            em, rm, eg, eo, rg, ro = self._remaps(u)
+            dr = self._dev_remaps.get(u)
+            if dr is None:
+                dr = self._dev_remaps[u] = torch.from_numpy(em).cuda()
+            ent, rel, nv = kge.tables()
+            U = _native.LpUniverse()
+            U.ent, U.rel = ent.data_ptr(), rel.data_ptr()
+            U.normv = nv.data_ptr() if nv is not None else None
+            U.ent_total, U.rel_total, U.dim = ent.shape[0], rel.shape[0], ent.shape[1]
+            U.d_ent_remap = dr.data_ptr()
+            lp_us.append(U)
+            model_id, p_norm, norm_flag = kge.native_model, int(kge.p_norm), 1 if kge.norm_flag else 0
+            la = self._lookup(eg, eo, st.key_anchor)
+            lr_ = self._lookup(rg, ro, st.key_rel)
+            sel = np.nonzero((la >= 0) & (lr_ >= 0))[0]
+            for k in sel.tolist():
+                pairs.append((k, slot, int(la[k]), int(lr_[k]), int(st.key_side[k])))
+        if pairs:
+            arr_u = (_native.LpUniverse * len(lp_us))(*lp_us)
+            arr_p = (_native.LpPair * len(pairs))(*[_native.LpPair(*p) for p in pairs])
+            tup = st.tuple if self.missing_embedding_handling == 'null_vector' else None
+            _native.check(L.pt_lp_min_scores(arr_u, len(lp_us), model_id, p_norm, norm_flag, arr_p, len(pairs),
+                                             self.ent_tot, _native.ptr(st.rows), _native.ptr(tup), _native.stream()))
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(st.rows, op=dist.ReduceOp.MIN)
+            dist.all_reduce(st.tuple, op=dist.ReduceOp.MIN)
+
+    def eval_universes(self, eval_mode):
+        if self.incremental_strategy == "deprecate":
+            raise NotImplementedError("the 'deprecate' incremental strategy is outside the accelerated path")
+        st = self._store(eval_mode)
+        start = self.current_tested_universes if eval_mode == 'test' else self.current_validated_universes
+        start = max(start, 0)
+        universes = list(range(start, self.next_universe_id))
+        print("Global energy estimation.")
+        print("- Mode: {}".format(eval_mode))
+        if universes:
+            print("- Universe range to obtain local energies: ({} -> {})".format(min(universes), max(universes)))
+            self._fold(st, universes)
+            st.folded = self.next_universe_id
+            if eval_mode == 'test':
+                self.current_tested_universes = self.next_universe_id
+            elif eval_mode == 'valid':
+                self.current_validated_universes = self.next_universe_id
+        else:
+            print("- No universes to be evaluated.")
+
+    def _ranks(self, eval_mode):
+        """raw / filtered ranks of every query of the split (head side, tail side) on the GPU."""
+        L = _native.lib()
+        st = self._store(eval_mode)
+        known = L.pt_legacy_known()
+        if not known:
+            raise RuntimeError("no evaluation data imported (TestDataLoader.read() imports it)")
+        dev = st.rows.device
+        n = len(st.h)
+        out = []
+        for side, anchor, truth in ((0, st.t, st.h), (1, st.h, st.t)):
+            off = np.zeros(n + 1, dtype=np.int64)
+            a = np.ascontiguousarray(anchor, dtype=np.int64)
+            r = np.ascontiguousarray(st.r, dtype=np.int64)
+            _native.check(L.pt_known_partners(known, side, n, a.ctypes.data, r.ctypes.data, off.ctypes.data, None))
+            part = np.zeros(max(int(off[-1]), 1), dtype=np.int64)
+            _native.check(L.pt_known_partners(known, side, n, a.ctypes.data, r.ctypes.data, off.ctypes.data,
+                                              part.ctypes.data))
+            d_row = torch.from_numpy(st.q_row[side]).to(dev)
+            d_truth = torch.from_numpy(np.ascontiguousarray(truth, dtype=np.int64)).to(dev)
+            d_off = torch.from_numpy(off).to(dev)
+            d_part = torch.from_numpy(part).to(dev)
+            d_repl = st.tuple[d_row].contiguous() if self.missing_embedding_handling == 'null_vector' else None
+            raw = torch.zeros(n, dtype=torch.int64, device=dev)
+            filt = torch.zeros(n, dtype=torch.int64, device=dev)
+            _native.check(L.pt_rank_rows(_native.ptr(st.rows), self.ent_tot, _native.ptr(d_row), _native.ptr(d_truth),
+                                         _native.ptr(d_repl), _native.ptr(d_off), _native.ptr(d_part), n,
+                                         _native.ptr(raw), _native.ptr(filt), _native.stream()))
+            out.append((raw.cpu().numpy(), filt.cpu().numpy()))
+        return out   # [(raw_head, filt_head), (raw_tail, filt_tail)]
+
+    def valid(self):
+        """Filtered hit@10 of the validation split (validHead/validTail + getValidHit10, Valid.h:117-259)."""
+        (_, fh), (_, ft) = self._ranks('valid')
+        n = np.float32(max(len(fh), 1))
+        lh = np.float32(np.count_nonzero(fh < 10)) / n
+        rt = np.float32(np.count_nonzero(ft < 10)) / n
+        return float((lh + rt) / np.float32(2))
+
+    def global_energy_estimation(self, data):
+        """Candidate-order score vector of one link-prediction query (:556-601), from the device rows."""
+        mode = data['mode']
+        batch_h, batch_t, batch_r = data['batch_h'], data['batch_t'], data['batch_r']
+        rel = int(batch_r[0])
+        if mode == 'head_batch':
+            side, anchor, ents = 0, int(batch_t[0]), batch_h
+        elif mode == 'tail_batch':
+            side, anchor, ents = 1, int(batch_h[0]), batch_t
+        else:
+            raise ValueError("global_energy_estimation needs head_batch / tail_batch data")
+        ents = np.asarray(ents, dtype=np.int64)
+        scores = np.full(len(ents), np.inf, dtype=np.float32)
+        repl = float("inf")
+        for st in self._stores.values():
+            k = st.row(side, anchor, rel)
+            if k is not None and st.folded > 0:
+                scores = st.rows[k].index_select(0, torch.from_numpy(ents).to(st.rows.device)).cpu().numpy()
+                repl = float(st.tuple[k].item())
+                break
+        if self.missing_embedding_handling == 'null_vector' and repl != float("inf"):
+            scores[scores == np.inf] = repl
+        return scores
+
+    def test_one_step(self, data):
+        if data['mode'] in ('head_batch', 'tail_batch'):
+            return self.global_energy_estimation(data)
+        raise NotImplementedError("triple classification ('normal' mode) is outside the accelerated path")
+
+    def run_link_prediction(self, type_constrain=False):
+        if type_constrain:
+            raise NotImplementedError("type-constrained ranking is outside the accelerated path")
+        self.data_loader.set_sampling_mode('link')
+        self.eval_universes(eval_mode='test')
+        (rh, fh), (rt, ft) = self._ranks('test')
+        L = _native.lib()
+        met = np.zeros(10, dtype=np.float32)
+        _native.check(L.pt_lp_metrics(rh.ctypes.data, fh.ctypes.data, rt.ctypes.data, ft.ctypes.data, len(rh),
+                                      met.ctypes.data))
+        self.last_ranks = (rh, fh, rt, ft)
+        mrr, mr, hit10, hit3, hit1 = (float(x) for x in met[:5])
+        print('Mean Reciprocal Rank: {}'.format(mrr))
+        print('Mean Rank: {}'.format(mr))
+        print('Hits@10: {}'.format(hit10))
+        print('Hits@3: {}'.format(hit3))
+        print('Hits@1: {}'.format(hit1))
+        return mrr, mr, hit10, hit3, hit1
+
+    def run_triple_classification(self, threshlod=None):
+        raise NotImplementedError("triple classification is outside the accelerated path")
+
+    def reset_evaluation_helpers(self):
+        self.current_validated_universes = 0
+        self.current_tested_universes = 0
+        self._stores.clear()
+        self.evaluation_head2tail_triple_score_dict.clear()
+        self.evaluation_tail2head_triple_score_dict.clear()
+        self.evaluation_head2rel_tuple_score_dict.clear()
+        self.evaluation_tail2rel_tuple_score_dict.clear()
+        self.incremental_strategy = "normal"
+
+    # ------------------------------------------------------------------ single-triple helpers ---
+    def gather_embedding_spaces(self, entity_1, rel, entity_2=None):
+        ids = self.entity_universes[entity_1].intersection(self.relation_universes[rel])
+        if entity_2 is not None:
+            ids = ids.intersection(self.entity_universes[entity_2])
+        return ids
+
+    def calc_tuple_score(self, local_ent_id, local_rel_id, mode, embedding_space):
+        dev = next(embedding_space.parameters()).device
+        rel_embedding = embedding_space.rel_embeddings(torch.tensor([local_rel_id], device=dev).reshape(-1))
+        ent = embedding_space.ent_embeddings(torch.tensor([local_ent_id], device=dev).reshape(-1))
+        zero_vec = torch.tensor([[0.0]], device=dev)
+        if mode == 'head_batch':
+            return embedding_space._calc(zero_vec, ent, rel_embedding, mode)
+        return embedding_space._calc(ent, zero_vec, rel_embedding, mode)
+
+    def predict_triple(self, head_id, rel_id, tail_id, mode='normal'):
+        best = float("inf")
+        for u in self.gather_embedding_spaces(head_id, rel_id, tail_id):
+            sp = self.trained_embedding_spaces.get(u)
+            if sp is None:
+                continue
+            s = sp.predict({"batch_h": np.array([self.entity_id_mappings[u][head_id]]),
+                            "batch_t": np.array([self.entity_id_mappings[u][tail_id]]),
+                            "batch_r": np.array([self.relation_id_mappings[u][rel_id]]), "mode": mode})
+            best = min(best, float(np.asarray(s).reshape(-1)[0]))
+        return best
+
+    # ------------------------------------------------------------------ state / checkpoints -----
+    def save_model(self, filename=None):
+        save_directory = self.checkpoint_dir
+        if not filename:
+            filename = "Pu{}_learned_spaces-{}_{}.ckpt".format(self.embedding_model.__name__,
+                                                               self.next_universe_id, self.training_identifier)
+        os.makedirs(save_directory, exist_ok=True)
+        self.save_parameters(os.path.join("{}{}".format(save_directory, filename)))
+
+    def save_best_state(self):
+        self.best_state = self.get_state()
+
+    def get_state(self):
+        return {
+            "trained_embedding_spaces": deepcopy(self.trained_embedding_spaces),
+            "next_universe_id": self.next_universe_id,
+            "entity_id_mappings": deepcopy(self.entity_id_mappings),
+            "relation_id_mappings": deepcopy(self.relation_id_mappings),
+            "entity_universes": deepcopy(self.entity_universes),
+            "relation_universes": deepcopy(self.relation_universes),
+        }
+
+    def get_best_state(self):
+        if self.best_state:
+            print("Get best state...")
+            self.trained_embedding_spaces = self.best_state["trained_embedding_spaces"]
+            self.entity_id_mappings = self.best_state["entity_id_mappings"]
+            self.relation_id_mappings = self.best_state["relation_id_mappings"]
+            self.entity_universes = self.best_state["entity_universes"]
+            self.relation_universes = self.best_state["relation_universes"]
+            self.next_universe_id = self.best_state["next_universe_id"]
+            self._remap_cache.clear()
+            self._dev_remaps.clear()
+        return self
+
+    def extend_state_dict(self):
+        return {'initial_num_universes': self.initial_num_universes,
+                'next_universe_id': self.next_universe_id,
+                'trained_embedding_spaces': self.trained_embedding_spaces,
+                'entity_id_mappings': self.entity_id_mappings,
+                'relation_id_mappings': self.relation_id_mappings,
+                'entity_universes': self.entity_universes,
+                'relation_universes': self.relation_universes,
+                'min_margin': self.min_margin,
+                'max_margin': self.max_margin,
+                'min_lr': self.min_lr,
+                'max_lr': self.max_lr,
+                'min_num_epochs': self.min_num_epochs,
+                'max_num_epochs': self.max_num_epochs,
+                'min_triple_constraint': self.min_triple_constraint,
+                'max_triple_constraint': self.max_triple_constraint,
+                'min_balance': self.min_balance,
+                'max_balance': self.max_balance,
+                'embedding_model': self.embedding_model,
+                'embedding_model_param': self.embedding_model_param,
+                'best_hit10': self.best_hit10,
+                'bad_counts': self.bad_counts,
+                'current_tested_universes': self.current_tested_universes,
+                'current_validated_universes': self.current_validated_universes}
+
+    def process_state_dict(self, state_dict):
+        self.initial_num_universes = state_dict['initial_num_universes']
+        self.next_universe_id = state_dict['next_universe_id']
+        self.trained_embedding_spaces = state_dict['trained_embedding_spaces']
+        self.entity_id_mappings = state_dict['entity_id_mappings']
+        self.relation_id_mappings = state_dict['relation_id_mappings']
+        self.entity_universes = state_dict['entity_universes']
+        self.relation_universes = state_dict['relation_universes']
+        self.min_margin = state_dict['min_margin']
+        self.max_margin = state_dict['max_margin']
+        self.min_lr = state_dict['min_lr']
+        self.max_lr = state_dict['max_lr']
+        self.min_num_epochs = state_dict['min_num_epochs']
+        self.max_num_epochs = state_dict['max_num_epochs']
+        self.min_triple_constraint = state_dict['min_triple_constraint']
+        self.max_triple_constraint = state_dict['max_triple_constraint']
+        if 'min_balance' in state_dict:
+            self.min_balance = state_dict['min_balance']
+            self.max_balance = state_dict['max_balance']
+        elif 'embedding_model' in state_dict:   # the reference's elif (:906-912)
+            self.embedding_model = state_dict['embedding_model']
+            self.embedding_model_param = state_dict['embedding_model_param']
+        if 'best_hit10' in state_dict:
+            self.best_hit10 = state_dict['best_hit10']
+            self.bad_counts = state_dict['bad_counts']
+        # the reference never restores its score dictionaries (`if '' in state_dict`, :917): the next
+        # evaluation re-folds every universe; the device rows start empty here for the same effect
+        self._stores.clear()
+        self.current_tested_universes = 0
+        self.current_validated_universes = 0
+        self._remap_cache.clear()
+        self._dev_remaps.clear()
+
+    def save_parameters(self, path):
+        torch.save(self.extend_state_dict(), path)
+
+    def load_parameters(self, filename):
+        # checkpoints written by save_parameters (models + python containers): a full unpickle of a
+        # file this code wrote
+        state_dict = torch.load(self.checkpoint_dir + filename, weights_only=False)
+        self.process_state_dict(state_dict)
+
+    def calculate_unembedded_ratio(self, mode='examine_entities'):
+        num_unembedded = 0
+        mapping_dict = self.entity_universes if mode == 'examine_entities' else self.relation_universes
+        num_total = self.train_dataloader.entTotal if mode == 'examine_entities' else self.train_dataloader.relTotal
+        for i in range(num_total):
+            if len(mapping_dict[i]) == 0:
+                num_unembedded += 1
+        return num_unembedded / num_total
+
+    def extend_parallel_universe(self, ParallelUniverse_inst):
+        shift = self.next_universe_id
+        for universe_id in list(ParallelUniverse_inst.trained_embedding_spaces.keys()):
+            self.trained_embedding_spaces[universe_id + shift] = \
+                ParallelUniverse_inst.trained_embedding_spaces[universe_id]
+        for entity in range(ParallelUniverse_inst.ent_tot):
+            self.entity_universes[entity].update(u + shift for u in ParallelUniverse_inst.entity_universes[entity])
+        for relation in range(ParallelUniverse_inst.rel_tot):
+            self.relation_universes[relation].update(
+                u + shift for u in ParallelUniverse_inst.relation_universes[relation])
+        for u in range(ParallelUniverse_inst.next_universe_id):
+            for k, v in ParallelUniverse_inst.entity_id_mappings[u].items():
+                self.entity_id_mappings[shift + u][k] = v
+            for k, v in ParallelUniverse_inst.relation_id_mappings[u].items():
+                self.relation_id_mappings[shift + u][k] = v
+        self.next_universe_id += ParallelUniverse_inst.next_universe_id

