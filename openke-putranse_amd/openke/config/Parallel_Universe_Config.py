@@ -68,6 +68,49 @@ def _dist():
     return 1, 0
 
 
+def universe_owner(universe_id, world_size):
+    """Rank that trains universe `universe_id` (universes are independent: round-robin sharding)."""
+    return universe_id % world_size
+
+
+def min_combine(tensors):
+    """Element-wise MIN of the same tensors across all ranks (RCCL all_reduce(MIN) on the GPU path,
+    gloo on CPU); no-op on one process. The global energy of a key is the min over every universe,
+    whichever rank trained it (Parallel_Universe_Config.py:516-543)."""
+    world, _ = _dist()
+    if world > 1:
+        import torch.distributed as dist
+        for t in tensors:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return tensors
+
+
+def lookup_local(sorted_global, order, query):
+    """Local ids of global ids `query` in a universe given its sorted global ids and their local ids
+    (-1 where absent)."""
+    query = np.asarray(query, dtype=np.int64)
+    if len(sorted_global) == 0:
+        return np.full(len(query), -1, dtype=np.int64)
+    pos = np.searchsorted(sorted_global, query)
+    pos = np.minimum(pos, len(sorted_global) - 1)
+    hit = sorted_global[pos] == query
+    return np.where(hit, order[pos], -1)
+
+
+def lp_pairs(slot, ent_remap, rel_remap, key_anchor, key_rel, key_side):
+    """(key, universe slot, local anchor, local relation, side) for every evaluation key whose anchor
+    entity AND relation the universe holds - the universes eval_universes scores for that key
+    (Parallel_Universe_Config.py:470-476)."""
+    em = np.asarray(ent_remap, dtype=np.int64)
+    rm = np.asarray(rel_remap, dtype=np.int64)
+    eo = np.argsort(em, kind="stable")
+    ro = np.argsort(rm, kind="stable")
+    la = lookup_local(em[eo], eo, key_anchor)
+    lr = lookup_local(rm[ro], ro, key_rel)
+    sel = np.nonzero((la >= 0) & (lr >= 0))[0]
+    return [(int(k), slot, int(la[k]), int(lr[k]), int(key_side[k])) for k in sel]
+
+
 class _KeyStore(object):
     """Device score rows of one evaluation split: one row per (side, anchor, relation) key.
 
@@ -292,7 +335,7 @@ class Parallel_Universe_Config(Tester):
                        "balance": balance, "margin": margin, "epochs": epochs, "lr": lr, "batch_size": bs,
                        "train_total": N_u, "losses": None}
                 recs.append(rec)
-                if uid % world != rank:
+                if universe_owner(uid, world) != rank:
                     continue   # trained on another rank
                 kge.to(dev)
                 ent, rel, nv = kge.tables()
@@ -358,7 +401,7 @@ class Parallel_Universe_Config(Tester):
     def _commit(self, rec):
         assert rec["id"] == self.next_universe_id
         world, rank = _dist()
-        uid = self.add_universe(rec["kge"] if rec["id"] % world == rank else None, rec["ent_remap"],
+        uid = self.add_universe(rec["kge"] if universe_owner(rec["id"], world) == rank else None, rec["ent_remap"],
                                 rec["rel_remap"])
         if rec["losses"] is not None:
             self.last_universe_losses[uid] = rec["losses"]
@@ -429,16 +472,6 @@ class Parallel_Universe_Config(Tester):
             c = self._remap_cache[uid] = self._remaps_from_arrays(em, rm)
         return c
 
-    @staticmethod
-    def _lookup(sorted_g, order, q):
-        """local ids of global ids q in a universe (-1 where absent)."""
-        if len(sorted_g) == 0:
-            return np.full(len(q), -1, dtype=np.int64)
-        pos = np.searchsorted(sorted_g, q)
-        pos = np.minimum(pos, len(sorted_g) - 1)
-        hit = sorted_g[pos] == q
-        return np.where(hit, order[pos], -1)
-
     def _store(self, eval_mode):
         st = self._stores.get(eval_mode)
         if st is None:
@@ -471,21 +504,14 @@ class Parallel_Universe_Config(Tester):
             U.d_ent_remap = dr.data_ptr()
             lp_us.append(U)
             model_id, p_norm, norm_flag = kge.native_model, int(kge.p_norm), 1 if kge.norm_flag else 0
-            la = self._lookup(eg, eo, st.key_anchor)
-            lr_ = self._lookup(rg, ro, st.key_rel)
-            sel = np.nonzero((la >= 0) & (lr_ >= 0))[0]
-            for k in sel.tolist():
-                pairs.append((k, slot, int(la[k]), int(lr_[k]), int(st.key_side[k])))
+            pairs.extend(lp_pairs(slot, em, rm, st.key_anchor, st.key_rel, st.key_side))
         if pairs:
             arr_u = (_native.LpUniverse * len(lp_us))(*lp_us)
             arr_p = (_native.LpPair * len(pairs))(*[_native.LpPair(*p) for p in pairs])
             tup = st.tuple if self.missing_embedding_handling == 'null_vector' else None
             _native.check(L.pt_lp_min_scores(arr_u, len(lp_us), model_id, p_norm, norm_flag, arr_p, len(pairs),
                                              self.ent_tot, _native.ptr(st.rows), _native.ptr(tup), _native.stream()))
-        if world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(st.rows, op=dist.ReduceOp.MIN)
-            dist.all_reduce(st.tuple, op=dist.ReduceOp.MIN)
+        min_combine([st.rows, st.tuple])
 
     def eval_universes(self, eval_mode):
         if self.incremental_strategy == "deprecate":
