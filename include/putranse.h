@@ -114,6 +114,9 @@ int pt_score(const pt_model_desc *m, int32_t mode, const int64_t *d_h, const int
  * e + (r - t)); side 1: tail prediction ((h + r) - e). d_out is [nq][ent_total]; nq <= 65535. */
 int pt_score_queries(const pt_model_desc *m, int32_t side, const int64_t *d_qh, const int64_t *d_qt,
                      const int64_t *d_qr, int64_t nq, float *d_out, void *stream);
+/* the same scores in global entity order (column e = entity e), the layout pt_rank_rows ranks */
+int pt_score_rows(const pt_model_desc *m, int32_t side, const int64_t *d_qh, const int64_t *d_qt,
+                  const int64_t *d_qr, int64_t nq, float *d_out, void *stream);
 /* Metrics from per-query ranks with the reference's float accumulation (Test.h:213-223, :398-454):
  * metrics[0..4] = filtered {MRR, MR, Hits@10, Hits@3, Hits@1}, metrics[5..9] = the raw ones. */
 int pt_lp_metrics(const int64_t *rank_head, const int64_t *frank_head, const int64_t *rank_tail,

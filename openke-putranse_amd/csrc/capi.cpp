@@ -474,6 +474,20 @@ extern "C" int pt_score_queries(const pt_model_desc *m, int32_t side, const int6
     return PT_OK;
 }
 
+extern "C" int pt_score_rows(const pt_model_desc *m, int32_t side, const int64_t *d_qh, const int64_t *d_qt,
+                             const int64_t *d_qr, int64_t nq, float *d_out, void *stream) {
+    pt::StepParams P{};
+    pt_model_desc mm = *m;
+    if (!mm.ent_acc) mm.opt = PT_SGD;
+    int rc = desc_to_params(&mm, P);
+    if (rc) return rc;
+    PT_CHECK(side == 0 || side == 1, PT_EINVAL, "side must be 0 (head prediction) or 1 (tail prediction)");
+    PT_CHECK(nq <= 65535, PT_EINVAL, "at most 65535 queries per call");
+    PT_CHECK((d_qh && d_qt && d_qr && d_out) || nq == 0, PT_EINVAL, "pt_score_rows: null argument");
+    PT_HIP(pt::launch_score_queries(P, side, d_qh, d_qt, d_qr, nq, P.ent_total, d_out, (hipStream_t)stream, 1));
+    return PT_OK;
+}
+
 // Test.h:213-223 + :398-454 accumulation for n ranked queries (float accumulators, same order)
 extern "C" int pt_lp_metrics(const int64_t *rank_head, const int64_t *frank_head, const int64_t *rank_tail,
                              const int64_t *frank_tail, int64_t n, float *metrics) {

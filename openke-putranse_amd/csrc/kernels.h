@@ -98,7 +98,7 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
 hipError_t launch_score(const StepParams &P, int mode, const int64_t *h, const int64_t *t, const int64_t *r, int64_t n,
                         float *out, hipStream_t st);
 hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh, const int64_t *qt, const int64_t *qr,
-                                int64_t nq, int64_t E, float *out, hipStream_t st);
+                                int64_t nq, int64_t E, float *out, hipStream_t st, int global_order = 0);
 hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, int64_t dim, int64_t max_ent,
                          int model, int p_norm, int norm_flag, int64_t global_E, float *rows, float *tuple_min,
                          hipStream_t st);

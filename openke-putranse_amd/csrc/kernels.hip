@@ -586,7 +586,7 @@ __global__ __launch_bounds__(256) void k_score(StepParams P, int mode, const int
 template <int MODEL, int G, int VEC, int KCH>
 __global__ __launch_bounds__(256) void k_score_queries(StepParams P, int side, const int64_t *__restrict__ qh,
                                                        const int64_t *__restrict__ qt, const int64_t *__restrict__ qr,
-                                                       int64_t nq, int64_t E, float *__restrict__ out) {
+                                                       int64_t nq, int64_t E, float *__restrict__ out, int global_order) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = 256 / G;
     const int lane = threadIdx.x % G;
@@ -618,7 +618,9 @@ __global__ __launch_bounds__(256) void k_score_queries(StepParams P, int side, c
     for (int k = 0; k < Vec::N; ++k) base.x[k] = side == 0 ? rh.x[k] - ah.x[k] : ah.x[k] + rh.x[k];
     float *row = out + q * E;
     for (int64_t j = (int64_t)blockIdx.x * GPB + grp; j < E; j += (int64_t)gridDim.x * GPB) {
-        const int64_t e = j == 0 ? truth : (j - 1 < truth ? j - 1 : j);
+        // candidate order of getHeadBatch/getTailBatch ([truth, 0..E-1 without truth], Test.h:37-107),
+        // or column = entity id (global_order, the layout pt_rank_rows ranks)
+        const int64_t e = global_order ? j : (j == 0 ? truth : (j - 1 < truth ? j - 1 : j));
         Vec X, xh, v;
         vload(X, P.ent + e * D, D, lane);
         if constexpr (MODEL == 1) {
@@ -889,7 +891,7 @@ hipError_t launch_score(const StepParams &P, int mode, const int64_t *h, const i
 }
 
 hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh, const int64_t *qt, const int64_t *qr,
-                                int64_t nq, int64_t E, float *out, hipStream_t st) {
+                                int64_t nq, int64_t E, float *out, hipStream_t st, int global_order) {
     if (nq <= 0) return hipSuccess;
     const Shape s = pick_shape(P.dim);
     const int64_t gpb = 256 / s.G;
@@ -900,10 +902,10 @@ hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh
     if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                                                 \
         if (P.model == 0)                                                                                            \
             hipLaunchKernelGGL((dev::k_score_queries<0, G_, V_, K_>), grid, block, 0, st, P, side, qh, qt, qr, nq, E, \
-                               out);                                                                                 \
+                               out, global_order);                                                                   \
         else                                                                                                         \
             hipLaunchKernelGGL((dev::k_score_queries<1, G_, V_, K_>), grid, block, 0, st, P, side, qh, qt, qr, nq, E, \
-                               out);                                                                                 \
+                               out, global_order);                                                                   \
         return hipGetLastError();                                                                                  \
     }
     PT_SHAPES(PT_SQ)

@@ -69,6 +69,7 @@ SIGNATURES = {
     "pt_trainer_run_timed": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "pt_score": (ctypes.c_int, [ctypes.POINTER(ModelDesc), c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "pt_score_queries": (ctypes.c_int, [ctypes.POINTER(ModelDesc), c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "pt_score_rows": (ctypes.c_int, [ctypes.POINTER(ModelDesc), c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "pt_lp_metrics": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "pt_universe_build": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_f32, ctypes.POINTER(c_vp)]),
     "pt_universe_free": (ctypes.c_int, [c_vp]),

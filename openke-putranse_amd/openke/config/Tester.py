@@ -1,10 +1,11 @@
 # coding:utf-8
 """Link-prediction tester (mirror of openke/config/Tester.py:17-93).
 
-run_link_prediction() returns the reference's (mrr, mr, hit10, hit3, hit1) (filtered). Candidate
-scores for a whole block of test queries come from one HIP launch (pt_score_queries) in exactly the
-candidate order of getHeadBatch/getTailBatch; ranks use the reference's rules (Test.h:118-359) on host
-threads, and the metrics its float accumulation (Test.h:398-454)."""
+run_link_prediction() returns the reference's (mrr, mr, hit10, hit3, hit1) (filtered). Scores for a
+block of test queries come from one HIP launch (pt_score_rows: every entity as the missing side, row in
+entity order), ranks from one more (pt_rank_rows: raw and filtered counts of testHead/testTail,
+Test.h:118-359, with the known-triple filter as a per-query partner list), the metrics with the
+reference's float accumulation (Test.h:398-454). Only the ranks leave the GPU."""
 import ctypes
 
 import numpy as np
@@ -60,22 +61,35 @@ class Tester(object):
         known = self.lib.pt_legacy_known()
         if not known:
             raise RuntimeError("no test data imported (TestDataLoader.read() imports it)")
+        kge = self.model
+        dev = kge.ent_embeddings.weight.device
+        desc = kge.native_desc()
         ranks = [np.zeros(n, dtype=np.int64) for _ in range(4)]
-        chunk = max(1, min(65535, (256 << 20) // (4 * max(E, 1))))
+        chunk = max(1, min(65535, (1 << 30) // (4 * max(E, 1))))
         for s in range(0, n, chunk):
             e = min(n, s + chunk)
-            hh, tt, rr = h[s:e].copy(), t[s:e].copy(), r[s:e].copy()
-            for side in (0, 1):
-                con = self._query_scores(side, hh, tt, rr).cpu().numpy()
-                raw = ranks[2 * side][s:e]
-                filt = ranks[2 * side + 1][s:e]
-                rawb = np.zeros(e - s, dtype=np.int64)
-                filtb = np.zeros(e - s, dtype=np.int64)
-                _native.check(self.lib.pt_rank_queries(known, E, hh.ctypes.data, tt.ctypes.data, rr.ctypes.data,
-                                                       e - s, side, con.ctypes.data, rawb.ctypes.data,
-                                                       filtb.ctypes.data, 0))
-                raw[:] = rawb
-                filt[:] = filtb
+            m = e - s
+            hh, tt, rr = (np.ascontiguousarray(x[s:e], dtype=np.int64) for x in (h, t, r))
+            qh, qt, qr = (torch.from_numpy(x).to(dev) for x in (hh, tt, rr))
+            rows = torch.empty((m, E), dtype=torch.float32, device=dev)
+            row_of = torch.arange(m, dtype=torch.int64, device=dev)
+            for side, anchor, truth in ((0, tt, qh), (1, hh, qt)):
+                _native.check(self.lib.pt_score_rows(ctypes.byref(desc), side, _native.ptr(qh), _native.ptr(qt),
+                                                     _native.ptr(qr), m, _native.ptr(rows), _native.stream()))
+                off = np.zeros(m + 1, dtype=np.int64)
+                _native.check(self.lib.pt_known_partners(known, side, m, anchor.ctypes.data, rr.ctypes.data,
+                                                         off.ctypes.data, None))
+                part = np.zeros(max(int(off[-1]), 1), dtype=np.int64)
+                _native.check(self.lib.pt_known_partners(known, side, m, anchor.ctypes.data, rr.ctypes.data,
+                                                         off.ctypes.data, part.ctypes.data))
+                d_off, d_part = torch.from_numpy(off).to(dev), torch.from_numpy(part).to(dev)
+                raw = torch.zeros(m, dtype=torch.int64, device=dev)
+                filt = torch.zeros(m, dtype=torch.int64, device=dev)
+                _native.check(self.lib.pt_rank_rows(_native.ptr(rows), E, _native.ptr(row_of), _native.ptr(truth),
+                                                    None, _native.ptr(d_off), _native.ptr(d_part), m, _native.ptr(raw),
+                                                    _native.ptr(filt), _native.stream()))
+                ranks[2 * side][s:e] = raw.cpu().numpy()
+                ranks[2 * side + 1][s:e] = filt.cpu().numpy()
         return ranks
 
     def run_link_prediction(self, type_constrain=False):

@@ -231,3 +231,57 @@ def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(_native, "LIB_PATH", "/nonexistent/libputranse_hip.so")
     with pytest.raises(_native.NativeError):
         _native.lib()
+
+
+@pytest.mark.parametrize("dup", [False, True])
+def test_gpu_ranking_matches_host_ranking(dup):
+    """pt_score_rows + pt_rank_rows (GPU, entity order) == pt_score_queries + pt_rank_queries (host rules
+    of testHead/testTail on the candidate-order rows), including exact ties (duplicated entity rows)."""
+    from openke import _native
+    from openke.data import TestDataLoader
+    from openke.module.model import TransE
+    L = _native.lib()
+    tdl = TestDataLoader(KG_SMALL, "link")
+    E, R = tdl.get_ent_tot(), tdl.get_rel_tot()
+    torch.manual_seed(5)
+    kge = TransE(E, R, dim=16, p_norm=1, norm_flag=True).cuda()
+    if dup:   # many exact ties: every 4th entity copies its predecessor
+        w = kge.ent_embeddings.weight.data
+        w[1::4] = w[0::4][:w[1::4].shape[0]]
+    h, t, r = tdl.eval_triples()
+    known = L.pt_legacy_known()
+    desc = kge.native_desc()
+    n = len(h)
+    dev = torch.device("cuda")
+    qh, qt, qr = (torch.from_numpy(x).to(dev) for x in (h, t, r))
+    for side, anchor, truth in ((0, t, qh), (1, h, qt)):
+        cand = torch.empty((n, E), device=dev)
+        _native.check(L.pt_score_queries(ctypes.byref(desc), side, _native.ptr(qh), _native.ptr(qt), _native.ptr(qr),
+                                         n, _native.ptr(cand), _native.stream()))
+        con = cand.cpu().numpy()
+        raw_h, filt_h = np.zeros(n, np.int64), np.zeros(n, np.int64)
+        _native.check(L.pt_rank_queries(known, E, h.ctypes.data, t.ctypes.data, r.ctypes.data, n, side,
+                                        con.ctypes.data, raw_h.ctypes.data, filt_h.ctypes.data, 0))
+        rows = torch.empty((n, E), device=dev)
+        _native.check(L.pt_score_rows(ctypes.byref(desc), side, _native.ptr(qh), _native.ptr(qt), _native.ptr(qr), n,
+                                      _native.ptr(rows), _native.stream()))
+        a = np.ascontiguousarray(anchor)
+        rr = np.ascontiguousarray(r)
+        off = np.zeros(n + 1, np.int64)
+        _native.check(L.pt_known_partners(known, side, n, a.ctypes.data, rr.ctypes.data, off.ctypes.data, None))
+        part = np.zeros(max(int(off[-1]), 1), np.int64)
+        _native.check(L.pt_known_partners(known, side, n, a.ctypes.data, rr.ctypes.data, off.ctypes.data,
+                                          part.ctypes.data))
+        raw = torch.zeros(n, dtype=torch.int64, device=dev)
+        filt = torch.zeros(n, dtype=torch.int64, device=dev)
+        _native.check(L.pt_rank_rows(_native.ptr(rows), E, _native.ptr(torch.arange(n, device=dev)),
+                                     _native.ptr(truth), None, _native.ptr(torch.from_numpy(off).to(dev)),
+                                     _native.ptr(torch.from_numpy(part).to(dev)), n, _native.ptr(raw),
+                                     _native.ptr(filt), _native.stream()))
+        np.testing.assert_array_equal(raw.cpu().numpy(), raw_h)
+        np.testing.assert_array_equal(filt.cpu().numpy(), filt_h)
+        # the two kernels score every (query, entity) identically
+        gl = rows.cpu().numpy()
+        for q in range(0, n, 17):
+            cidx = oracle.candidates(E, int(h[q] if side == 0 else t[q]))
+            np.testing.assert_array_equal(con[q], gl[q][cidx])
