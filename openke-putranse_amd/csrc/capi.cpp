@@ -101,6 +101,7 @@ int desc_to_params(const pt_model_desc *m, pt::StepParams &P) {
     P.dim = m->dim;
     P.ent = m->ent; P.rel = m->rel; P.normv = m->normv;
     P.ent_acc = m->ent_acc; P.rel_acc = m->rel_acc; P.norm_acc = m->norm_acc;
+    if (const char *v = getenv("PT_STEP_DBG")) P.dbg = atoi(v);
     return PT_OK;
 }
 
@@ -298,19 +299,32 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
 // Launch recorder for the measurement hook: an event pair around every launch, by kernel kind
 // (0 sampling, 1 bucket scan, 2 forward/backward, 3 optimizer apply).
 struct Timing {
+    // events created up front (hipEventCreate between launches would stall the enqueue and let the
+    // GPU idle inside a measured interval)
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
     std::vector<std::tuple<int, hipEvent_t, hipEvent_t>> ev;
+    int reserve(size_t n) {
+        pool.resize(n);
+        for (auto &e : pool) PT_HIP(hipEventCreate(&e));
+        return PT_OK;
+    }
     int begin(int kind, hipStream_t st, hipEvent_t *a) {
-        PT_HIP(hipEventCreate(a));
+        if (used >= pool.size()) return pt::fail(PT_EHIP, "timing event pool exhausted");
+        *a = pool[used++];
         PT_HIP(hipEventRecord(*a, st));
         ev.emplace_back(kind, *a, nullptr);
         return PT_OK;
     }
     int end(hipStream_t st) {
-        hipEvent_t b;
-        PT_HIP(hipEventCreate(&b));
+        if (used >= pool.size()) return pt::fail(PT_EHIP, "timing event pool exhausted");
+        hipEvent_t b = pool[used++];
         PT_HIP(hipEventRecord(b, st));
         std::get<2>(ev.back()) = b;
         return PT_OK;
+    }
+    ~Timing() {
+        for (auto e : pool) (void)hipEventDestroy(e);
     }
 };
 
@@ -405,6 +419,11 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     Timing tm;
+    rc = tm.reserve((size_t)(8 * steps + 64));
+    if (rc) return rc;
+    // hold the stream in a short spin kernel while the host enqueues every measured launch, so each
+    // kernel starts as soon as its predecessor ends (no host-side gaps inside an event pair)
+    PT_HIP(pt::launch_spin(20000, st));
     rc = enqueue_run(t, s, bs, neg, bern, filter, steps, d_losses, st, &tm);
     if (rc) return rc;
     PT_HIP(hipStreamSynchronize(st));
@@ -413,8 +432,6 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
         float ms = 0;
         PT_HIP(hipEventElapsedTime(&ms, std::get<1>(e), std::get<2>(e)));
         tot[std::get<0>(e)] += ms;
-        (void)hipEventDestroy(std::get<1>(e));
-        (void)hipEventDestroy(std::get<2>(e));
     }
     for (int k = 0; k < 4; ++k) ms4[k] = (float)(tot[k] / (double)steps);
     return PT_OK;
@@ -634,7 +651,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         PT_CHECK(J.batch_size * (4 + J.neg) <= 16384, PT_EINVAL, "universe job: batch too large for the LDS work list");
         const int64_t rows = g.ent_total + g.rel_total * (model == 1 ? 2 : 1);
         slots[i].states = total; total += al(8 * J.threads);
-        slots[i].contrib = total; total += al(4 * J.batch_size * (2 + J.neg) * J.dim);
+        slots[i].contrib = total; total += al(4 * J.batch_size * (4 + J.neg) * J.dim);
         slots[i].grad = total;   total += al(4 * rows * J.dim);
         slots[i].flags = total;  total += al(4 * (g.ent_total + 2 * g.rel_total));
     }
@@ -668,7 +685,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         loss_of[i] = loss_off;
         loss_off += jobs[i].epochs;
     }
-    int64_t max_bs = 0, max_flags = 0, max_relg = 0, max_ent = 0, max_rel = 0, max_seq = 0, max_nb = 0;
+    int64_t max_bs = 0, max_relg = 0, max_ent = 0, max_rel = 0, max_seq = 0, max_nb = 0;
     for (int64_t i : order) {
         const pt_universe_job &J = jobs[i];
         pt::Graph &g = const_cast<pt::Graph &>(reinterpret_cast<const pt_graph *>(J.graph)->g);
@@ -697,7 +714,6 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         set->host.push_back(U);
         set->host_loss_off.push_back(loss_of[i]);
         max_bs = std::max(max_bs, J.batch_size);
-        max_flags = std::max(max_flags, g.ent_total + 2 * g.rel_total);
         max_relg = std::max(max_relg, g.rel_total * J.dim);
         max_ent = std::max(max_ent, g.ent_total);
         max_rel = std::max(max_rel, g.rel_total);
@@ -713,19 +729,24 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     auto a4 = [](int64_t v) { return 4 * ((v + 3) & ~int64_t(3)); };
     const int64_t list_b = a4(C.list_cap);
     const int64_t relg_b = 4 * max_relg * (model == 1 ? 2 : 1);
-    const int64_t contrib_b = a4(max_ent) + a4(max_bs * (2 + set->neg));
     int64_t used = list_b;
     auto env_on = [](const char *name) {
         const char *v = getenv(name);
         return !v || atoi(v) != 0;
     };
     PT_CHECK(used <= lds_budget, PT_EINVAL, "universe batch too large for the LDS work list");
+    // entity rows as contribution lists (heads for entities and relations, next per slot)
+    const int64_t heads_b = a4(max_ent + 2 * max_rel) + a4(max_bs * (4 + set->neg));
+    C.contrib = used + heads_b <= lds_budget && env_on("PT_UNI_CONTRIB");
+    used += C.contrib ? heads_b : 0;
+    // relation rows: LDS gradient rows (hot rows, few) if they fit, else contribution lists
     C.lds_relgrad = used + relg_b <= lds_budget && env_on("PT_UNI_RELGRAD");
+    C.rel_list = C.contrib && !C.lds_relgrad;
     used += C.lds_relgrad ? relg_b : 0;
-    C.contrib = used + contrib_b + a4(2 * max_rel) <= lds_budget && env_on("PT_UNI_CONTRIB");
-    used += C.contrib ? contrib_b : 0;
-    const int64_t flags_b = C.contrib ? a4(2 * max_rel) : a4(max_flags);
-    C.lds_flags = used + flags_b <= lds_budget && env_on("PT_UNI_LDSFLAGS");
+    // touched flags of the rows that are not lists
+    const int64_t nfl = (C.contrib ? 0 : max_ent) + (C.rel_list ? 0 : 2 * max_rel);
+    const int64_t flags_b = a4(nfl);
+    C.lds_flags = nfl > 0 && used + flags_b <= lds_budget && env_on("PT_UNI_LDSFLAGS");
     used += C.lds_flags ? flags_b : 0;
     const int64_t per_batch = 12 * max_seq;
     C.pchunk = env_on("PT_UNI_PRESAMPLE") && per_batch > 0 ? std::min<int64_t>(max_nb, (lds_budget - used) / per_batch)
@@ -733,8 +754,8 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     if (C.pchunk < 0) C.pchunk = 0;
     used += C.pchunk * per_batch;
     C.lds_bytes = used;
-    // agent-scope fences only while some gradient row is a global float atomic
-    C.agent_fence = !(C.contrib && C.lds_relgrad && C.lds_flags);
+    // agent-scope fences only while some gradient row is a global float atomic (or a flag global)
+    C.agent_fence = !(C.contrib && (C.rel_list || (C.lds_relgrad && C.lds_flags)));
     if (const char *v = getenv("PT_UNI_FENCE")) C.agent_fence = C.agent_fence || atoi(v) != 0;
     C.threads = 512;
     // tuning overrides (benchmarks): PT_UNI_RELGRAD / CONTRIB / LDSFLAGS / PRESAMPLE = 0 disable the

@@ -16,6 +16,8 @@ struct StepParams {
     float *ent_acc, *rel_acc, *norm_acc;
     int64_t batch_size, neg;
     float inv_count;   // 1 / (batch_size * neg)
+    int dbg = 0;       // timing experiments only (PT_STEP_DBG): bit 0 skip corrupted-row stores, bit 1 skip
+                       // positive-row atomics, bit 2 skip negative row loads (results are then wrong)
 };
 
 struct StepWorkspace {
@@ -85,6 +87,7 @@ inline Shape pick_shape(int64_t D, bool vec4 = true) {
 bool shape_supported(int64_t dim);
 hipError_t launch_sample(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                          int bern, int filter, int64_t *h, int64_t *t, int64_t *r, float *y, hipStream_t st);
+hipError_t launch_spin(int64_t us, hipStream_t st);
 hipError_t launch_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t dpp, hipStream_t st);
 hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                              int bern, int filter, int64_t calls, const CsrWork &w, hipStream_t st);

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "device.h"
 #include "graph.h"
@@ -44,6 +45,13 @@ __global__ void k_sample(DeviceGraph g, const uint64_t *__restrict__ states, int
         orr[o] = rp;
         if (oy) oy[o] = -1.f;
     }
+}
+
+// busy-waits `us` microseconds (100 MHz constant wall clock): keeps a stream occupied while the host
+// enqueues a measured sequence behind it
+__global__ void k_spin(int64_t us) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < (uint64_t)us * 100) __builtin_amdgcn_s_sleep(8);
 }
 
 __global__ void k_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t dpp) {
@@ -214,14 +222,14 @@ __global__ __launch_bounds__(256) void k_step(StepParams P, const int64_t *__res
 //
 // CSR = true: the batch was drawn by k_sample_csr; the corrupted entities' gradient rows are written
 // with plain stores to their counting-sort slots (contrib) instead of float atomics.
-template <int MODEL, int G, int KCH, int NCH, int S, bool CSR>
+template <int MODEL, int G, int VEC, int KCH, int NCH, int S, bool CSR, bool DB>
 __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph g, const uint64_t *__restrict__ states,
                                                       int64_t threads, int bern, int filter, GlobalSink sink,
                                                       float *__restrict__ loss, CsrWork cw) {
-    using Vec = V<G, 1, KCH>;
+    using Vec = V<G, VEC, KCH>;
     constexpr int GPB = 256 / G;      // lane groups per block
     constexpr int PPB = GPB / S;      // positives per block
-    constexpr int RW = KCH * G;       // floats per row slot in the reduction area
+    constexpr int RW = KCH * G * VEC; // floats per row slot in the reduction area
     // LDS: s_neg[PPB*neg] (entity << 1 | tail_side) [, s_dst[PPB*neg]] , then red[GPB][4][RW] + cs[GPB][2]
     extern __shared__ __attribute__((aligned(16))) int64_t s_neg[];
     const int lane = threadIdx.x % G;
@@ -271,19 +279,20 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
     const bool nf = P.norm_flag != 0;
     const int64_t hp = pd.h, rp = pd.r, tp = pd.t;
     const int64_t *mine = s_neg + pl * neg;
-    Vec E[NCH];
+    // DB: double buffer (the next chunk's rows load while this chunk computes), for nper > NCH
+    Vec EA[NCH], EB[DB ? NCH : 1];
     Vec aH, aT, aR, aW;
     vzero(aH); vzero(aT); vzero(aR); vzero(aW);
     float csum = 0.f, lsum = 0.f;
     Vec Hs, Ts;
     float hn = 0, tn = 0, hdot = 0, tdot = 0, ps = 0;
     if (active) {
-        auto load_chunk = [&](int64_t c0) {
+        auto load_chunk = [&](Vec(&E)[NCH], int64_t c0) {
 #pragma unroll
             for (int k = 0; k < NCH; ++k)
-                if (c0 + k < k_hi) vload(E[k], P.ent + (mine[c0 + k] >> 1) * D, D, lane);
+                if (c0 + k < k_hi && !(P.dbg & 4)) vload(E[k], P.ent + (mine[c0 + k] >> 1) * D, D, lane);
         };
-        load_chunk(k_lo);
+        load_chunk(EA, k_lo);
         // ---- positive forward
         Hs = H; Ts = T;
         if constexpr (MODEL == 1) {
@@ -307,10 +316,10 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
         for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
         ps = vpnorm<true>(vpos, p);
         const float m = P.margin, inv = P.inv_count;
-        for (int64_t c0 = k_lo; c0 < k_hi;) {
+        auto process = [&](Vec(&E)[NCH], int64_t c0) {
 #pragma unroll
             for (int k = 0; k < NCH; ++k) {
-                if (c0 + k >= k_hi) break;
+                if (c0 + k >= k_hi) return;
                 const int32_t v = uni<G>((int32_t)mine[c0 + k]);
                 const int64_t e = v >> 1;
                 const bool tail_side = v & 1;
@@ -349,7 +358,11 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
                     gs.x[i] = tail_side ? -gk.x[i] : gk.x[i];   // corrupted tail gets -g, corrupted head +g
                 }
                 if constexpr (MODEL == 0) {
-                    if constexpr (CSR) vstore(gs, dst, D, lane); else sink.ent(e, gs, D, lane);
+                    if constexpr (CSR) {
+                        if (!(P.dbg & 1)) vstore(gs, dst, D, lane);
+                    } else {
+                        sink.ent(e, gs, D, lane);
+                    }
                 } else {
                     Vec gp, ge;
                     if (nf) vnormalize_bwd<true>(Es, en, gs, gp); else gp = gs;
@@ -362,17 +375,32 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
                     if constexpr (CSR) vstore(ge, dst, D, lane); else sink.ent(e, ge, D, lane);
                 }
             }
-            c0 += NCH;
-            if (c0 >= k_hi) break;
-            load_chunk(c0);
+        };
+        if constexpr (DB) {
+            for (int64_t c0 = k_lo; c0 < k_hi;) {
+                if (c0 + NCH < k_hi) load_chunk(EB, c0 + NCH);
+                process(EA, c0);
+                c0 += NCH;
+                if (c0 >= k_hi) break;
+                if (c0 + NCH < k_hi) load_chunk(EA, c0 + NCH);
+                process(EB, c0);
+                c0 += NCH;
+            }
+        } else {
+            for (int64_t c0 = k_lo; c0 < k_hi;) {
+                process(EA, c0);
+                c0 += NCH;
+                if (c0 >= k_hi) break;
+                load_chunk(EA, c0);
+            }
         }
     }
     if constexpr (S > 1) {
         // ---- meet the positive's partials in LDS
         float *mr = red + grp * 4 * RW;
 #pragma unroll
-        for (int k = 0; k < KCH; ++k) {
-            const int c = k * G + lane;
+        for (int k = 0; k < Vec::N; ++k) {
+            const int c = ((k / VEC) * G + lane) * VEC + k % VEC;
             mr[0 * RW + c] = aH.x[k];
             mr[1 * RW + c] = aT.x[k];
             mr[2 * RW + c] = aR.x[k];
@@ -390,8 +418,8 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
         for (int q = 0; q < S; ++q) {   // fixed order: deterministic
             const float *qr = red + (grp + q) * 4 * RW;
 #pragma unroll
-            for (int k = 0; k < KCH; ++k) {
-                const int c = k * G + lane;
+            for (int k = 0; k < Vec::N; ++k) {
+                const int c = ((k / VEC) * G + lane) * VEC + k % VEC;
                 aH.x[k] += qr[0 * RW + c];
                 aT.x[k] += qr[1 * RW + c];
                 aR.x[k] += qr[2 * RW + c];
@@ -412,11 +440,14 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
             aR.x[i] += gv.x[i];
             aT.x[i] -= gv.x[i];
         }
-        sink.rel(rp, aR, D, lane);
         if constexpr (MODEL == 0) {
-            sink.ent(hp, aH, D, lane);
-            sink.ent(tp, aT, D, lane);
+            if (!(P.dbg & 2)) {
+                sink.rel(rp, aR, D, lane);
+                sink.ent(hp, aH, D, lane);
+                sink.ent(tp, aT, D, lane);
+            }
         } else {
+            sink.rel(rp, aR, D, lane);
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
                 const Vec &acc = s2 == 0 ? aH : aT;
@@ -533,6 +564,117 @@ __global__ __launch_bounds__(256) void k_apply(ApplyParams A) {
         vzero(z);
         vstore(z, T.grad + row * D, D, lane);
         if (lane == 0) T.flag[row] = 0;
+    }
+}
+
+// Apply pass, RPW consecutive rows per lane group with all their loads in flight together (the
+// one-row-per-group form is a chain of two dependent memory round trips per row). Consecutive entity
+// rows own consecutive counting-sort contribution ranges, so a group streams ONE contiguous range
+// [start[r0], start[r0 + RPW]) and adds each contribution to its row.
+template <int G, int VEC, int KCH, int RPW>
+__global__ __launch_bounds__(256) void k_apply_rows(ApplyParams A) {
+    using Vec = V<G, VEC, KCH>;
+    constexpr int GPB = 256 / G;
+    const int lane = threadIdx.x % G;
+    const int64_t gi = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        if (A.states) advance_states(A.states, A.threads, A.bs, A.dpp, (int)threadIdx.x);
+        if (A.loss && threadIdx.x == 0) *A.loss += A.margin;
+    }
+    const int D = (int)A.dim;
+    int ti[RPW];
+    int64_t row[RPW];
+    int flag[RPW], c0[RPW], c1[RPW];
+    bool live[RPW];
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        int64_t r = gi * RPW + u;
+        int t = 0;
+        while (t < A.ntab && r >= A.t[t].rows) {
+            r -= A.t[t].rows;
+            ++t;
+        }
+        ti[u] = t;
+        row[u] = r;
+        flag[u] = 0;
+        c0[u] = c1[u] = 0;
+        if (t < A.ntab) {
+            flag[u] = A.t[t].flag[r];
+            if (A.t[t].start) {
+                c0[u] = A.t[t].start[r];
+                c1[u] = A.t[t].start[r + 1];
+            }
+        }
+        live[u] = t < A.ntab && (flag[u] || c0[u] != c1[u]);
+    }
+    Vec x[RPW], g[RPW], a[RPW];
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        if (!live[u]) continue;
+        const ApplyTable &T = A.t[ti[u]];
+        vload(x[u], T.w + row[u] * D, D, lane);
+        if (flag[u]) vload(g[u], T.grad + row[u] * D, D, lane); else vzero(g[u]);
+        if (A.opt != 0) vload(a[u], T.acc + row[u] * D, D, lane);
+    }
+    // the group's contribution range (entity table rows only carry contributions)
+    int cs = 0, ce = 0;
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        if (c0[u] == c1[u]) continue;
+        if (!any) cs = c0[u];
+        ce = c1[u];
+        any = true;
+    }
+    if (any) {
+        const float *contrib = A.t[0].contrib;
+        for (int j = cs; j < ce; j += 4) {
+            Vec c[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (j + q < ce) vload(c[q], contrib + (int64_t)(j + q) * D, D, lane);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (j + q >= ce) break;
+#pragma unroll
+                for (int u = 0; u < RPW; ++u) {
+                    if (j + q >= c0[u] && j + q < c1[u]) {
+#pragma unroll
+                        for (int i = 0; i < Vec::N; ++i) g[u].x[i] += c[q].x[i];
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        if (!live[u]) continue;
+        const ApplyTable &T = A.t[ti[u]];
+        Vec gg;
+        if (T.jacobian) {
+            const float n = sqrtf(vdot(x[u], x[u]));
+            vnormalize_bwd(x[u], n, g[u], gg);
+        } else {
+            gg = g[u];
+        }
+        if (A.opt == 0) {
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) x[u].x[i] = x[u].x[i] + (-A.lr) * gg.x[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) {
+                a[u].x[i] = a[u].x[i] + gg.x[i] * gg.x[i];
+                x[u].x[i] = x[u].x[i] + (-A.lr) * gg.x[i] / (sqrtf(a[u].x[i]) + 1e-10f);
+            }
+            vstore(a[u], T.acc + row[u] * D, D, lane);
+        }
+        vstore(x[u], T.w + row[u] * D, D, lane);
+        if (flag[u]) {
+            Vec z;
+            vzero(z);
+            vstore(z, T.grad + row[u] * D, D, lane);
+            if (lane == 0) T.flag[row[u]] = 0;
+        }
     }
 }
 
@@ -729,15 +871,23 @@ int pick_nch(int64_t neg, int kch) {
 // VEC=1 shapes x NCH x S of the sampled step kernel: S = 1 for neg < 8 (NCH covers neg), S = 4 with
 // NCH covering ceil(neg/4) (chunks beyond 32 negatives per sub-group loop)
 #define PT_SSHAPES(X)                                                                                  \
-    X(2, 1, 1, 1) X(2, 1, 4, 1) X(2, 1, 8, 1) X(2, 1, 8, 4) X(2, 1, 32, 4)                             \
-    X(4, 1, 1, 1) X(4, 1, 4, 1) X(4, 1, 8, 1) X(4, 1, 8, 4) X(4, 1, 32, 4)                             \
-    X(8, 1, 1, 1) X(8, 1, 4, 1) X(8, 1, 8, 1) X(8, 1, 8, 4) X(8, 1, 32, 4)                             \
-    X(16, 1, 1, 1) X(16, 1, 4, 1) X(16, 1, 8, 1) X(16, 1, 8, 4) X(16, 1, 32, 4)                        \
-    X(32, 1, 1, 1) X(32, 1, 4, 1) X(32, 1, 8, 1) X(32, 1, 8, 4) X(32, 1, 32, 4)                        \
-    X(64, 1, 1, 1) X(64, 1, 4, 1) X(64, 1, 8, 1) X(64, 1, 8, 4) X(64, 1, 32, 4)                        \
-    X(64, 2, 1, 1) X(64, 2, 4, 1) X(64, 2, 8, 1) X(64, 2, 8, 4) X(64, 2, 32, 4)                        \
-    X(64, 4, 1, 1) X(64, 4, 4, 1) X(64, 4, 8, 1) X(64, 4, 8, 4) X(64, 4, 32, 4)                        \
-    X(64, 8, 1, 1) X(64, 8, 4, 1) X(64, 8, 8, 1) X(64, 8, 8, 4)
+    X(2, 1, 1, 1, 1, false) X(2, 1, 1, 4, 1, false) X(2, 1, 1, 8, 1, false) X(2, 1, 1, 8, 4, false) X(2, 1, 1, 32, 4, false)                  \
+    X(4, 1, 1, 1, 1, false) X(4, 1, 1, 4, 1, false) X(4, 1, 1, 8, 1, false) X(4, 1, 1, 8, 4, false) X(4, 1, 1, 32, 4, false)                  \
+    X(8, 1, 1, 1, 1, false) X(8, 1, 1, 4, 1, false) X(8, 1, 1, 8, 1, false) X(8, 1, 1, 8, 4, false) X(8, 1, 1, 32, 4, false)                  \
+    X(16, 1, 1, 1, 1, false) X(16, 1, 1, 4, 1, false) X(16, 1, 1, 8, 1, false) X(16, 1, 1, 8, 4, false) X(16, 1, 1, 32, 4, false)             \
+    X(32, 1, 1, 1, 1, false) X(32, 1, 1, 4, 1, false) X(32, 1, 1, 8, 1, false) X(32, 1, 1, 8, 4, false) X(32, 1, 1, 32, 4, false)             \
+    X(64, 1, 1, 1, 1, false) X(64, 1, 1, 4, 1, false) X(64, 1, 1, 8, 1, false) X(64, 1, 1, 8, 4, false) X(64, 1, 1, 32, 4, false)             \
+    X(64, 1, 2, 1, 1, false) X(64, 1, 2, 4, 1, false) X(64, 1, 2, 8, 1, false) X(64, 1, 2, 8, 4, false) X(64, 1, 2, 32, 4, false)             \
+    X(64, 1, 4, 1, 1, false) X(64, 1, 4, 4, 1, false) X(64, 1, 4, 8, 1, false) X(64, 1, 4, 8, 4, false) X(64, 1, 4, 32, 4, false)             \
+    X(64, 1, 4, 8, 2, false) X(64, 1, 4, 4, 4, false) X(64, 1, 4, 4, 2, false)                             \
+    X(64, 1, 4, 8, 1, true) X(64, 1, 4, 8, 2, true) X(64, 1, 4, 4, 1, true) X(64, 1, 4, 4, 2, true)         \
+    X(64, 1, 4, 4, 4, true)                                                                                \
+    X(64, 1, 8, 1, 1, false) X(64, 1, 8, 4, 1, false) X(64, 1, 8, 8, 1, false) X(64, 1, 8, 8, 4, false)                                \
+    X(8, 4, 1, 1, 1, false) X(8, 4, 1, 4, 1, false) X(8, 4, 1, 8, 1, false) X(8, 4, 1, 8, 4, false)                                    \
+    X(16, 4, 1, 1, 1, false) X(16, 4, 1, 4, 1, false) X(16, 4, 1, 8, 1, false) X(16, 4, 1, 8, 4, false)                                \
+    X(32, 4, 1, 1, 1, false) X(32, 4, 1, 4, 1, false) X(32, 4, 1, 8, 1, false) X(32, 4, 1, 8, 4, false)                                \
+    X(64, 4, 1, 1, 1, false) X(64, 4, 1, 4, 1, false) X(64, 4, 1, 8, 1, false) X(64, 4, 1, 8, 4, false) X(64, 4, 1, 32, 4, false)             \
+    X(64, 4, 2, 1, 1, false) X(64, 4, 2, 4, 1, false) X(64, 4, 2, 8, 1, false) X(64, 4, 2, 8, 4, false)
 
 }  // namespace
 
@@ -758,6 +908,11 @@ hipError_t launch_sample(const DeviceGraph &g, const uint64_t *states, int64_t t
     const int bl = 256;
     hipLaunchKernelGGL(dev::k_sample, dim3((unsigned)((bs + bl - 1) / bl)), dim3(bl), 0, st, g, states, threads, bs,
                        neg, bern, filter, h, t, r, y);
+    return hipGetLastError();
+}
+
+hipError_t launch_spin(int64_t us, hipStream_t st) {
+    hipLaunchKernelGGL(dev::k_spin, dim3(1), dim3(64), 0, st, us);
     return hipGetLastError();
 }
 
@@ -802,38 +957,58 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
 #undef PT_STEP
         return hipErrorInvalidValue;
     }
-    const Shape s = pick_shape(P.dim, false);
-    // split a positive's negatives over 4 lane groups when there are enough of them
-    const int S = (P.neg >= 8 && 256 / s.G >= 4) ? 4 : 1;
-    const int64_t nper = (P.neg + S - 1) / S;
-    const int nch = pick_nch(nper, s.KCH);
-    const int64_t gpb = 256 / s.G, ppb = gpb / S;
-    const dim3 grid((unsigned)((P.batch_size + ppb - 1) / ppb)), block(256);
-    size_t lds = (size_t)ppb * (size_t)P.neg * sizeof(int64_t) * (csr ? 2 : 1);
-    if (S > 1) lds += sizeof(float) * ((size_t)gpb * 4 * s.KCH * s.G + (size_t)gpb * 2);
-    if (lds > 64 * 1024) return hipErrorInvalidValue;
-    const CsrWork cw = csr ? *csr : CsrWork{};
-#define PT_SSTEP(G_, K_, N_, S_)                                                                                  \
-    if (s.G == G_ && s.KCH == K_ && nch == N_ && S == S_) {                                                     \
-        if (csr) {                                                                                                \
-            if (P.model == 0)                                                                                     \
-                hipLaunchKernelGGL((dev::k_step_sampled<0, G_, K_, N_, S_, true>), grid, block, lds, st, P, g,     \
-                                   states, threads, bern, filter, sink, loss, cw);                                \
-            else                                                                                                  \
-                hipLaunchKernelGGL((dev::k_step_sampled<1, G_, K_, N_, S_, true>), grid, block, lds, st, P, g,     \
-                                   states, threads, bern, filter, sink, loss, cw);                                \
-        } else {                                                                                                  \
-            if (P.model == 0)                                                                                     \
-                hipLaunchKernelGGL((dev::k_step_sampled<0, G_, K_, N_, S_, false>), grid, block, lds, st, P, g,    \
-                                   states, threads, bern, filter, sink, loss, cw);                                \
-            else                                                                                                  \
-                hipLaunchKernelGGL((dev::k_step_sampled<1, G_, K_, N_, S_, false>), grid, block, lds, st, P, g,    \
-                                   states, threads, bern, filter, sink, loss, cw);                                \
-        }                                                                                                         \
-        return hipGetLastError();                                                                                 \
-    }
-    PT_SSHAPES(PT_SSTEP)
+    // row layout: one float per lane (each wave instruction moves 64 contiguous floats), or float4
+    // lanes when PT_STEP_VEC=4 and D % 4 == 0 (measured slower on the C2 step: 48.9 vs 40.6 us)
+    const char *vec_env = getenv("PT_STEP_VEC");
+    const bool try_vec4 = vec_env && atoi(vec_env) == 4;
+    for (int attempt = try_vec4 ? 0 : 1; attempt < 2; ++attempt) {
+        const Shape s = pick_shape(P.dim, attempt == 0);
+        if (attempt == 0 && s.VEC != 4) continue;
+        // split a positive's negatives over 4 lane groups when there are enough of them
+        // (PT_STEP_S = 1 | 2 | 4 and PT_STEP_NCH override, for tuning)
+        int S = (P.neg >= 8 && 256 / s.G >= 4) ? 4 : 1;
+        if (const char *v = getenv("PT_STEP_S")) {
+            const int want = atoi(v);
+            if ((want == 1 || want == 2 || want == 4) && 256 / s.G >= want) S = want;
+        }
+        const int64_t nper = (P.neg + S - 1) / S;
+        int nch = pick_nch(nper, s.KCH * s.VEC);
+        if (const char *v = getenv("PT_STEP_NCH")) nch = atoi(v);
+        // double-buffer the negative rows when a lane group takes more than one chunk (PT_STEP_DB=0 off)
+        bool db = nper > nch;
+        if (const char *v = getenv("PT_STEP_DB")) db = db && atoi(v) != 0;
+        const int64_t gpb = 256 / s.G, ppb = gpb / S;
+        const dim3 grid((unsigned)((P.batch_size + ppb - 1) / ppb)), block(256);
+        size_t lds = (size_t)ppb * (size_t)P.neg * sizeof(int64_t) * (csr ? 2 : 1);
+        if (S > 1) lds += sizeof(float) * ((size_t)gpb * 4 * s.KCH * s.G * s.VEC + (size_t)gpb * 2);
+        if (lds > 64 * 1024) continue;
+        const CsrWork cw = csr ? *csr : CsrWork{};
+#define PT_SSTEP(G_, V_, K_, N_, S_, DB_)                                                                            \
+        if (s.G == G_ && s.VEC == V_ && s.KCH == K_ && nch == N_ && S == S_ && db == DB_) {                              \
+            if (csr) {                                                                                            \
+                if (P.model == 0)                                                                                 \
+                    hipLaunchKernelGGL((dev::k_step_sampled<0, G_, V_, K_, N_, S_, true, DB_>), grid, block, lds, st,   \
+                                       P, g, states, threads, bern, filter, sink, loss, cw);                      \
+                else                                                                                              \
+                    hipLaunchKernelGGL((dev::k_step_sampled<1, G_, V_, K_, N_, S_, true, DB_>), grid, block, lds, st,   \
+                                       P, g, states, threads, bern, filter, sink, loss, cw);                      \
+            } else {                                                                                              \
+                if (P.model == 0)                                                                                 \
+                    hipLaunchKernelGGL((dev::k_step_sampled<0, G_, V_, K_, N_, S_, false, DB_>), grid, block, lds, st,  \
+                                       P, g, states, threads, bern, filter, sink, loss, cw);                      \
+                else                                                                                              \
+                    hipLaunchKernelGGL((dev::k_step_sampled<1, G_, V_, K_, N_, S_, false, DB_>), grid, block, lds, st,  \
+                                       P, g, states, threads, bern, filter, sink, loss, cw);                      \
+            }                                                                                                     \
+            return hipGetLastError();                                                                             \
+        }
+        for (int pass = 0; pass < 2; ++pass) {   // no double-buffered instance: single buffer
+            PT_SSHAPES(PT_SSTEP)
+            if (!db) break;
+            db = false;
+        }
 #undef PT_SSTEP
+    }
     return hipErrorInvalidValue;
 }
 
@@ -860,6 +1035,24 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
     int64_t rows = 0;
     for (int i = 0; i < A.ntab; ++i) rows += A.t[i].rows;
     const int64_t gpb = 256 / s.G;
+    // PT_APPLY_RPW=2|4: several rows per lane group with one contribution stream (measured slower on
+    // C2: 20.4 / 22.0 us vs 16.8 us for one row per group, which stays the default)
+    const char *rpw_env = getenv("PT_APPLY_RPW");
+    const int rpw = rpw_env ? atoi(rpw_env) : 1;
+    if (rpw == 4 || rpw == 2) {
+        const int64_t groups = (rows + rpw - 1) / rpw;
+        const dim3 grid((unsigned)((groups + gpb - 1) / gpb)), block(256);
+#define PT_APPLY4(G_, V_, K_)                                                                 \
+        if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                      \
+            if (rpw == 4)                                                                   \
+                hipLaunchKernelGGL((dev::k_apply_rows<G_, V_, K_, 4>), grid, block, 0, st, A); \
+            else                                                                            \
+                hipLaunchKernelGGL((dev::k_apply_rows<G_, V_, K_, 2>), grid, block, 0, st, A); \
+            return hipGetLastError();                                                       \
+        }
+        PT_SHAPES(PT_APPLY4)
+#undef PT_APPLY4
+    }
     const dim3 grid((unsigned)((rows + gpb - 1) / gpb)), block(256);
 #define PT_APPLY(G_, V_, K_)                                                                  \
     if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                          \

@@ -17,7 +17,7 @@ struct UniverseDev {
     float *ent_acc, *rel_acc, *norm_acc;            // Adagrad accumulators (same shapes)
     float *gent, *grel, *gnorm;                     // gradient rows, zero between steps
     int32_t *fent, *frel, *fnorm;                   // touched-row flags, zero between steps
-    float *contrib;                                 // [bs*(2+neg)][dim] entity-row gradient contributions
+    float *contrib;                                 // [bs*(4+neg)][dim] gradient-row contributions
     float *losses;                                  // [epochs] Trainer.run's per-epoch loss sum (or null)
     uint64_t *prof;                                 // null, or [4] cycle counters (presample, A, B, steps)
     int64_t threads, bs, nbatches, epochs, dim;
@@ -33,6 +33,7 @@ struct UniverseLaunch {
     int contrib = 0;            // entity gradients as LDS-linked contribution slots (needs head[E] + next[ccap])
     int64_t pchunk = 0;         // batches drawn into LDS at a time (0: sample inside each step)
     int lds_relgrad = 0;        // relation / norm_vector gradient rows in LDS (R x D floats, x2 for TransH)
+    int rel_list = 0;           // relation / norm_vector rows as contribution lists (when their rows do not fit)
     int agent_fence = 1;        // agent-scope fences around the phase barriers (global atomics in use)
     int64_t lds_bytes = 0;      // dynamic LDS per workgroup
 };

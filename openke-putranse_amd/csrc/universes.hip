@@ -60,25 +60,33 @@ struct UniverseSink {
     int32_t *fent, *frel, *fnorm;
     int32_t *list;
     int *count;
-    float *contrib;     // [ccap][D] (global) or null
-    int32_t *head;      // [E] LDS
-    int32_t *next;      // [ccap] LDS
-    int *ccount;        // LDS counter of contribution slots
+    float *contrib;      // [ccap][D] (global) or null: entity rows as contribution lists
+    int32_t *head;       // [E + 2R] LDS list heads (entity rows, then relation rows, then norm_vector rows)
+    int32_t *next;       // [ccap] LDS
+    int *ccount;         // LDS counter of contribution slots
+    int64_t E, R;
+    bool rel_list;       // relation / norm_vector rows as contribution lists too
     __device__ __forceinline__ void touch(int32_t *flag, int64_t row, int table) const {
         if (atomicExch(flag + row, 1) == 0) list[atomicAdd(count, 1)] = (int32_t)(row << 2) | table;
+    }
+    // plain store of the row gradient into a fresh contribution slot, linked into the row's list
+    template <int G, int VEC, int KCH>
+    __device__ __forceinline__ void link(int32_t *h, int64_t row, int table, const V<G, VEC, KCH> &g, int D,
+                                         int lane) const {
+        int c = 0;
+        if (lane == 0) c = atomicAdd(ccount, 1);
+        c = __shfl(c, 0, G);
+        vstore(g, contrib + (int64_t)c * D, D, lane);
+        if (lane == 0) {
+            const int32_t prev = atomicExch(h + row, c);
+            next[c] = prev;
+            if (prev < 0) list[atomicAdd(count, 1)] = (int32_t)(row << 2) | table;
+        }
     }
     template <int G, int VEC, int KCH>
     __device__ __forceinline__ void ent(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
         if (contrib) {
-            int c = 0;
-            if (lane == 0) c = atomicAdd(ccount, 1);
-            c = __shfl(c, 0, G);
-            vstore(g, contrib + (int64_t)c * D, D, lane);
-            if (lane == 0) {
-                const int32_t prev = atomicExch(head + row, c);
-                next[c] = prev;
-                if (prev < 0) list[atomicAdd(count, 1)] = (int32_t)(row << 2);
-            }
+            link(head, row, 0, g, D, lane);
         } else {
             vatomic(g, gent + row * D, D, lane);
             if (lane == 0) touch(fent, row, 0);
@@ -86,13 +94,21 @@ struct UniverseSink {
     }
     template <int G, int VEC, int KCH>
     __device__ __forceinline__ void rel(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
-        vatomic(g, grel + row * D, D, lane);
-        if (lane == 0) touch(frel, row, 1);
+        if (rel_list) {
+            link(head + E, row, 1, g, D, lane);
+        } else {
+            vatomic(g, grel + row * D, D, lane);
+            if (lane == 0) touch(frel, row, 1);
+        }
     }
     template <int G, int VEC, int KCH>
     __device__ __forceinline__ void norm(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
-        vatomic(g, gnorm + row * D, D, lane);
-        if (lane == 0) touch(fnorm, row, 2);
+        if (rel_list) {
+            link(head + E + R, row, 2, g, D, lane);
+        } else {
+            vatomic(g, gnorm + row * D, D, lane);
+            if (lane == 0) touch(fnorm, row, 2);
+        }
     }
 };
 
@@ -192,27 +208,29 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     const int64_t bs = U.bs, threads = U.threads, D = U.dim;
     const int64_t E = U.g.ent_total, R = U.g.rel_total;
     const bool contrib = cfg.contrib && U.contrib;
-    const int64_t seq = bs * (1 + neg), ccap = bs * (2 + neg);
+    const int64_t seq = bs * (1 + neg);
     const int64_t pchunk = cfg.pchunk < U.nbatches ? cfg.pchunk : U.nbatches;
     // carve the LDS
+    const bool rel_list = contrib && cfg.rel_list;
+    const int64_t ccap = bs * ((rel_list ? 4 : 2) + neg);
     int32_t *p = s_dyn;
     int32_t *s_list = p;
     p += cfg.list_cap;
-    int32_t *s_flags = p;   // [E (atomic mode only)][R][R]
-    const int64_t nflags = cfg.lds_flags ? (contrib ? 2 * R : E + 2 * R) : 0;
+    int32_t *s_flags = p;   // [E (entity atomics only)][R][R] (relation rows not in lists)
+    const int64_t nflags = cfg.lds_flags ? ((contrib ? 0 : E) + (rel_list ? 0 : 2 * R)) : 0;
     p += (nflags + 3) & ~int64_t(3);
     int32_t *s_head = p;
-    int32_t *s_next = p + ((E + 3) & ~int64_t(3));
-    if (contrib) p += ((E + 3) & ~int64_t(3)) + ((ccap + 3) & ~int64_t(3));
+    const int64_t nheads = contrib ? E + 2 * R : 0;
+    int32_t *s_next = p + ((nheads + 3) & ~int64_t(3));
+    if (contrib) p += ((nheads + 3) & ~int64_t(3)) + ((ccap + 3) & ~int64_t(3));
     int32_t *s_bh = p, *s_br = p + pchunk * seq, *s_bt = p + 2 * pchunk * seq;
     p += 3 * pchunk * seq;
     float *s_grel = reinterpret_cast<float *>(p);
-    const int64_t nrelg = cfg.lds_relgrad ? R * D * (MODEL == 1 ? 2 : 1) : 0;
+    const int64_t nrelg = cfg.lds_relgrad && !rel_list ? R * D * (MODEL == 1 ? 2 : 1) : 0;
 
     if (tid < threads) s_states[tid] = U.states[tid];
     for (int64_t i = tid; i < nflags; i += NT) s_flags[i] = 0;
-    if (contrib)
-        for (int64_t i = tid; i < E; i += NT) s_head[i] = -1;
+    for (int64_t i = tid; i < nheads; i += NT) s_head[i] = -1;
     for (int64_t i = tid; i < nrelg; i += NT) s_grel[i] = 0.f;
     StepParams P{};
     P.model = MODEL; P.p_norm = p_norm; P.norm_flag = norm_flag; P.opt = opt;
@@ -223,17 +241,19 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     P.batch_size = bs; P.neg = neg;
     P.inv_count = 1.0f / (float)(bs * neg);
     UniverseSink sink{U.gent, U.grel, U.gnorm, U.fent, U.frel, U.fnorm, s_list, &s_count,
-                      contrib ? U.contrib : nullptr, s_head, s_next, &s_ccount};
+                      contrib ? U.contrib : nullptr, s_head, s_next, &s_ccount, E, R, rel_list};
     if (cfg.lds_flags) {
         int32_t *f = s_flags;
         if (!contrib) {
             sink.fent = f;
             f += E;
         }
-        sink.frel = f;
-        sink.fnorm = f + R;
+        if (!rel_list) {
+            sink.frel = f;
+            sink.fnorm = f + R;
+        }
     }
-    if (cfg.lds_relgrad) {
+    if (nrelg) {
         sink.grel = s_grel;
         sink.gnorm = s_grel + R * D;
     }
@@ -360,9 +380,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     ap[u] = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
                     vload(x[u], wp[u], (int)D, lane);
                     if (opt != 0) vload(a[u], ap[u], (int)D, lane);
-                    if (table == 0 && contrib) {
+                    if ((table == 0 && contrib) || (table > 0 && rel_list)) {
                         // the row's contributions (linked in LDS), summed in list order
-                        int32_t c = s_head[row];
+                        int32_t c = s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row];
                         vload(gs[u], U.contrib + (int64_t)c * D, (int)D, lane);
                         for (c = s_next[c]; c >= 0; c = s_next[c]) {
                             Vec y;
@@ -401,8 +421,8 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                         vstore(a[u], ap[u], (int)D, lane);
                     }
                     vstore(x[u], wp[u], (int)D, lane);
-                    if (table == 0 && contrib) {
-                        if (lane == 0) s_head[row] = -1;
+                    if ((table == 0 && contrib) || (table > 0 && rel_list)) {
+                        if (lane == 0) s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row] = -1;
                     } else {
                         Vec z;
                         vzero(z);

@@ -274,10 +274,13 @@ def test_gpu_ranking_matches_host_ranking(dup):
                                           part.ctypes.data))
         raw = torch.zeros(n, dtype=torch.int64, device=dev)
         filt = torch.zeros(n, dtype=torch.int64, device=dev)
-        _native.check(L.pt_rank_rows(_native.ptr(rows), E, _native.ptr(torch.arange(n, device=dev)),
-                                     _native.ptr(truth), None, _native.ptr(torch.from_numpy(off).to(dev)),
-                                     _native.ptr(torch.from_numpy(part).to(dev)), n, _native.ptr(raw),
-                                     _native.ptr(filt), _native.stream()))
+        # device arguments held by names until the kernel has run (a temporary would be freed and its
+        # memory reused by the next argument's allocation before the launch)
+        row_of = torch.arange(n, device=dev)
+        d_off, d_part = torch.from_numpy(off).to(dev), torch.from_numpy(part).to(dev)
+        _native.check(L.pt_rank_rows(_native.ptr(rows), E, _native.ptr(row_of), _native.ptr(truth), None,
+                                     _native.ptr(d_off), _native.ptr(d_part), n, _native.ptr(raw), _native.ptr(filt),
+                                     _native.stream()))
         np.testing.assert_array_equal(raw.cpu().numpy(), raw_h)
         np.testing.assert_array_equal(filt.cpu().numpy(), filt_h)
         # the two kernels score every (query, entity) identically
