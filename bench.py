@@ -87,33 +87,54 @@ def cpu_baseline(path, wl, seconds=15.0):
                       "oracle/oracle.c single thread, %.1f s" % (steps, bs, neg, dim, el)}
 
 
-def universe_draws(k, seed0=4):
+# PuTransE workloads (BASELINE.json configs[2..4]); ranges from the reference's experiments
+# (static_experiment_PuTransE_on_WN18.py:67-88, static_experiment_PuTransH_on_WN18.py:70-79,
+# incremental_experiment_PuTransE_on_WikidataEvolve.py:173-182)
+PU_WORKLOADS = {
+    # name: shape, universes, model, dim (int or (lo, hi) per-universe draw), p, tc range, margin range, lp
+    "c3": ("wn18", 512, "TransE", (20, 100), 1, (500, 2000), (1, 4), False),
+    "c4": ("wikidata", 1024, "TransE", 200, 1, (500, 1500), (1, 5), True),
+    "c5": ("fb15k", 256, "TransH", 20, 1, (500, 2000), (1, 4), False),
+}
+
+
+def universe_draws(k, tc_range=(500, 2000), margin_range=(1, 4), seed0=4):
     """Python-RNG hyperparameters of universe k exactly as Parallel_Universe_Config draws them
-    (:157-161, :210-236) with the PuTransE WN18 experiment's ranges
-    (experiments/static_experiment_PuTransE_on_WN18.py:67-88)."""
+    (:157-161, :210-236): randrange(tc), uniform(balance), randrange(margin), randrange(epochs),
+    uniform(lr) rounded to 3 digits."""
     import random
     rs = random.Random(seed0 + k)
-    tc = rs.randrange(500, 2000)
+    tc = rs.randrange(*tc_range)
     bal = round(rs.uniform(0.25, 0.5), 2)
-    margin = rs.randrange(1, 4)
+    margin = rs.randrange(*margin_range)
     epochs = rs.randrange(50, 200)
     lr = round(rs.uniform(0.001, 0.1), 3)
     return tc, bal, margin, epochs, lr
 
 
-def run_universes(args, ws, rank, dev, n_univ=512):
-    """C3: PuTransE on WN18-shaped data, 512 universes with D ~ U{20..100}, Adagrad, neg 1, bern 0,
-    filter 0, nbatches 20, 8 sampler threads; universe k on rank k % N (strong scaling, no collective).
-    One step = every universe's full training run (all its epochs) in one persistent launch per shape."""
+def _xavier(rng, rows, dim):
+    b = np.sqrt(6.0 / (rows + dim))
+    return rng.uniform(-b, b, (rows, dim)).astype(np.float32)
+
+
+def run_universes(args, ws, rank, dev, name="c3"):
+    """PuTransE / PuTransH universes: universe k on rank k % N (no collective in training), Adagrad,
+    neg 1, bern 0, filter 0, nbatches 20, 8 sampler threads. One step = every universe's full training
+    run (all its epochs) in one persistent launch. C4 adds link prediction over the test split: each
+    rank MINs its universes' scores into the key rows, one RCCL all_reduce(MIN), GPU ranking."""
     import synth_kg
     from openke import _native
     L = _native.lib()
-    path = synth_kg.ensure_dataset(os.path.join(args.data_dir, "rank%d" % rank), "wn18")
+    shape, n_univ, model, dim_spec, p_norm, tc_range, margin_range, do_lp = PU_WORKLOADS[name]
+    path = synth_kg.ensure_dataset(os.path.join(args.data_dir, "rank%d" % rank), shape)
     g = ctypes.c_void_p()
     _native.check(L.pt_graph_load(path.encode(), ctypes.byref(g)))
     own = [k for k in range(n_univ) if k % ws == rank]
-    draws = [universe_draws(k) for k in own]
-    dims = [int(np.random.default_rng(1000 + k).integers(20, 101)) for k in own]
+    draws = [universe_draws(k, tc_range, margin_range) for k in own]
+    if isinstance(dim_spec, tuple):
+        dims = [int(np.random.default_rng(1000 + k).integers(dim_spec[0], dim_spec[1] + 1)) for k in own]
+    else:
+        dims = [dim_spec] * len(own)
     seeds = np.array([4 + k for k in own], dtype=np.int64)
     tcs = np.array([d[0] for d in draws], dtype=np.int64)
     bals = np.array([d[1] for d in draws], dtype=np.float32)
@@ -122,18 +143,18 @@ def run_universes(args, ws, rank, dev, n_univ=512):
     _native.check(L.pt_universe_build_many(g, len(own), seeds.ctypes.data, 8, tcs.ctypes.data, bals.ctypes.data, 0,
                                            handles))
     build_s = time.perf_counter() - t0
-    jobs, keep = [], []
+    mid = 0 if model == "TransE" else 1
+    jobs, keep, unis = [], [], []
     slots_step, bytes_step = 0, 0
     for i, k in enumerate(own):
         h = handles[i]
         E, R, N = L.pt_universe_ent_total(h), L.pt_universe_rel_total(h), L.pt_universe_train_total(h)
         D = dims[i]
         rng = np.random.default_rng(k)
-        b = np.sqrt(6.0 / (E + D))
-        ent = torch.from_numpy(rng.uniform(-b, b, (E, D)).astype(np.float32)).to(dev)
-        b = np.sqrt(6.0 / (R + D))
-        rel = torch.from_numpy(rng.uniform(-b, b, (R, D)).astype(np.float32)).to(dev)
-        accs = (torch.zeros_like(ent), torch.zeros_like(rel))
+        ent = torch.from_numpy(_xavier(rng, E, D)).to(dev)
+        rel = torch.from_numpy(_xavier(rng, R, D)).to(dev)
+        nv = torch.from_numpy(_xavier(rng, R, D)).to(dev) if mid == 1 else None
+        accs = [torch.zeros_like(x) if x is not None else None for x in (ent, rel, nv)]
         st = np.zeros(8, dtype=np.uint64)
         _native.check(L.pt_universe_seeds(h, st.ctypes.data))
         tc, bal, margin, epochs, lr = draws[i]
@@ -143,17 +164,23 @@ def run_universes(args, ws, rank, dev, n_univ=512):
         j.seeds = st.ctypes.data
         j.threads, j.batch_size, j.epochs, j.nbatches, j.neg = 8, bs, epochs, 20, 1
         j.lr, j.margin = lr, margin
-        j.ent, j.rel, j.normv = ent.data_ptr(), rel.data_ptr(), None
-        j.ent_acc, j.rel_acc, j.norm_acc = accs[0].data_ptr(), accs[1].data_ptr(), None
+        j.ent, j.rel, j.normv = ent.data_ptr(), rel.data_ptr(), nv.data_ptr() if nv is not None else None
+        j.ent_acc, j.rel_acc = accs[0].data_ptr(), accs[1].data_ptr()
+        j.norm_acc = accs[2].data_ptr() if accs[2] is not None else None
         j.dim = D
         jobs.append(j)
-        keep.append((st, ent, rel, accs))
+        keep.append((st, accs))
+        em = np.zeros(max(E, 1), dtype=np.int64)
+        rm = np.zeros(max(R, 1), dtype=np.int64)
+        _native.check(L.pt_universe_remaps(h, em.ctypes.data, rm.ctypes.data))
+        unis.append({"ent": ent, "rel": rel, "nv": nv, "em": em[:E], "rm": rm[:R], "dim": D})
         slots = epochs * 20 * bs * 2
         slots_step += slots
-        bytes_step += slots * algorithmic_bytes_per_slot("TransE", "adagrad", D)
+        bytes_step += slots * algorithmic_bytes_per_slot(model, "adagrad", D)
     arr = (_native.UniverseJob * max(len(jobs), 1))(*jobs)
     uset = ctypes.c_void_p()
-    _native.check(L.pt_universe_set_create(arr, len(jobs), 0, 1, 1, _native.PT_ADAGRAD, 0, 0, ctypes.byref(uset)))
+    _native.check(L.pt_universe_set_create(arr, len(jobs), mid, p_norm, 1, _native.PT_ADAGRAD, 0, 0,
+                                           ctypes.byref(uset)))
     total_epochs = sum(int(j.epochs) for j in jobs)
     losses = torch.zeros(max(total_epochs, 1), device=dev)
     stream = _native.stream()
@@ -186,20 +213,105 @@ def run_universes(args, ws, rank, dev, n_univ=512):
             steps = max(prof[i, 3], 1)
             print("universe-prof steps %d  cycles/step: presample %.0f  A %.0f  B %.0f" %
                   (steps, prof[i, 0] / steps, prof[i, 1] / steps, prof[i, 2] / steps), file=sys.stderr)
-        tot = prof[:, :3].sum(axis=0) / max(prof[:, 3].sum(), 1)
-        print("universe-prof all: cycles/step presample %.0f A %.0f B %.0f" % tuple(tot), file=sys.stderr)
+        tot_p = prof[:, :3].sum(axis=0) / max(prof[:, 3].sum(), 1)
+        print("universe-prof all: cycles/step presample %.0f A %.0f B %.0f" % tuple(tot_p), file=sys.stderr)
     _native.check(L.pt_universe_set_free(uset))
     for i in range(len(own)):
         L.pt_universe_free(handles[i])
-    L.pt_graph_free(g)
     achieved = bytes_all * args.c3_steps / el / 1e9 / max(ws, 1)
-    return {"workload": "C3 PuTransE wn18-shaped, %d universes, D~U{20..100}, tc~U[500,2000), epochs~U[50,200), "
-                        "Adagrad, neg 1, nbatches 20" % n_univ,
-            "value": slots_all * args.c3_steps / el, "unit": "triples/s", "scaling": "strong",
-            "steps": args.c3_steps, "warmup": args.c3_warmup, "s_per_step": el / args.c3_steps,
-            "universes_per_gpu": len(own), "host_universe_build_s": build_s,
-            "roofline": {"bound": "latency (per-universe dependent step chain)", "achieved_per_gpu": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}}
+    out = {"workload": "%s Pu%s %s-shaped, %d universes, D=%s, p%d, tc~U[%d,%d), epochs~U[50,200), Adagrad, neg 1, "
+                       "nbatches 20" % (name.upper(), model, shape, n_univ,
+                                        "U{%d..%d}" % dim_spec if isinstance(dim_spec, tuple) else dim_spec, p_norm,
+                                        tc_range[0], tc_range[1]),
+           "value": slots_all * args.c3_steps / el, "unit": "triples/s", "scaling": "strong",
+           "steps": args.c3_steps, "warmup": args.c3_warmup, "s_per_step": el / args.c3_steps,
+           "universes_per_gpu": len(own), "host_universe_build_s": build_s,
+           "roofline": {"bound": "latency (per-universe dependent step chain)", "achieved_per_gpu": achieved,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}}
+    if do_lp:
+        out["link_prediction"] = universe_link_prediction(L, path, unis, mid, p_norm, ws, dev)
+    L.pt_graph_free(g)
+    return out
+
+
+def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
+    """PuTransE link prediction of the test split over the trained universes (global energy
+    estimation, Parallel_Universe_Config.py:446-642): per rank pt_lp_min_scores of its universes into
+    the key rows, RCCL all_reduce(MIN), pt_rank_rows, pt_lp_metrics. Timed end to end on the device."""
+    from openke import _native
+    from openke.config.Parallel_Universe_Config import lp_pairs
+    E = sum(1 for _ in open(os.path.join(path, "entity2id.txt")))
+    trip = {f: np.loadtxt(os.path.join(path, f), dtype=np.int64, ndmin=2) for f in
+            ("train2id.txt", "valid2id.txt", "test2id.txt")}
+    allt = np.concatenate(list(trip.values()))
+    known = ctypes.c_void_p()
+    ah, at, ar = (np.ascontiguousarray(allt[:, c]) for c in range(3))
+    _native.check(L.pt_known_create(ah.ctypes.data, at.ctypes.data, ar.ctypes.data, len(ah), ctypes.byref(known)))
+    th, tt, tr = (np.ascontiguousarray(trip["test2id.txt"][:, c]) for c in range(3))
+    n = len(th)
+    keys = {}
+    q_row = [np.zeros(n, np.int64), np.zeros(n, np.int64)]
+    for q in range(n):
+        for side, anchor in ((0, int(tt[q])), (1, int(th[q]))):
+            q_row[side][q] = keys.setdefault((side, anchor, int(tr[q])), len(keys))
+    ks = np.array([k[0] for k in keys], np.int64)
+    ka = np.array([k[1] for k in keys], np.int64)
+    kr = np.array([k[2] for k in keys], np.int64)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rows = torch.full((len(keys), E), float("inf"), device=dev)
+    tup = torch.full((len(keys),), float("inf"), device=dev)
+    lp_us, pairs, dremaps = [], [], []
+    for slot, u in enumerate(unis):
+        U = _native.LpUniverse()
+        U.ent, U.rel = u["ent"].data_ptr(), u["rel"].data_ptr()
+        U.normv = u["nv"].data_ptr() if u["nv"] is not None else None
+        U.ent_total, U.rel_total, U.dim = u["ent"].shape[0], u["rel"].shape[0], u["dim"]
+        dr = torch.from_numpy(u["em"]).to(dev)
+        dremaps.append(dr)
+        U.d_ent_remap = dr.data_ptr()
+        lp_us.append(U)
+        pairs.extend(lp_pairs(slot, u["em"], u["rm"], ka, kr, ks))
+    if pairs:
+        arr_u = (_native.LpUniverse * len(lp_us))(*lp_us)
+        arr_p = (_native.LpPair * len(pairs))(*[_native.LpPair(*p) for p in pairs])
+        _native.check(L.pt_lp_min_scores(arr_u, len(lp_us), mid, p_norm, 1, arr_p, len(pairs), E, _native.ptr(rows),
+                                         _native.ptr(tup), _native.stream()))
+    torch.cuda.synchronize()
+    t_score = time.perf_counter() - t0
+    if ws > 1:
+        import torch.distributed as dist
+        dist.all_reduce(rows, op=dist.ReduceOp.MIN)
+        dist.all_reduce(tup, op=dist.ReduceOp.MIN)
+    torch.cuda.synchronize()
+    t_comb = time.perf_counter() - t0 - t_score
+    ranks = []
+    for side, anchor, truth in ((0, tt, th), (1, th, tt)):
+        off = np.zeros(n + 1, np.int64)
+        _native.check(L.pt_known_partners(known, side, n, anchor.ctypes.data, tr.ctypes.data, off.ctypes.data, None))
+        part = np.zeros(max(int(off[-1]), 1), np.int64)
+        _native.check(L.pt_known_partners(known, side, n, anchor.ctypes.data, tr.ctypes.data, off.ctypes.data,
+                                          part.ctypes.data))
+        d_row = torch.from_numpy(q_row[side]).to(dev)
+        d_truth = torch.from_numpy(truth).to(dev)
+        d_off, d_part = torch.from_numpy(off).to(dev), torch.from_numpy(part).to(dev)
+        raw = torch.zeros(n, dtype=torch.int64, device=dev)
+        filt = torch.zeros(n, dtype=torch.int64, device=dev)
+        _native.check(L.pt_rank_rows(_native.ptr(rows), E, _native.ptr(d_row), _native.ptr(d_truth), None,
+                                     _native.ptr(d_off), _native.ptr(d_part), n, _native.ptr(raw), _native.ptr(filt),
+                                     _native.stream()))
+        ranks += [raw.cpu().numpy(), filt.cpu().numpy()]
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    met = np.zeros(10, dtype=np.float32)
+    _native.check(L.pt_lp_metrics(ranks[0].ctypes.data, ranks[1].ctypes.data, ranks[2].ctypes.data,
+                                  ranks[3].ctypes.data, n, met.ctypes.data))
+    L.pt_known_free(known)
+    cand = sum(len(u["em"]) for u in unis)
+    return {"queries": int(n), "keys": len(keys), "pairs_this_rank": len(pairs), "seconds": el,
+            "score_s": t_score, "min_combine_s": t_comb, "rank_s": el - t_score - t_comb,
+            "mrr_mr_hit10_hit3_hit1": [float(x) for x in met[:5]],
+            "note": "universe scoring 4D+4 B per (key, universe entity); ranking 4 B per (query, entity)"}
 
 
 def load_traffic(tag):
@@ -218,7 +330,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS) + ["c3"])
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS) + sorted(PU_WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "putranse_bench"))
@@ -228,17 +340,20 @@ def main():
     args = ap.parse_args()
 
     ws, rank, local = dist_setup()
-    if args.workload == "c3":
+    if args.workload in PU_WORKLOADS:
         dev = torch.device("cuda", torch.cuda.current_device())
         args.c3_steps, args.c3_warmup = args.steps, args.warmup
-        c3 = run_universes(args, ws, rank, dev)
+        c3 = run_universes(args, ws, rank, dev, args.workload)
         if rank == 0:
             rec = {"metric": "training triples/sec (pos+neg)", "value": c3["value"], "unit": "triples/s",
                    "n_gpus": ws, "steps": args.steps, "warmup": args.warmup, "ms_per_step": c3["s_per_step"] * 1e3,
                    "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
-                   "data": "synthetic wn18-shaped graph (tools/synth_kg.py, seed 0), xavier-uniform tables",
+                   "data": "synthetic %s-shaped graph (tools/synth_kg.py, seed 0), xavier-uniform tables" %
+                           PU_WORKLOADS[args.workload][0],
                    "config": {"workload": c3["workload"], "parallelism": "universes sharded k %% %d" % ws},
                    "roofline": c3["roofline"], "universes_per_gpu": c3["universes_per_gpu"]}
+            if "link_prediction" in c3:
+                rec["link_prediction"] = c3["link_prediction"]
             print(json.dumps(rec), flush=True)
         if ws > 1:
             import torch.distributed as dist
@@ -310,7 +425,7 @@ def main():
     bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
     achieved = bytes_step / (sum(per_kernel.values()) * 1e-3) / 1e9
 
-    c3 = None if args.no_c3 else run_universes(args, ws, rank, dev)
+    c3 = None if args.no_c3 else run_universes(args, ws, rank, dev, "c3")
     if rank != 0:
         if ws > 1:
             import torch.distributed as dist

@@ -816,41 +816,90 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
     PT_CHECK((us && pairs && d_key_rows) || n_pairs == 0, PT_EINVAL, "pt_lp_min_scores: null argument");
     if (n_pairs == 0) return PT_OK;
     hipStream_t st = (hipStream_t)stream;
-    // group pairs by universe dim (one kernel shape per dim)
-    std::map<int64_t, std::vector<pt::LpPair>> by_dim;
-    std::map<int64_t, int64_t> max_ent;
     for (int64_t i = 0; i < n_pairs; ++i) {
         const pt_lp_pair &p = pairs[i];
         PT_CHECK(p.universe >= 0 && p.universe < n_universes, PT_EINVAL, "pair universe out of range");
         const pt_lp_universe &U = us[p.universe];
         PT_CHECK(p.anchor >= 0 && p.anchor < U.ent_total && p.rel >= 0 && p.rel < U.rel_total, PT_EINVAL,
                  "pair local ids out of range");
-        by_dim[U.dim].push_back(pt::LpPair{p.key, p.universe, p.anchor, p.rel, p.side});
-        max_ent[U.dim] = std::max(max_ent[U.dim], U.ent_total);
+        PT_CHECK(p.side == 0 || p.side == 1, PT_EINVAL, "pair side must be 0 or 1");
+        PT_CHECK(pt::shape_supported(U.dim), PT_ENOTSUP, "dim not supported");
+    }
+    // one launch pair per embedding dim; pairs sorted by universe inside
+    std::map<int64_t, std::vector<int64_t>> by_dim;   // dim -> universe ids
+    for (int64_t u = 0; u < n_universes; ++u) by_dim[us[u].dim].push_back(u);
+    std::vector<std::vector<pt::LpPair>> per_u((size_t)n_universes);
+    for (int64_t i = 0; i < n_pairs; ++i) {
+        const pt_lp_pair &p = pairs[i];
+        per_u[p.universe].push_back(pt::LpPair{p.key, p.universe, p.anchor, p.rel, p.side});
     }
     std::vector<pt::LpUniverseDev> hu((size_t)n_universes);
     for (int64_t i = 0; i < n_universes; ++i)
         hu[i] = pt::LpUniverseDev{us[i].ent, us[i].rel, us[i].normv, us[i].d_ent_remap, us[i].ent_total, us[i].dim};
-    pt::LpUniverseDev *du = nullptr;
-    PT_HIP(hipMallocAsync((void **)&du, sizeof(pt::LpUniverseDev) * hu.size(), st));
-    PT_HIP(hipMemcpyAsync(du, hu.data(), sizeof(pt::LpUniverseDev) * hu.size(), hipMemcpyHostToDevice, st));
+    // host staging, kept alive until the stream has consumed it (synchronize at the end). Per dim group:
+    // its pairs contiguous and sorted by universe; uoff[2u], uoff[2u+1] = universe u's range relative to
+    // the group's first pair
+    std::vector<pt::LpPair> hp;
+    hp.reserve((size_t)n_pairs);
+    std::vector<int64_t> uoff((size_t)n_universes * 2, 0);
+    std::vector<int32_t> uids;
+    struct DimJob {
+        int64_t dim, p_begin, p_end, u_begin, u_end, max_ent;
+    };
+    std::vector<DimJob> dj;
     for (auto &kv : by_dim) {
-        PT_CHECK(pt::shape_supported(kv.first), PT_ENOTSUP, "dim not supported");
-        auto &v = kv.second;
-        // y-grid limit 65535 per launch
-        for (size_t off = 0; off < v.size(); off += 65535) {
-            const size_t cnt = std::min<size_t>(65535, v.size() - off);
-            pt::LpPair *dp = nullptr;
-            PT_HIP(hipMallocAsync((void **)&dp, sizeof(pt::LpPair) * cnt, st));
-            PT_HIP(hipMemcpyAsync(dp, v.data() + off, sizeof(pt::LpPair) * cnt, hipMemcpyHostToDevice, st));
-            PT_HIP(pt::launch_lp_min(du, dp, (int64_t)cnt, kv.first, max_ent[kv.first], model, p_norm, norm_flag,
-                                     global_ent_total, d_key_rows, d_key_tuple, st));
-            PT_HIP(hipFreeAsync(dp, st));
+        DimJob d{kv.first, (int64_t)hp.size(), 0, (int64_t)uids.size(), 0, 0};
+        for (int64_t u : kv.second) {
+            if (per_u[u].empty()) continue;
+            uoff[2 * u] = (int64_t)hp.size() - d.p_begin;
+            hp.insert(hp.end(), per_u[u].begin(), per_u[u].end());
+            uoff[2 * u + 1] = (int64_t)hp.size() - d.p_begin;
+            uids.push_back((int32_t)u);
+            d.max_ent = std::max(d.max_ent, us[u].ent_total);
+        }
+        d.p_end = (int64_t)hp.size();
+        d.u_end = (int64_t)uids.size();
+        if (d.p_end > d.p_begin) dj.push_back(d);
+    }
+    int64_t max_dim = 0;
+    for (auto &d : dj) max_dim = std::max(max_dim, d.dim);
+    const size_t scratch = (size_t)n_pairs * (size_t)max_dim * (model == 1 ? 2 : 1);
+    char *blk = nullptr;
+    const size_t bytes = sizeof(pt::LpUniverseDev) * hu.size() + sizeof(pt::LpPair) * hp.size() +
+                         sizeof(int64_t) * uoff.size() + sizeof(int32_t) * (uids.size() + 1) + sizeof(float) * scratch +
+                         5 * 256;
+    PT_HIP(hipMallocAsync((void **)&blk, bytes, st));
+    auto carve = [&](size_t n) {
+        char *p = blk;
+        blk += (n + 255) & ~size_t(255);
+        return p;
+    };
+    char *base0 = blk;
+    auto *du = (pt::LpUniverseDev *)carve(sizeof(pt::LpUniverseDev) * hu.size());
+    auto *dp = (pt::LpPair *)carve(sizeof(pt::LpPair) * hp.size());
+    auto *duoff = (int64_t *)carve(sizeof(int64_t) * uoff.size());
+    auto *duids = (int32_t *)carve(sizeof(int32_t) * (uids.size() + 1));
+    auto *dbase = (float *)carve(sizeof(float) * scratch);
+    PT_HIP(hipMemcpyAsync(du, hu.data(), sizeof(pt::LpUniverseDev) * hu.size(), hipMemcpyHostToDevice, st));
+    PT_HIP(hipMemcpyAsync(dp, hp.data(), sizeof(pt::LpPair) * hp.size(), hipMemcpyHostToDevice, st));
+    PT_HIP(hipMemcpyAsync(duoff, uoff.data(), sizeof(int64_t) * uoff.size(), hipMemcpyHostToDevice, st));
+    PT_HIP(hipMemcpyAsync(duids, uids.data(), sizeof(int32_t) * uids.size(), hipMemcpyHostToDevice, st));
+    int rc = PT_OK;
+    for (auto &d : dj) {
+        const int64_t np = d.p_end - d.p_begin;
+        float *b = dbase + d.p_begin * max_dim * (model == 1 ? 2 : 1);   // the group's own scratch region
+        float *nrm = model == 1 ? b + np * d.dim : nullptr;
+        const hipError_t e = pt::launch_lp_min(du, dp + d.p_begin, np, duoff, duids + d.u_begin, d.u_end - d.u_begin,
+                                               d.dim, d.max_ent, model, p_norm, norm_flag, global_ent_total,
+                                               b, nrm, d_key_rows, d_key_tuple, st);
+        if (e != hipSuccess) {
+            rc = pt::fail(PT_EHIP, std::string("launch_lp_min: ") + hipGetErrorString(e));
+            break;
         }
     }
-    PT_HIP(hipFreeAsync(du, st));
+    (void)hipFreeAsync(base0, st);
     PT_HIP(hipStreamSynchronize(st));   // host vectors above must outlive the async copies
-    return PT_OK;
+    return rc;
 }
 
 extern "C" int pt_rank_rows(const float *d_rows, int64_t ent_total, const int64_t *d_row_of, const int64_t *d_truth,

@@ -102,8 +102,11 @@ hipError_t launch_score(const StepParams &P, int mode, const int64_t *h, const i
                         float *out, hipStream_t st);
 hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh, const int64_t *qt, const int64_t *qr,
                                 int64_t nq, int64_t E, float *out, hipStream_t st, int global_order = 0);
-hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, int64_t dim, int64_t max_ent,
-                         int model, int p_norm, int norm_flag, int64_t global_E, float *rows, float *tuple_min,
+// pairs sorted by universe; universe u's pairs are pairs[uoff[2u] .. uoff[2u+1]); uids = the n_active
+// universes with pairs; base / normal: scratch [n_pairs][dim]
+hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, const int64_t *uoff,
+                         const int32_t *uids, int64_t n_active, int64_t dim, int64_t max_ent, int model, int p_norm,
+                         int norm_flag, int64_t global_E, float *base, float *normal, float *rows, float *tuple_min,
                          hipStream_t st);
 
 hipError_t launch_rank_rows(const float *rows, int64_t E, const int64_t *row_of, const int64_t *truth,

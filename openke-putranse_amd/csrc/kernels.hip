@@ -779,75 +779,111 @@ __global__ __launch_bounds__(256) void k_score_queries(StepParams P, int side, c
 }
 
 // ---------------------------------------------------------------- universe link prediction ------
-// For a (key, universe) pair: score every local entity of the universe as the missing side and MIN
-// it into the key's global score row (scores are norms >= 0, so float order == int order).
+// Global energy estimation (Parallel_Universe_Config.py:446-554): for every (key, universe) pair score
+// every local entity of the universe as the missing side and MIN it into the key's global row
+// (scores are norms >= 0, so float order == int order and atomicMin on the bits is exact).
 // side 0 = head prediction (anchor is the tail: e + (r - anchor)), side 1 = tail prediction
 // (anchor is the head: (anchor + r) - e).
+//
+// k_lp_bases: one lane group per pair: the pair's normalized (projected for TransH) anchor combined
+//   with its relation -> base[pair][D] (+ the relation's normal for TransH), and the null_vector tuple
+//   score of the key in this universe (calc_tuple_score, :378-388: raw anchor, no projection).
+// k_lp_scan: one workgroup per (entity chunk, universe): each entity row is loaded (and, for TransE,
+//   normalized) ONCE and scored against every pair of its universe - the universe's rows are read once
+//   per chunk instead of once per pair.
 template <int MODEL, int G, int VEC, int KCH>
-__global__ __launch_bounds__(256) void k_lp_min(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
-                                                int64_t n_pairs, int p_norm, int norm_flag, int64_t global_E,
-                                                float *__restrict__ rows, float *__restrict__ tuple_min) {
+__global__ __launch_bounds__(256) void k_lp_bases(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
+                                                  int64_t n_pairs, int p_norm, int norm_flag, float *__restrict__ base,
+                                                  float *__restrict__ normal, float *__restrict__ tuple_min) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = 256 / G;
     const int lane = threadIdx.x % G;
-    const int grp = threadIdx.x / G;
-    const int64_t pi = blockIdx.y;
+    const int64_t pi = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
     if (pi >= n_pairs) return;
     const LpPair pr = pairs[pi];
     const LpUniverseDev U = us[pr.universe];
     const int D = (int)U.dim;
-    Vec A, R, ah, rh, nW;
+    Vec A, R, ah, rh, nW, b;
     vload(A, U.ent + (int64_t)pr.anchor * D, D, lane);
     vload(R, U.rel + (int64_t)pr.rel * D, D, lane);
-    float adot = 0.f;
-    if (tuple_min && blockIdx.x == 0 && grp == 0) {
-        // null_vector fallback score of the key in this universe: _calc on the RAW anchor row against a
-        // zero vector, ||a^ + r^ - 0|| (tail side) or ||0 + r^ - a^|| (head side)
-        // (Parallel_Universe_Config.py:405-416 calc_tuple_score, :545-554)
-        Vec an, rn, v;
-        if (norm_flag) {
-            vnormalize(A, an);
-            vnormalize(R, rn);
-        } else {
-            an = A; rn = R;
-        }
+    if (norm_flag) vnormalize(R, rh); else rh = R;
+    if (tuple_min) {
+        Vec an, v;
+        if (norm_flag) vnormalize(A, an); else an = A;
 #pragma unroll
-        for (int k = 0; k < Vec::N; ++k) v.x[k] = pr.side == 0 ? rn.x[k] - an.x[k] : an.x[k] + rn.x[k];
-        const float s = vpnorm(v, p_norm);
-        if (lane == 0) atomicMin(reinterpret_cast<int *>(tuple_min + pr.key), __float_as_int(s));
+        for (int k = 0; k < Vec::N; ++k) v.x[k] = pr.side == 0 ? rh.x[k] - an.x[k] : an.x[k] + rh.x[k];
+        const float sc = vpnorm(v, p_norm);
+        if (lane == 0) atomicMin(reinterpret_cast<int *>(tuple_min + pr.key), __float_as_int(sc));
     }
     if constexpr (MODEL == 1) {
         Vec W;
         vload(W, U.normv + (int64_t)pr.rel * D, D, lane);
         vnormalize(W, nW);
-        adot = vdot(A, nW);
+        const float ad = vdot(A, nW);
 #pragma unroll
-        for (int k = 0; k < Vec::N; ++k) A.x[k] = A.x[k] - adot * nW.x[k];
+        for (int k = 0; k < Vec::N; ++k) A.x[k] = A.x[k] - ad * nW.x[k];
+        vstore(nW, normal + pi * D, D, lane);
     }
-    if (norm_flag) {
-        vnormalize(A, ah);
-        vnormalize(R, rh);
-    } else {
-        ah = A; rh = R;
-    }
-    // head prediction: score = e + (r - t); tail prediction: (h + r) - e   (TransE.py:56-59)
-    Vec base;
+    if (norm_flag) vnormalize(A, ah); else ah = A;
 #pragma unroll
-    for (int k = 0; k < Vec::N; ++k) base.x[k] = pr.side == 0 ? rh.x[k] - ah.x[k] : ah.x[k] + rh.x[k];
-    float *out = rows + (int64_t)pr.key * global_E;
-    for (int64_t e = (int64_t)blockIdx.x * GPB + grp; e < U.ent_total; e += (int64_t)gridDim.x * GPB) {
-        Vec X, xh, v;
-        vload(X, U.ent + e * D, D, lane);
-        if constexpr (MODEL == 1) {
-            const float xd = vdot(X, nW);
+    for (int k = 0; k < Vec::N; ++k) b.x[k] = pr.side == 0 ? rh.x[k] - ah.x[k] : ah.x[k] + rh.x[k];
+    vstore(b, base + pi * D, D, lane);
+}
+
+template <int MODEL, int G, int VEC, int KCH>
+__global__ __launch_bounds__(256) void k_lp_scan(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
+                                                 const int64_t *__restrict__ uoff, const int32_t *__restrict__ uids,
+                                                 int p_norm, int norm_flag, int64_t global_E,
+                                                 const float *__restrict__ base, const float *__restrict__ normal,
+                                                 float *__restrict__ rows) {
+    using Vec = V<G, VEC, KCH>;
+    constexpr int GPB = 256 / G;
+    constexpr int EPG = 4;   // entities per lane group: each pair's base row is loaded once per 4 entities
+    const int lane = threadIdx.x % G;
+    const int grp = threadIdx.x / G;
+    const int32_t u = uids[blockIdx.y];
+    const LpUniverseDev U = us[u];
+    const int D = (int)U.dim;
+    const int64_t p0 = uoff[2 * u], p1 = uoff[2 * u + 1];   // the universe's pairs (relative to `pairs`)
+    const int64_t stride = (int64_t)gridDim.x * GPB * EPG;
+    for (int64_t e0 = ((int64_t)blockIdx.x * GPB + grp) * EPG; e0 < U.ent_total; e0 += stride) {
+        Vec X[EPG], xh[EPG];
+        int64_t col[EPG];
 #pragma unroll
-            for (int k = 0; k < Vec::N; ++k) X.x[k] = X.x[k] - xd * nW.x[k];
+        for (int q = 0; q < EPG; ++q) {
+            const int64_t e = e0 + q < U.ent_total ? e0 + q : U.ent_total - 1;   // tail: repeat the last row
+            vload(X[q], U.ent + e * D, D, lane);
+            col[q] = e0 + q < U.ent_total ? U.remap[e] : -1;
         }
-        if (norm_flag) vnormalize(X, xh); else xh = X;
+        if constexpr (MODEL == 0) {
 #pragma unroll
-        for (int k = 0; k < Vec::N; ++k) v.x[k] = pr.side == 0 ? xh.x[k] + base.x[k] : base.x[k] - xh.x[k];
-        const float s = vpnorm(v, p_norm);
-        if (lane == 0) atomicMin(reinterpret_cast<int *>(out + U.remap[e]), __float_as_int(s));
+            for (int q = 0; q < EPG; ++q) {
+                if (norm_flag) vnormalize(X[q], xh[q]); else xh[q] = X[q];
+            }
+        }
+        for (int64_t pi = p0; pi < p1; ++pi) {
+            const LpPair pr = pairs[pi];
+            Vec b;
+            vload(b, base + pi * D, D, lane);
+            Vec nW;
+            if constexpr (MODEL == 1) vload(nW, normal + pi * D, D, lane);
+#pragma unroll
+            for (int q = 0; q < EPG; ++q) {
+                if constexpr (MODEL == 1) {
+                    Vec xp;
+                    const float xd = vdot(X[q], nW);
+#pragma unroll
+                    for (int k = 0; k < Vec::N; ++k) xp.x[k] = X[q].x[k] - xd * nW.x[k];
+                    if (norm_flag) vnormalize(xp, xh[q]); else xh[q] = xp;
+                }
+                Vec v;
+#pragma unroll
+                for (int k = 0; k < Vec::N; ++k) v.x[k] = pr.side == 0 ? xh[q].x[k] + b.x[k] : b.x[k] - xh[q].x[k];
+                const float sc = vpnorm(v, p_norm);
+                if (lane == 0 && col[q] >= 0)
+                    atomicMin(reinterpret_cast<int *>(rows + (int64_t)pr.key * global_E + col[q]), __float_as_int(sc));
+            }
+        }
     }
 }
 
@@ -1106,25 +1142,37 @@ hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, int64_t dim, int64_t max_ent,
-                         int model, int p_norm, int norm_flag, int64_t global_E, float *rows, float *tuple_min,
+hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, const int64_t *uoff,
+                         const int32_t *uids, int64_t n_active, int64_t dim, int64_t max_ent, int model, int p_norm,
+                         int norm_flag, int64_t global_E, float *base, float *normal, float *rows, float *tuple_min,
                          hipStream_t st) {
     if (n_pairs <= 0) return hipSuccess;
     const Shape s = pick_shape(dim);
     const int64_t gpb = 256 / s.G;
-    int64_t bx = (max_ent + gpb - 1) / gpb;
-    if (bx > 64) bx = 64;
+    const dim3 gb((unsigned)((n_pairs + gpb - 1) / gpb)), block(256);
+    int64_t bx = (max_ent + gpb * 4 - 1) / (gpb * 4);
+    if (bx > 32) bx = 32;
     if (bx < 1) bx = 1;
-    const dim3 grid((unsigned)bx, (unsigned)n_pairs), block(256);
-#define PT_LP(G_, V_, K_)                                                                                         \
-    if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                                              \
-        if (model == 0)                                                                                           \
-            hipLaunchKernelGGL((dev::k_lp_min<0, G_, V_, K_>), grid, block, 0, st, us, pairs, n_pairs, p_norm,    \
-                               norm_flag, global_E, rows, tuple_min);                                             \
-        else                                                                                                      \
-            hipLaunchKernelGGL((dev::k_lp_min<1, G_, V_, K_>), grid, block, 0, st, us, pairs, n_pairs, p_norm,    \
-                               norm_flag, global_E, rows, tuple_min);                                             \
-        return hipGetLastError();                                                                               \
+#define PT_LP(G_, V_, K_)                                                                                          \
+    if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                                               \
+        for (int64_t y0 = 0; y0 < n_active; y0 += 65535) {                                                         \
+            const dim3 gs((unsigned)bx, (unsigned)(n_active - y0 < 65535 ? n_active - y0 : 65535));              \
+            if (y0 == 0) {                                                                                         \
+                if (model == 0)                                                                                    \
+                    hipLaunchKernelGGL((dev::k_lp_bases<0, G_, V_, K_>), gb, block, 0, st, us, pairs, n_pairs,    \
+                                       p_norm, norm_flag, base, normal, tuple_min);                                \
+                else                                                                                               \
+                    hipLaunchKernelGGL((dev::k_lp_bases<1, G_, V_, K_>), gb, block, 0, st, us, pairs, n_pairs,    \
+                                       p_norm, norm_flag, base, normal, tuple_min);                                \
+            }                                                                                                      \
+            if (model == 0)                                                                                        \
+                hipLaunchKernelGGL((dev::k_lp_scan<0, G_, V_, K_>), gs, block, 0, st, us, pairs, uoff, uids + y0,   \
+                                   p_norm, norm_flag, global_E, base, normal, rows);                                \
+            else                                                                                                   \
+                hipLaunchKernelGGL((dev::k_lp_scan<1, G_, V_, K_>), gs, block, 0, st, us, pairs, uoff, uids + y0,   \
+                                   p_norm, norm_flag, global_E, base, normal, rows);                                \
+        }                                                                                                          \
+        return hipGetLastError();                                                                                  \
     }
     PT_SHAPES(PT_LP)
 #undef PT_LP
