@@ -117,7 +117,7 @@ def _xavier(rng, rows, dim):
     return rng.uniform(-b, b, (rows, dim)).astype(np.float32)
 
 
-def run_universes(args, ws, rank, dev, name="c3"):
+def run_universes(args, ws, rank, dev, name="c3", cpu=True):
     """PuTransE / PuTransH universes: universe k on rank k % N (no collective in training), Adagrad,
     neg 1, bern 0, filter 0, nbatches 20, 8 sampler threads. One step = every universe's full training
     run (all its epochs) in one persistent launch. C4 adds link prediction over the test split: each
@@ -231,7 +231,41 @@ def run_universes(args, ws, rank, dev, name="c3"):
     if do_lp:
         out["link_prediction"] = universe_link_prediction(L, path, unis, mid, p_norm, ws, dev)
     L.pt_graph_free(g)
+    if cpu and ws == 1 and rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = universe_cpu_baseline(path, name, args.cpu_seconds)
     return out
+
+
+def universe_cpu_baseline(path, name, seconds):
+    """Oracle (single-thread C restatement) training whole universes of the same workload, in id
+    order, until `seconds` have elapsed: universe construction + epochs x 20 Adagrad steps each."""
+    sys.path.insert(0, HERE)
+    import oracle
+    shape, n_univ, model, dim_spec, p_norm, tc_range, margin_range, _ = PU_WORKLOADS[name]
+    kg = oracle.KG.load(path)
+    slots, n, t0 = 0, 0, time.perf_counter()
+    for k in range(n_univ):
+        if time.perf_counter() - t0 >= seconds:
+            break
+        tc, bal, margin, epochs, lr = universe_draws(k, tc_range, margin_range)
+        D = int(np.random.default_rng(1000 + k).integers(dim_spec[0], dim_spec[1] + 1)) \
+            if isinstance(dim_spec, tuple) else dim_spec
+        rng_c = oracle.GlibcRand(4 + k)
+        st = rng_c.rand_reset(8)
+        ug, _, _ = kg.universe(rng_c, tc, bal)
+        bs = ug.train_total // 20
+        rng = np.random.default_rng(k)
+        ent = _xavier(rng, ug.ent_total, D)
+        rel = _xavier(rng, ug.rel_total, D)
+        nv = _xavier(rng, ug.rel_total, D) if model == "TransH" else None
+        accs = (np.zeros_like(ent), np.zeros_like(rel), None if nv is None else np.zeros_like(nv))
+        slots += oracle.train_loop(ug, st, 8, bs, 1, 0, 0, model, p_norm, True, "adagrad", lr, margin,
+                                   (ent, rel, nv), accs, epochs * 20)
+        n += 1
+    el = time.perf_counter() - t0
+    return {"value": slots / el, "unit": "triples/s", "cores": 1, "kind": "port",
+            "sample": "%d whole universes (construction + epochs x 20 Adagrad steps) of the same workload, "
+                      "oracle/oracle.c single thread, %.1f s" % (n, el)}
 
 
 def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
@@ -354,6 +388,8 @@ def main():
                    "roofline": c3["roofline"], "universes_per_gpu": c3["universes_per_gpu"]}
             if "link_prediction" in c3:
                 rec["link_prediction"] = c3["link_prediction"]
+            if "cpu_baseline" in c3:
+                rec["cpu_baseline"] = c3["cpu_baseline"]
             print(json.dumps(rec), flush=True)
         if ws > 1:
             import torch.distributed as dist
@@ -425,7 +461,7 @@ def main():
     bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
     achieved = bytes_step / (sum(per_kernel.values()) * 1e-3) / 1e9
 
-    c3 = None if args.no_c3 else run_universes(args, ws, rank, dev, "c3")
+    c3 = None if args.no_c3 else run_universes(args, ws, rank, dev, "c3", cpu=False)
     if rank != 0:
         if ws > 1:
             import torch.distributed as dist

@@ -825,35 +825,48 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
         PT_CHECK(p.side == 0 || p.side == 1, PT_EINVAL, "pair side must be 0 or 1");
         PT_CHECK(pt::shape_supported(U.dim), PT_ENOTSUP, "dim not supported");
     }
-    // one launch pair per embedding dim; pairs sorted by universe inside
-    std::map<int64_t, std::vector<int64_t>> by_dim;   // dim -> universe ids
-    for (int64_t u = 0; u < n_universes; ++u) by_dim[us[u].dim].push_back(u);
-    std::vector<std::vector<pt::LpPair>> per_u((size_t)n_universes);
+    // Jobs = (embedding dim, key batch): a key batch's score rows (keys x global_ent_total floats) are
+    // sized to stay resident in the Infinity Cache while its pairs' atomicMins land (PT_LP_BATCH_MB,
+    // default 192); inside a job the pairs are sorted by universe so each universe's entity rows are
+    // read once per job.
+    int64_t n_keys = 0;
+    for (int64_t i = 0; i < n_pairs; ++i) n_keys = std::max<int64_t>(n_keys, (int64_t)pairs[i].key + 1);
+    int64_t batch_mb = 192;
+    if (const char *v = getenv("PT_LP_BATCH_MB")) batch_mb = std::max<int64_t>(1, atoll(v));
+    const int64_t keys_per_batch =
+        std::max<int64_t>(1, (batch_mb << 20) / (4 * std::max<int64_t>(global_ent_total, 1)));
+    const int64_t n_batches = (n_keys + keys_per_batch - 1) / keys_per_batch;
+    std::map<std::pair<int64_t, int64_t>, std::vector<std::vector<pt::LpPair>>> jobs_pairs;   // (dim, batch)
     for (int64_t i = 0; i < n_pairs; ++i) {
         const pt_lp_pair &p = pairs[i];
+        auto &per_u = jobs_pairs[{us[p.universe].dim, p.key / keys_per_batch}];
+        if (per_u.empty()) per_u.resize((size_t)n_universes);
         per_u[p.universe].push_back(pt::LpPair{p.key, p.universe, p.anchor, p.rel, p.side});
     }
+    (void)n_batches;
     std::vector<pt::LpUniverseDev> hu((size_t)n_universes);
     for (int64_t i = 0; i < n_universes; ++i)
         hu[i] = pt::LpUniverseDev{us[i].ent, us[i].rel, us[i].normv, us[i].d_ent_remap, us[i].ent_total, us[i].dim};
-    // host staging, kept alive until the stream has consumed it (synchronize at the end). Per dim group:
-    // its pairs contiguous and sorted by universe; uoff[2u], uoff[2u+1] = universe u's range relative to
-    // the group's first pair
+    // host staging, kept alive until the stream has consumed it (synchronize at the end). Per job: its
+    // pairs contiguous and sorted by universe; uoff[job][2u], uoff[job][2u+1] = universe u's range
+    // relative to the job's first pair
     std::vector<pt::LpPair> hp;
     hp.reserve((size_t)n_pairs);
-    std::vector<int64_t> uoff((size_t)n_universes * 2, 0);
+    std::vector<int64_t> uoff;
     std::vector<int32_t> uids;
     struct DimJob {
-        int64_t dim, p_begin, p_end, u_begin, u_end, max_ent;
+        int64_t dim, p_begin, p_end, u_begin, u_end, max_ent, uoff_begin;
     };
     std::vector<DimJob> dj;
-    for (auto &kv : by_dim) {
-        DimJob d{kv.first, (int64_t)hp.size(), 0, (int64_t)uids.size(), 0, 0};
-        for (int64_t u : kv.second) {
-            if (per_u[u].empty()) continue;
-            uoff[2 * u] = (int64_t)hp.size() - d.p_begin;
-            hp.insert(hp.end(), per_u[u].begin(), per_u[u].end());
-            uoff[2 * u + 1] = (int64_t)hp.size() - d.p_begin;
+    for (auto &kv : jobs_pairs) {
+        DimJob d{kv.first.first, (int64_t)hp.size(), 0, (int64_t)uids.size(), 0, 0, (int64_t)uoff.size()};
+        uoff.resize(uoff.size() + 2 * (size_t)n_universes, 0);
+        for (int64_t u = 0; u < n_universes; ++u) {
+            const auto &v = kv.second[u];
+            if (v.empty()) continue;
+            uoff[d.uoff_begin + 2 * u] = (int64_t)hp.size() - d.p_begin;
+            hp.insert(hp.end(), v.begin(), v.end());
+            uoff[d.uoff_begin + 2 * u + 1] = (int64_t)hp.size() - d.p_begin;
             uids.push_back((int32_t)u);
             d.max_ent = std::max(d.max_ent, us[u].ent_total);
         }
@@ -889,7 +902,8 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
         const int64_t np = d.p_end - d.p_begin;
         float *b = dbase + d.p_begin * max_dim * (model == 1 ? 2 : 1);   // the group's own scratch region
         float *nrm = model == 1 ? b + np * d.dim : nullptr;
-        const hipError_t e = pt::launch_lp_min(du, dp + d.p_begin, np, duoff, duids + d.u_begin, d.u_end - d.u_begin,
+        const hipError_t e = pt::launch_lp_min(du, dp + d.p_begin, np, duoff + d.uoff_begin, duids + d.u_begin,
+                                               d.u_end - d.u_begin,
                                                d.dim, d.max_ent, model, p_norm, norm_flag, global_ent_total,
                                                b, nrm, d_key_rows, d_key_tuple, st);
         if (e != hipSuccess) {
