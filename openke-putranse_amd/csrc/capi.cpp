@@ -63,6 +63,7 @@ struct pt_trainer {
     size_t csr_cap = 0;
     pt::CsrWork csr{};
     int64_t csr_bs = 0, csr_neg = 0, csr_chunk = 0;   // layout the workspace was carved for
+    int64_t lpart_cap = 0;                             // W.lpart capacity (positives)
     int device = -1;
     hipStream_t cap = nullptr;
     std::map<GraphKey, hipGraphExec_t> graphs;
@@ -75,6 +76,7 @@ struct pt_trainer {
         if (cap) (void)hipStreamDestroy(cap);
         if (ws_block) (void)hipFree(ws_block);
         if (csr_block) (void)hipFree(csr_block);
+        if (W.lpart) (void)hipFree(W.lpart);
     }
 };
 
@@ -385,8 +387,24 @@ static int enqueue_external(pt_trainer *t, int64_t bs, int64_t neg, const int64_
     return PT_OK;
 }
 
+// per-positive loss partials for batches of up to `bs` positives (grown on demand, never during a
+// capture: callers prepare before enqueueing)
+static int ensure_lpart(pt_trainer *t, int64_t bs) {
+    if (bs <= t->lpart_cap) return PT_OK;
+    PT_HIP(hipDeviceSynchronize());   // queued work may still use the old buffer
+    t->drop_graphs();
+    if (t->W.lpart) (void)hipFree(t->W.lpart);
+    t->W.lpart = nullptr;
+    t->lpart_cap = 0;
+    PT_HIP(hipMalloc(&t->W.lpart, sizeof(float) * (size_t)bs));
+    t->lpart_cap = bs;
+    return PT_OK;
+}
+
 static int prepare_sampled(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t steps) {
     int rc = check_step_args(t->P, s, bs, neg, nullptr);
+    if (rc) return rc;
+    rc = ensure_lpart(t, bs);
     if (rc) return rc;
     rc = s->g->upload();
     if (rc) return rc;
@@ -402,6 +420,8 @@ extern "C" int pt_trainer_step(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t
     if (d_bh) {
         PT_CHECK(d_bt && d_br, PT_EINVAL, "external batch needs h, t and r arrays");
         PT_CHECK(bs > 0 && neg > 0, PT_EINVAL, "batch_size and neg_ent must be positive");
+        int rc = ensure_lpart(t, bs);
+        if (rc) return rc;
         return enqueue_external(t, bs, neg, d_bh, d_bt, d_br, d_loss, (hipStream_t)stream);
     }
     int rc = prepare_sampled(t, s, bs, neg, 1);

@@ -119,6 +119,49 @@ __device__ __forceinline__ bool vnonzero(const V<G, VEC, KCH> &a) {
     return gsum<G>((float)nz) != 0.f;
 }
 
+// Raw-buffer row access (buffer_load / buffer_store with a table-wide resource): lanes past the row
+// end get an out-of-range offset, so the hardware returns 0 / drops the store - no exec masking and
+// no branches around the access, which keeps s_waitcnt counting exact for software pipelining.
+// Callers check that every byte offset fits in 31 bits.
+typedef unsigned int pt_u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOob = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
+}
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void bload(V<G, VEC, KCH> &o, __amdgpu_buffer_rsrc_t rs, uint32_t row_bytes, int D,
+                                      int lane) {
+#pragma unroll
+    for (int k = 0; k < KCH; ++k) {
+        const int c = k * G + lane;
+        const uint32_t off = c * VEC < D ? row_bytes + (uint32_t)(c * VEC * 4) : kOob;
+        if constexpr (VEC == 4) {
+            const pt_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+            o.x[k * 4 + 0] = __uint_as_float(v.x); o.x[k * 4 + 1] = __uint_as_float(v.y);
+            o.x[k * 4 + 2] = __uint_as_float(v.z); o.x[k * 4 + 3] = __uint_as_float(v.w);
+        } else {
+            static_assert(VEC == 1, "bload: VEC 1 or 4");
+            o.x[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+    }
+}
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void bstore(const V<G, VEC, KCH> &o, __amdgpu_buffer_rsrc_t rs, uint32_t row_bytes, int D,
+                                       int lane) {
+#pragma unroll
+    for (int k = 0; k < KCH; ++k) {
+        const int c = k * G + lane;
+        const uint32_t off = c * VEC < D ? row_bytes + (uint32_t)(c * VEC * 4) : kOob;
+        if constexpr (VEC == 4) {
+            const pt_u32x4 v = {__float_as_uint(o.x[k * 4 + 0]), __float_as_uint(o.x[k * 4 + 1]),
+                                __float_as_uint(o.x[k * 4 + 2]), __float_as_uint(o.x[k * 4 + 3])};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.x[k]), rs, off, 0, 0);
+        }
+    }
+}
+
 // sqrt / reciprocal: correctly rounded by default; FAST = the hardware v_sqrt_f32 / v_rcp_f32 (1 ulp),
 // used by the training step, whose results are compared with a tolerance anyway (the scoring kernels
 // that feed ranking keep the IEEE forms)

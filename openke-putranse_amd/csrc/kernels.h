@@ -23,6 +23,10 @@ struct StepParams {
 struct StepWorkspace {
     float *gent = nullptr, *grel = nullptr, *gnorm = nullptr;   // gradient rows (zero between steps)
     int *fent = nullptr, *frel = nullptr, *fnorm = nullptr;      // touched-row flags
+    // per-positive loss partials [batch]: sum over the positive's negatives of max(p - n, -m); the apply
+    // pass reduces them in a fixed order into the step's loss (one same-address float atomic per
+    // positive serialises at the memory side: it cost ~13 us per C2 step)
+    float *lpart = nullptr;
 };
 
 // Workspace of the counting-sort (CSR) gradient path for large neg (see k_sample_csr). The sampling

@@ -172,6 +172,7 @@ __global__ __launch_bounds__(1024) void k_scan_counts(int32_t *__restrict__ cnt_
 struct GlobalSink {
     float *gent, *grel, *gnorm;
     int *fent, *frel, *fnorm;
+    float *lpart;   // per-positive loss partials
     template <int G, int VEC, int KCH>
     __device__ __forceinline__ void ent(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
         vatomic(g, gent + row * D, D, lane);
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(256) void k_step(StepParams P, const int64_t *__res
             h = bh[o]; t = bt[o]; r = br[o];
         },
         sink, lane);
-    if (lane == 0 && loss) atomicAdd(loss, lsum * P.inv_count);
+    if (lane == 0 && sink.lpart) sink.lpart[b] = lsum;
 }
 
 // Fused step with in-kernel sampling (the Trainer.run hot loop).
@@ -468,7 +469,219 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
             sink.norm(rp, aW, D, lane);
         }
     }
-    if (lane == 0 && loss) atomicAdd(loss, lsum * P.inv_count);
+    if (lane == 0 && sink.lpart) sink.lpart[b] = lsum;
+}
+
+// Fused TransE step on a counting-sort batch (the C2 hot loop, CSR path). ONE lane group per positive
+// takes all of its negatives: the positive's forward runs once (no sub-group split, no LDS meet), its
+// negatives' records sit in registers (lane j of the group holds negative w0 + j of the current window
+// of G) and are broadcast with readlane (G = 64: scalar entity ids, scalar branches) or a group
+// shuffle; the rows of NCH negatives load while the previous NCH compute (double buffer).
+// The kernel is VALU-issue bound at C2's shape, so the per-negative work is kept minimal: the tail-side
+// base h-hat + r-hat is formed once (same association as (h + r) - t), the corrupted row's gradient is
+// formed with the sign of its slot and stored to its counting-sort slot, and two accumulators collect
+// the positive's rows: At = sum over tail-corrupted negatives of dL/dv, Ah over head-corrupted ones
+// (dL/dh-hat = At + g+, dL/dr-hat = At + Ah + g+, dL/dt-hat = -(Ah + g+)).
+template <int G>
+__device__ __forceinline__ int32_t gbcast(int32_t v, int j) {
+    if constexpr (G == 64) return __builtin_amdgcn_readlane(v, j); else return __shfl(v, j, G);
+}
+
+template <int G, int VEC, int KCH, int NCH, int S, int PN>
+__global__ __launch_bounds__(256) void k_step_csr(StepParams P, GlobalSink sink, CsrWork cw) {
+    using Vec = V<G, VEC, KCH>;
+    constexpr int GPB = 256 / G;     // lane groups per block
+    constexpr int PPB = GPB / S;     // positives per block
+    constexpr int RW = KCH * G * VEC;
+    __shared__ float red[S > 1 ? GPB * 2 * RW + 2 * GPB : 1];
+    __shared__ float trb[PPB * 3 * RW];   // positive-row gradients, transposed for coalesced atomics
+    const int lane = threadIdx.x % G;
+    const int grp = threadIdx.x / G;
+    const int sub = grp % S;
+    const int64_t b = (int64_t)blockIdx.x * PPB + grp / S;
+    const bool active = b < P.batch_size;   // group-uniform
+    const int D = (int)P.dim;
+    const uint32_t rowb = (uint32_t)D * 4u;
+    const int neg = (int)P.neg;
+    constexpr int p = PN;   // p_norm as a template parameter: no per-negative branch on it
+    const bool nf = P.norm_flag != 0;
+    const float m = P.margin, inv = P.inv_count;
+    // sub-group `sub` takes negatives [k_lo, k_hi)
+    const int nper = (neg + S - 1) / S;
+    const int k_lo = sub * nper < neg ? sub * nper : neg;
+    const int k_hi = k_lo + nper < neg ? k_lo + nper : neg;
+    Vec At, Ah, vpos;
+    vzero(At); vzero(Ah); vzero(vpos);
+    float csum = 0.f, lsum = 0.f, ps = 0.f;
+    int32_t hp = 0, rp = 0, tp = 0;
+    if (active) {
+        const auto ent_rs = make_rsrc(P.ent, (uint32_t)P.ent_total * rowb);
+        const auto rel_rs = make_rsrc(P.rel, (uint32_t)P.rel_total * rowb);
+        const auto con_rs = make_rsrc(cw.contrib, (uint32_t)(P.batch_size * neg) * rowb);
+        const int4 q = cw.pos[b];
+        hp = uni<G>(q.x); rp = uni<G>(q.y); tp = uni<G>(q.z);
+        const int32_t *nrec = cw.neg + b * neg;
+        const int32_t *ndst = cw.off + b * neg;
+        int w0 = k_lo, wend = k_hi - k_lo < G ? k_hi : k_lo + G;
+        int32_t rec = 0, dst = 0;
+        if (w0 + lane < wend) {
+            rec = nrec[w0 + lane];
+            dst = ndst[w0 + lane];
+        }
+        Vec H, T, Rr;
+        bload(H, ent_rs, (uint32_t)hp * rowb, D, lane);
+        bload(T, ent_rs, (uint32_t)tp * rowb, D, lane);
+        bload(Rr, rel_rs, (uint32_t)rp * rowb, D, lane);
+        // every chunk issues exactly NCH row loads (past the window end: the window's last row again), so
+        // the waits for a chunk never cover the next chunk's loads
+        Vec EA[NCH], EB[NCH];
+        auto load_chunk = [&](Vec(&E)[NCH], int k0) {
+#pragma unroll
+            for (int u = 0; u < NCH; ++u) {
+                const int kk = k0 + u < wend ? k0 + u : wend - 1;
+                const uint32_t e = (uint32_t)(gbcast<G>(rec, kk - w0) >> 1);
+                bload(E[u], ent_rs, e * rowb, D, lane);
+            }
+        };
+        if (w0 < wend) load_chunk(EA, w0);
+        // ---- positive forward
+        Vec hh, rh, th, bt;
+        if (nf) {
+            vnormalize<true>(H, hh);
+            vnormalize<true>(Rr, rh);
+            vnormalize<true>(T, th);
+        } else {
+            hh = H; rh = Rr; th = T;
+        }
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            bt.x[i] = hh.x[i] + rh.x[i];
+            vpos.x[i] = bt.x[i] - th.x[i];
+        }
+        ps = vpnorm<true>(vpos, p);
+        auto process = [&](Vec(&E)[NCH], int k0) {
+#pragma unroll
+            for (int u = 0; u < NCH; ++u) {
+                if (k0 + u < wend) {   // (a guard, not a break: the loop must unroll fully, E[u] are registers)
+                const int32_t r = gbcast<G>(rec, k0 + u - w0);
+                const uint32_t slot = (uint32_t)gbcast<G>(dst, k0 + u - w0) * rowb;
+                const bool tail_side = r & 1;
+                Vec eh, vk, gs;
+                if (nf) vnormalize<true>(E[u], eh); else eh = E[u];
+                if (tail_side) {
+#pragma unroll
+                    for (int i = 0; i < Vec::N; ++i) vk.x[i] = bt.x[i] - eh.x[i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < Vec::N; ++i) vk.x[i] = (eh.x[i] + rh.x[i]) - th.x[i];
+                }
+                const float ns = vpnorm<true>(vk, p);
+                const float a = uni<G>(ps - ns);
+                lsum += a > -m ? a : -m;
+                const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
+                csum += c;
+                // slot gradient d loss / d e-hat: -g for a corrupted tail, +g for a corrupted head
+                // (g = dL/dv); an inactive pair stores zeros (the reserved slot must be defined)
+                vpnorm_bwd<true>(vk, ns, p, tail_side ? c : -c, gs);
+                bstore(gs, con_rs, slot, D, lane);
+                if (tail_side) {
+#pragma unroll
+                    for (int i = 0; i < Vec::N; ++i) At.x[i] -= gs.x[i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < Vec::N; ++i) Ah.x[i] += gs.x[i];
+                }
+                }
+            }
+        };
+        while (w0 < wend) {
+            for (int c0 = w0; c0 < wend;) {
+                if (c0 + NCH < wend) load_chunk(EB, c0 + NCH);
+                process(EA, c0);
+                c0 += NCH;
+                if (c0 >= wend) break;
+                if (c0 + NCH < wend) load_chunk(EA, c0 + NCH);
+                process(EB, c0);
+                c0 += NCH;
+            }
+            w0 = wend;
+            if (w0 >= k_hi) break;
+            wend = k_hi - w0 < G ? k_hi : w0 + G;
+            rec = dst = 0;
+            if (w0 + lane < wend) {
+                rec = nrec[w0 + lane];
+                dst = ndst[w0 + lane];
+            }
+            load_chunk(EA, w0);
+        }
+    }
+    if constexpr (S > 1) {
+        // ---- the sub-groups' partials meet in LDS; sub-group 0 sums them in a fixed order
+        float *mr = red + grp * 2 * RW;
+#pragma unroll
+        for (int k = 0; k < Vec::N; ++k) {
+            const int c = ((k / VEC) * G + lane) * VEC + k % VEC;
+            mr[c] = At.x[k];
+            mr[RW + c] = Ah.x[k];
+        }
+        float *cs = red + GPB * 2 * RW;
+        if (lane == 0) {
+            cs[grp * 2 + 0] = csum;
+            cs[grp * 2 + 1] = lsum;
+        }
+        __syncthreads();
+        if (sub != 0 || !active) return;
+        vzero(At); vzero(Ah);
+        csum = lsum = 0.f;
+        for (int q2 = 0; q2 < S; ++q2) {
+            const float *qr = red + (grp + q2) * 2 * RW;
+#pragma unroll
+            for (int k = 0; k < Vec::N; ++k) {
+                const int c = ((k / VEC) * G + lane) * VEC + k % VEC;
+                At.x[k] += qr[c];
+                Ah.x[k] += qr[RW + c];
+            }
+            csum += cs[(grp + q2) * 2 + 0];
+            lsum += cs[(grp + q2) * 2 + 1];
+        }
+    }
+    if (!active) return;
+    if (lane == 0 && sink.lpart) sink.lpart[b] = lsum;
+    if (uni<G>(csum) == 0.f) return;   // no active pair: every accumulator is zero
+    Vec gv, aH, aR, aT;
+    vpnorm_bwd<true>(vpos, ps, p, csum, gv);
+#pragma unroll
+    for (int i = 0; i < Vec::N; ++i) {
+        aH.x[i] = At.x[i] + gv.x[i];
+        aR.x[i] = (At.x[i] + Ah.x[i]) + gv.x[i];
+        aT.x[i] = -(Ah.x[i] + gv.x[i]);
+    }
+    // float4 lanes make a row atomic touch 4x the cache lines per instruction: pass the three rows
+    // through LDS so lane l adds floats l, l + G, ... (256 contiguous bytes per instruction at G = 64)
+    float *tb = trb + (grp / S) * 3 * RW;
+#pragma unroll
+    for (int k = 0; k < Vec::N; ++k) {
+        const int c = ((k / VEC) * G + lane) * VEC + k % VEC;
+        tb[c] = aR.x[k];
+        tb[RW + c] = aH.x[k];
+        tb[2 * RW + c] = aT.x[k];
+    }
+    __builtin_amdgcn_wave_barrier();   // the group is within one wave: LDS order is program order
+    float *gr = sink.grel + (int64_t)rp * D, *gh = sink.gent + (int64_t)hp * D, *gt = sink.gent + (int64_t)tp * D;
+#pragma unroll
+    for (int k = 0; k < KCH * VEC; ++k) {
+        const int c = k * G + lane;
+        if (c < D) {
+            atomicAdd(gr + c, tb[c]);
+            atomicAdd(gh + c, tb[RW + c]);
+            atomicAdd(gt + c, tb[2 * RW + c]);
+        }
+    }
+    if (lane == 0) {
+        sink.frel[rp] = 1;
+        sink.fent[hp] = 1;
+        sink.fent[tp] = 1;
+    }
 }
 
 // Sparse apply: for every touched row finish the gradient (normalize Jacobian of the pre-step row
@@ -487,12 +700,32 @@ struct ApplyParams {
     int64_t dim;
     int opt;
     float lr;
-    // sampler advance + loss margin (done by block 0)
+    // sampler advance + loss (done by block 0)
     uint64_t *states;
     int64_t threads, bs, dpp;
     float *loss;
-    float margin;
+    const float *lpart;   // [bs] per-positive loss partials of the step
+    float margin, inv_count;
 };
+
+// block 0, first wave: advance the sampler streams and reduce the step's loss partials in a fixed
+// order: loss += inv_count * sum(lpart) + margin (MarginLoss.py:24-28)
+__device__ __forceinline__ void apply_block0(const ApplyParams &A) {
+    const int lane = (int)threadIdx.x;
+    if (A.states) advance_states(A.states, A.threads, A.bs, A.dpp, lane);
+    if (A.loss && A.lpart) {
+        float s = 0.f;
+        for (int64_t i0 = lane; i0 < A.bs; i0 += 64 * 8) {   // 8 independent loads in flight per lane
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = i0 + u * 64 < A.bs ? A.lpart[i0 + u * 64] : 0.f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        s = gsum<64>(s);
+        if (lane == 0) *A.loss += s * A.inv_count + A.margin;
+    }
+}
 
 template <int G, int VEC, int KCH>
 __global__ __launch_bounds__(256) void k_apply(ApplyParams A) {
@@ -500,10 +733,7 @@ __global__ __launch_bounds__(256) void k_apply(ApplyParams A) {
     constexpr int GPB = 256 / G;
     const int lane = threadIdx.x % G;
     int64_t row = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
-    if (blockIdx.x == 0 && threadIdx.x < 64) {
-        if (A.states) advance_states(A.states, A.threads, A.bs, A.dpp, (int)threadIdx.x);
-        if (A.loss && threadIdx.x == 0) *A.loss += A.margin;
-    }
+    if (blockIdx.x == 0 && threadIdx.x < 64) apply_block0(A);
     int ti = 0;
     while (ti < A.ntab && row >= A.t[ti].rows) {
         row -= A.t[ti].rows;
@@ -577,10 +807,7 @@ __global__ __launch_bounds__(256) void k_apply_rows(ApplyParams A) {
     constexpr int GPB = 256 / G;
     const int lane = threadIdx.x % G;
     const int64_t gi = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
-    if (blockIdx.x == 0 && threadIdx.x < 64) {
-        if (A.states) advance_states(A.states, A.threads, A.bs, A.dpp, (int)threadIdx.x);
-        if (A.loss && threadIdx.x == 0) *A.loss += A.margin;
-    }
+    if (blockIdx.x == 0 && threadIdx.x < 64) apply_block0(A);
     const int D = (int)A.dim;
     int ti[RPW];
     int64_t row[RPW];
@@ -938,6 +1165,15 @@ bool shape_supported(int64_t dim) {
     return a && b;
 }
 
+// k_step_csr instances (G, KCH, NCH), float4 lanes
+#define PT_CSTEPS(X)                                                                                   \
+    X(2, 1, 8, 1) X(4, 1, 8, 1) X(8, 1, 8, 1) X(16, 1, 8, 1) X(32, 1, 8, 1) X(64, 1, 8, 1)                \
+    X(2, 1, 4, 1) X(4, 1, 4, 1) X(8, 1, 4, 1) X(16, 1, 4, 1) X(32, 1, 4, 1) X(64, 1, 4, 1)                \
+    X(4, 1, 8, 2) X(8, 1, 8, 2) X(16, 1, 8, 2) X(32, 1, 8, 2) X(64, 1, 8, 2)                             \
+    X(4, 1, 8, 4) X(8, 1, 8, 4) X(16, 1, 8, 4) X(32, 1, 8, 4) X(64, 1, 8, 4)                             \
+    X(4, 1, 4, 4) X(8, 1, 4, 4) X(16, 1, 4, 4) X(32, 1, 4, 4) X(64, 1, 4, 4)                             \
+    X(64, 2, 4, 1) X(64, 2, 4, 2) X(64, 2, 4, 4) X(64, 3, 4, 1) X(64, 3, 4, 4) X(64, 4, 4, 1) X(64, 4, 4, 4)
+
 hipError_t launch_sample(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                          int bern, int filter, int64_t *h, int64_t *t, int64_t *r, float *y, hipStream_t st) {
     if (bs <= 0) return hipSuccess;
@@ -976,7 +1212,7 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
                        int filter, const int64_t *bh, const int64_t *bt, const int64_t *br, const StepWorkspace &W,
                        float *loss, hipStream_t st, const CsrWork *csr) {
     if (P.batch_size <= 0) return hipSuccess;
-    dev::GlobalSink sink{W.gent, W.grel, W.gnorm, W.fent, W.frel, W.fnorm};
+    dev::GlobalSink sink{W.gent, W.grel, W.gnorm, W.fent, W.frel, W.fnorm, W.lpart};
     if (bh) {   // external batch
         const Shape s = pick_shape(P.dim);
         const int64_t gpb = 256 / s.G;
@@ -992,6 +1228,43 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
         PT_SHAPES(PT_STEP)
 #undef PT_STEP
         return hipErrorInvalidValue;
+    }
+    // TransE on a counting-sort batch with float4 rows: one lane group per positive (k_step_csr);
+    // PT_STEP_OLD=1 keeps the sub-group kernel below, PT_STEP_G / PT_STEP_NCH pick the shape
+    static const bool old_step = [] {
+        const char *v = getenv("PT_STEP_OLD");
+        return v && atoi(v) != 0;
+    }();
+    // (raw-buffer offsets must fit in 31 bits)
+    const int64_t lim = int64_t(1) << 31;
+    const bool fits31 = (P.ent_total + P.rel_total + P.batch_size * P.neg) * P.dim * 4 < lim;
+    if (csr && P.model == 0 && P.dim % 4 == 0 && fits31 && !old_step) {
+        const int64_t chunks = P.dim / 4;
+        int G = 2;
+        while (G < chunks && G < 64) G <<= 1;
+        if (const char *v = getenv("PT_STEP_G")) G = atoi(v);
+        const int KCH = (int)((chunks + G - 1) / G);
+        // split a positive's negatives over S lane groups of one block (more waves in flight: the step
+        // is latency-bound when one group walks all negatives)
+        int S = 1;
+        while (S < 4 && S * 2 <= 256 / G && P.neg >= 6 * S * 2) S *= 2;
+        if (const char *v = getenv("PT_STEP_S")) S = atoi(v);
+        const int64_t nper = (P.neg + S - 1) / S;
+        int nch = KCH == 1 ? 8 : 4;
+        if (nper <= 4 && KCH == 1) nch = 4;
+        if (const char *v = getenv("PT_STEP_NCH")) nch = atoi(v);
+        const int64_t ppb = 256 / G / S;
+        const dim3 grid((unsigned)((P.batch_size + ppb - 1) / ppb)), block(256);
+#define PT_CSTEP(G_, K_, N_, S_)                                                                       \
+        if (G == G_ && KCH == K_ && nch == N_ && S == S_) {                                          \
+            if (P.p_norm == 1)                                                                       \
+                hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 1>), grid, block, 0, st, P, sink, *csr); \
+            else                                                                                     \
+                hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 2>), grid, block, 0, st, P, sink, *csr); \
+            return hipGetLastError();                                                                \
+        }
+        PT_CSTEPS(PT_CSTEP)
+#undef PT_CSTEP
     }
     // row layout: one float per lane (each wave instruction moves 64 contiguous floats), or float4
     // lanes when PT_STEP_VEC=4 and D % 4 == 0 (measured slower on the C2 step: 48.9 vs 40.6 us)
@@ -1067,7 +1340,9 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
     A.bs = bs;
     A.dpp = dpp;
     A.loss = loss;
+    A.lpart = W.lpart;
     A.margin = P.margin;
+    A.inv_count = P.inv_count;
     int64_t rows = 0;
     for (int i = 0; i < A.ntab; ++i) rows += A.t[i].rows;
     const int64_t gpb = 256 / s.G;
