@@ -1,0 +1,409 @@
+// HIP kernels of the optimizer apply pass (sparse SGD / Adagrad rows) for gfx950.
+//
+// Layout and mapping
+//  * Tables are row-major fp32 [rows][dim]. A "lane group" of G lanes (G | 64, a power of two) owns one
+//    row-sized vector: lane l holds chunks c = k*G + l (k < KCH) of VEC consecutive floats, so a row is
+//    read with fully coalesced 16-B (VEC=4) or 4-B (VEC=1) accesses and every reduction is a shuffle
+//    butterfly inside the group. One positive triple and all its negatives belong to one group.
+//  * This is gather/axpy work (no dense contraction): the roofline is HBM / Infinity-Cache bandwidth
+//    and the memory-side float-atomic rate, not MFMA.
+//
+// Semantics (all cited in DESIGN.md): sampler = Base.cpp:185-310 + Corrupt.h:9-105 + Random.h:18-29;
+// forward = TransE.py:46-74 / TransH.py:52-93; loss = MarginLoss.py:24-28 via NegativeSampling.py:13-31;
+// backward = torch autograd of those ops (normalize Jacobian, sign / v/||v|| norm derivatives, maximum
+// tie -> half); update = torch.optim.SGD / Adagrad (eps 1e-10) as built in Trainer.py:62-88, applied
+// only to rows with a nonzero gradient (identical to the dense update).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "device.h"
+#include "graph.h"
+#include "kernels.h"
+#include "rng.h"
+
+namespace pt {
+namespace dev {
+using pt::CsrWork;
+
+// Sparse apply: for every touched row finish the gradient (normalize Jacobian of the pre-step row
+// when that table's gradient is in normalized space) and run SGD / Adagrad; then clear the row.
+struct ApplyTable {
+    float *w, *acc, *grad;
+    int *flag;
+    int64_t rows;
+    int jacobian;
+    const int *start;       // CSR of extra contribution rows (NULL: none): rows start[r] .. start[r+1]-1
+    const float *contrib;   // [n][dim]
+};
+struct ApplyParams {
+    ApplyTable t[3];
+    int ntab;
+    int64_t dim;
+    int opt;
+    float lr;
+    // sampler advance + loss (done by block 0)
+    uint64_t *states;
+    int64_t threads, bs, dpp;
+    float *loss;
+    const float *lpart;   // [bs] per-positive loss partials of the step
+    float margin, inv_count;
+};
+
+// block 0, first wave: advance the sampler streams and reduce the step's loss partials in a fixed
+// order: loss += inv_count * sum(lpart) + margin (MarginLoss.py:24-28)
+__device__ __forceinline__ void apply_block0(const ApplyParams &A) {
+    const int lane = (int)threadIdx.x;
+    if (A.states) advance_states(A.states, A.threads, A.bs, A.dpp, lane);
+    if (A.loss && A.lpart) {
+        float s = 0.f;
+        for (int64_t i0 = lane; i0 < A.bs; i0 += 64 * 8) {   // 8 independent loads in flight per lane
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = i0 + u * 64 < A.bs ? A.lpart[i0 + u * 64] : 0.f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        s = gsum<64>(s);
+        if (lane == 0) *A.loss += s * A.inv_count + A.margin;
+    }
+}
+
+template <int G, int VEC, int KCH>
+__global__ __launch_bounds__(256) void k_apply(ApplyParams A) {
+    using Vec = V<G, VEC, KCH>;
+    constexpr int GPB = 256 / G;
+    const int lane = threadIdx.x % G;
+    int64_t row = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    if (blockIdx.x == 0 && threadIdx.x < 64) apply_block0(A);
+    int ti = 0;
+    while (ti < A.ntab && row >= A.t[ti].rows) {
+        row -= A.t[ti].rows;
+        ++ti;
+    }
+    if (ti >= A.ntab) return;
+    const ApplyTable &T = A.t[ti];
+    const int flagged = T.flag[row];
+    int c0 = 0, c1 = 0;
+    if (T.start) {
+        c0 = T.start[row];
+        c1 = T.start[row + 1];
+    }
+    if (!flagged && c0 == c1) return;
+    const int D = (int)A.dim;
+    Vec x, gsum_, g;
+    vload(x, T.w + row * D, D, lane);
+    if (flagged) vload(gsum_, T.grad + row * D, D, lane); else vzero(gsum_);
+    // contributions of this step's corrupted-entity slots (counting-sort order)
+    int j = c0;
+    for (; j + 4 <= c1; j += 4) {
+        Vec c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) vload(c[u], T.contrib + (int64_t)(j + u) * D, D, lane);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) gsum_.x[i] += c[u].x[i];
+    }
+    for (; j < c1; ++j) {
+        Vec c;
+        vload(c, T.contrib + (int64_t)j * D, D, lane);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) gsum_.x[i] += c.x[i];
+    }
+    if (T.jacobian) {
+        const float n = sqrtf(vdot(x, x));
+        vnormalize_bwd(x, n, gsum_, g);
+    } else {
+        g = gsum_;
+    }
+    if (A.opt == 0) {
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) x.x[i] = x.x[i] + (-A.lr) * g.x[i];
+    } else {
+        Vec a;
+        vload(a, T.acc + row * D, D, lane);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            a.x[i] = a.x[i] + g.x[i] * g.x[i];
+            x.x[i] = x.x[i] + (-A.lr) * g.x[i] / (sqrtf(a.x[i]) + 1e-10f);
+        }
+        vstore(a, T.acc + row * D, D, lane);
+    }
+    vstore(x, T.w + row * D, D, lane);
+    if (flagged) {
+        Vec z;
+        vzero(z);
+        vstore(z, T.grad + row * D, D, lane);
+        if (lane == 0) T.flag[row] = 0;
+    }
+}
+
+// Apply pass with float4 rows and raw-buffer access (D % 4 == 0, offsets within 31 bits): one lane
+// group per table row. The row (and its Adagrad state) load is issued before the flag / bucket range
+// loads return; a bucket's contribution rows stream NC at a time with out-of-range offsets past its
+// end (the hardware returns zeros, so the adds need no branches), summed in bucket order after the
+// row's own gradient row.
+template <int G, int VEC, int KCH, int NC>
+__global__ __launch_bounds__(256) void k_apply_buf(ApplyParams A) {
+    using Vec = V<G, VEC, KCH>;
+    constexpr int GPB = 256 / G;
+    const int lane = threadIdx.x % G;
+    int64_t row = uni<G>((int32_t)(blockIdx.x * GPB + threadIdx.x / G));   // scalar at G = 64
+    if (blockIdx.x == 0 && threadIdx.x < 64) apply_block0(A);
+    int ti = 0;
+    while (ti < A.ntab && row >= A.t[ti].rows) {
+        row -= A.t[ti].rows;
+        ++ti;
+    }
+    if (ti >= A.ntab) return;
+    const ApplyTable &T = A.t[ti];
+    const int D = (int)A.dim;
+    const uint32_t rowb = (uint32_t)D * 4u;
+    const uint32_t tbytes = (uint32_t)T.rows * rowb;
+    const auto w_rs = make_rsrc(T.w, tbytes);
+    Vec x, g, a;
+    bload(x, w_rs, (uint32_t)row * rowb, D, lane);
+    if (A.opt != 0) bload(a, make_rsrc(T.acc, tbytes), (uint32_t)row * rowb, D, lane);
+    const int flagged = T.flag[row];
+    int c0 = 0, c1 = 0;
+    if (T.start) {
+        c0 = T.start[row];
+        c1 = T.start[row + 1];
+    }
+    if (!flagged && c0 == c1) return;
+    const auto g_rs = make_rsrc(T.grad, tbytes);
+    bload(g, g_rs, flagged ? (uint32_t)row * rowb : kOob, D, lane);
+    if (c1 > c0) {
+        const auto c_rs = make_rsrc(T.contrib, (uint32_t)c1 * rowb);
+        for (int j0 = c0; j0 < c1; j0 += NC) {
+            Vec c[NC];
+#pragma unroll
+            for (int u = 0; u < NC; ++u) bload(c[u], c_rs, j0 + u < c1 ? (uint32_t)(j0 + u) * rowb : kOob, D, lane);
+#pragma unroll
+            for (int u = 0; u < NC; ++u)
+#pragma unroll
+                for (int i = 0; i < Vec::N; ++i) g.x[i] += c[u].x[i];
+        }
+    }
+    Vec gg;
+    if (T.jacobian) {
+        const float n = sqrtf(vdot(x, x));
+        vnormalize_bwd(x, n, g, gg);
+    } else {
+        gg = g;
+    }
+    if (A.opt == 0) {
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) x.x[i] = x.x[i] + (-A.lr) * gg.x[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            a.x[i] = a.x[i] + gg.x[i] * gg.x[i];
+            x.x[i] = x.x[i] + (-A.lr) * gg.x[i] / (sqrtf(a.x[i]) + 1e-10f);
+        }
+        bstore(a, make_rsrc(T.acc, tbytes), (uint32_t)row * rowb, D, lane);
+    }
+    bstore(x, w_rs, (uint32_t)row * rowb, D, lane);
+    if (flagged) {
+        Vec z;
+        vzero(z);
+        bstore(z, g_rs, (uint32_t)row * rowb, D, lane);
+        if (lane == 0) T.flag[row] = 0;
+    }
+}
+
+// Apply pass, RPW consecutive rows per lane group with all their loads in flight together (the
+// one-row-per-group form is a chain of two dependent memory round trips per row). Consecutive entity
+// rows own consecutive counting-sort contribution ranges, so a group streams ONE contiguous range
+// [start[r0], start[r0 + RPW]) and adds each contribution to its row.
+template <int G, int VEC, int KCH, int RPW>
+__global__ __launch_bounds__(256) void k_apply_rows(ApplyParams A) {
+    using Vec = V<G, VEC, KCH>;
+    constexpr int GPB = 256 / G;
+    const int lane = threadIdx.x % G;
+    const int64_t gi = (int64_t)blockIdx.x * GPB + threadIdx.x / G;
+    if (blockIdx.x == 0 && threadIdx.x < 64) apply_block0(A);
+    const int D = (int)A.dim;
+    int ti[RPW];
+    int64_t row[RPW];
+    int flag[RPW], c0[RPW], c1[RPW];
+    bool live[RPW];
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        int64_t r = gi * RPW + u;
+        int t = 0;
+        while (t < A.ntab && r >= A.t[t].rows) {
+            r -= A.t[t].rows;
+            ++t;
+        }
+        ti[u] = t;
+        row[u] = r;
+        flag[u] = 0;
+        c0[u] = c1[u] = 0;
+        if (t < A.ntab) {
+            flag[u] = A.t[t].flag[r];
+            if (A.t[t].start) {
+                c0[u] = A.t[t].start[r];
+                c1[u] = A.t[t].start[r + 1];
+            }
+        }
+        live[u] = t < A.ntab && (flag[u] || c0[u] != c1[u]);
+    }
+    Vec x[RPW], g[RPW], a[RPW];
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        if (!live[u]) continue;
+        const ApplyTable &T = A.t[ti[u]];
+        vload(x[u], T.w + row[u] * D, D, lane);
+        if (flag[u]) vload(g[u], T.grad + row[u] * D, D, lane); else vzero(g[u]);
+        if (A.opt != 0) vload(a[u], T.acc + row[u] * D, D, lane);
+    }
+    // the group's contribution range (entity table rows only carry contributions)
+    int cs = 0, ce = 0;
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        if (c0[u] == c1[u]) continue;
+        if (!any) cs = c0[u];
+        ce = c1[u];
+        any = true;
+    }
+    if (any) {
+        const float *contrib = A.t[0].contrib;
+        for (int j = cs; j < ce; j += 4) {
+            Vec c[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (j + q < ce) vload(c[q], contrib + (int64_t)(j + q) * D, D, lane);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (j + q >= ce) break;
+#pragma unroll
+                for (int u = 0; u < RPW; ++u) {
+                    if (j + q >= c0[u] && j + q < c1[u]) {
+#pragma unroll
+                        for (int i = 0; i < Vec::N; ++i) g[u].x[i] += c[q].x[i];
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        if (!live[u]) continue;
+        const ApplyTable &T = A.t[ti[u]];
+        Vec gg;
+        if (T.jacobian) {
+            const float n = sqrtf(vdot(x[u], x[u]));
+            vnormalize_bwd(x[u], n, g[u], gg);
+        } else {
+            gg = g[u];
+        }
+        if (A.opt == 0) {
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) x[u].x[i] = x[u].x[i] + (-A.lr) * gg.x[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) {
+                a[u].x[i] = a[u].x[i] + gg.x[i] * gg.x[i];
+                x[u].x[i] = x[u].x[i] + (-A.lr) * gg.x[i] / (sqrtf(a[u].x[i]) + 1e-10f);
+            }
+            vstore(a[u], T.acc + row[u] * D, D, lane);
+        }
+        vstore(x[u], T.w + row[u] * D, D, lane);
+        if (flag[u]) {
+            Vec z;
+            vzero(z);
+            vstore(z, T.grad + row[u] * D, D, lane);
+            if (lane == 0) T.flag[row[u]] = 0;
+        }
+    }
+}
+
+}  // namespace dev
+
+// ==================================================================== host launchers ===========
+hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *states, int64_t threads, int64_t bs,
+                        int64_t dpp, float *loss, hipStream_t st, const CsrWork *csr) {
+    const Shape s = pick_shape(P.dim);
+    dev::ApplyParams A{};
+    A.ntab = 0;
+    const int ent_j = P.model == 0 && P.norm_flag;
+    A.t[A.ntab++] = dev::ApplyTable{P.ent, P.ent_acc, W.gent, W.fent, P.ent_total, ent_j,
+                                    csr ? csr->start : nullptr, csr ? csr->contrib : nullptr};
+    A.t[A.ntab++] = dev::ApplyTable{P.rel, P.rel_acc, W.grel, W.frel, P.rel_total, P.norm_flag, nullptr, nullptr};
+    if (P.model == 1)
+        A.t[A.ntab++] = dev::ApplyTable{P.normv, P.norm_acc, W.gnorm, W.fnorm, P.rel_total, 1, nullptr, nullptr};
+    A.dim = P.dim;
+    A.opt = P.opt;
+    A.lr = P.lr;
+    A.states = states;
+    A.threads = threads;
+    A.bs = bs;
+    A.dpp = dpp;
+    A.loss = loss;
+    A.lpart = W.lpart;
+    A.margin = P.margin;
+    A.inv_count = P.inv_count;
+    int64_t rows = 0;
+    for (int i = 0; i < A.ntab; ++i) rows += A.t[i].rows;
+    // float4 rows through raw buffers (PT_APPLY_OLD=1 keeps the kernels below)
+    static const bool old_apply = [] {
+        const char *v = getenv("PT_APPLY_OLD");
+        return v && atoi(v) != 0;
+    }();
+    int64_t con_rows = 0;
+    if (csr) con_rows = P.batch_size * P.neg;
+    const bool fits31 = (P.ent_total + P.rel_total + con_rows) * P.dim * 4 < (int64_t(1) << 31);
+    if (P.dim % 4 == 0 && fits31 && !old_apply) {
+        const int64_t chunks = P.dim / 4;
+        int G = 2;
+        while (G < chunks && G < 64) G <<= 1;
+        const int KCH = (int)((chunks + G - 1) / G);
+        int nc = 4;
+        if (const char *v = getenv("PT_APPLY_NC")) nc = atoi(v);
+        const int64_t gpb4 = 256 / G;
+        const dim3 grid((unsigned)((rows + gpb4 - 1) / gpb4)), block(256);
+#define PT_APPLYB(G_, K_, N_)                                                              \
+        if (G == G_ && KCH == K_ && nc == N_) {                                           \
+            hipLaunchKernelGGL((dev::k_apply_buf<G_, 4, K_, N_>), grid, block, 0, st, A);   \
+            return hipGetLastError();                                                     \
+        }
+        PT_APPLYB(2, 1, 4) PT_APPLYB(4, 1, 4) PT_APPLYB(8, 1, 4) PT_APPLYB(16, 1, 4) PT_APPLYB(32, 1, 4)
+        PT_APPLYB(64, 1, 4) PT_APPLYB(64, 1, 8) PT_APPLYB(64, 1, 2) PT_APPLYB(64, 2, 4) PT_APPLYB(64, 3, 4)
+        PT_APPLYB(64, 4, 4)
+#undef PT_APPLYB
+    }
+    const int64_t gpb = 256 / s.G;
+    // PT_APPLY_RPW=2|4: several rows per lane group with one contribution stream (measured slower on
+    // C2: 20.4 / 22.0 us vs 16.8 us for one row per group, which stays the default)
+    const char *rpw_env = getenv("PT_APPLY_RPW");
+    const int rpw = rpw_env ? atoi(rpw_env) : 1;
+    if (rpw == 4 || rpw == 2) {
+        const int64_t groups = (rows + rpw - 1) / rpw;
+        const dim3 grid((unsigned)((groups + gpb - 1) / gpb)), block(256);
+#define PT_APPLY4(G_, V_, K_)                                                                 \
+        if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                      \
+            if (rpw == 4)                                                                   \
+                hipLaunchKernelGGL((dev::k_apply_rows<G_, V_, K_, 4>), grid, block, 0, st, A); \
+            else                                                                            \
+                hipLaunchKernelGGL((dev::k_apply_rows<G_, V_, K_, 2>), grid, block, 0, st, A); \
+            return hipGetLastError();                                                       \
+        }
+        PT_SHAPES(PT_APPLY4)
+#undef PT_APPLY4
+    }
+    const dim3 grid((unsigned)((rows + gpb - 1) / gpb)), block(256);
+#define PT_APPLY(G_, V_, K_)                                                                  \
+    if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                          \
+        hipLaunchKernelGGL((dev::k_apply<G_, V_, K_>), grid, block, 0, st, A);              \
+        return hipGetLastError();                                                           \
+    }
+    PT_SHAPES(PT_APPLY)
+#undef PT_APPLY
+    return hipErrorInvalidValue;
+}
+
+}  // namespace pt
