@@ -456,7 +456,7 @@ def main():
     tl = torch.zeros(n_t, device=dev)
     _native.check(L.pt_trainer_run_timed(tr._native, sampler, bs, neg, bern, filt, n_t, _native.ptr(tl), ms4,
                                          _native.stream()))
-    names = ["k_sample_csr", "k_scan_counts", "k_step_sampled", "k_apply"]
+    names = ["k_sample_csr", "k_scan_counts", "k_step_csr", "k_apply_buf"]
     per_kernel = {n: float(v) for n, v in zip(names, ms4) if v > 0}
     bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
     achieved = bytes_step / (sum(per_kernel.values()) * 1e-3) / 1e9

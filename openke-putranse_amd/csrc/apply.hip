@@ -145,72 +145,102 @@ __global__ __launch_bounds__(256) void k_apply(ApplyParams A) {
 // loads return; a bucket's contribution rows stream NC at a time with out-of-range offsets past its
 // end (the hardware returns zeros, so the adds need no branches), summed in bucket order after the
 // row's own gradient row.
-template <int G, int VEC, int KCH, int NC>
+template <int G, int VEC, int KCH, int NC, int RPW>
 __global__ __launch_bounds__(256) void k_apply_buf(ApplyParams A) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = 256 / G;
     const int lane = threadIdx.x % G;
-    int64_t row = uni<G>((int32_t)(blockIdx.x * GPB + threadIdx.x / G));   // scalar at G = 64
+    const int64_t gi = uni<G>((int32_t)(blockIdx.x * GPB + threadIdx.x / G));   // scalar at G = 64
     if (blockIdx.x == 0 && threadIdx.x < 64) apply_block0(A);
-    int ti = 0;
-    while (ti < A.ntab && row >= A.t[ti].rows) {
-        row -= A.t[ti].rows;
-        ++ti;
-    }
-    if (ti >= A.ntab) return;
-    const ApplyTable &T = A.t[ti];
     const int D = (int)A.dim;
     const uint32_t rowb = (uint32_t)D * 4u;
-    const uint32_t tbytes = (uint32_t)T.rows * rowb;
-    const auto w_rs = make_rsrc(T.w, tbytes);
-    Vec x, g, a;
-    bload(x, w_rs, (uint32_t)row * rowb, D, lane);
-    if (A.opt != 0) bload(a, make_rsrc(T.acc, tbytes), (uint32_t)row * rowb, D, lane);
-    const int flagged = T.flag[row];
-    int c0 = 0, c1 = 0;
-    if (T.start) {
-        c0 = T.start[row];
-        c1 = T.start[row + 1];
+    // RPW consecutive rows per group, every load of all of them in flight together
+    int ti[RPW], flag[RPW], c0[RPW], c1[RPW];
+    int64_t row[RPW];
+    bool live[RPW];
+    Vec x[RPW], g[RPW], a[RPW];
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        int64_t r = gi * RPW + u;
+        int t = 0;
+        while (t < A.ntab && r >= A.t[t].rows) {
+            r -= A.t[t].rows;
+            ++t;
+        }
+        ti[u] = t;
+        row[u] = r;
+        live[u] = t < A.ntab;
+        flag[u] = 0;
+        c0[u] = c1[u] = 0;
     }
-    if (!flagged && c0 == c1) return;
-    const auto g_rs = make_rsrc(T.grad, tbytes);
-    bload(g, g_rs, flagged ? (uint32_t)row * rowb : kOob, D, lane);
-    if (c1 > c0) {
-        const auto c_rs = make_rsrc(T.contrib, (uint32_t)c1 * rowb);
-        for (int j0 = c0; j0 < c1; j0 += NC) {
-            Vec c[NC];
 #pragma unroll
-            for (int u = 0; u < NC; ++u) bload(c[u], c_rs, j0 + u < c1 ? (uint32_t)(j0 + u) * rowb : kOob, D, lane);
-#pragma unroll
-            for (int u = 0; u < NC; ++u)
-#pragma unroll
-                for (int i = 0; i < Vec::N; ++i) g.x[i] += c[u].x[i];
+    for (int u = 0; u < RPW; ++u) {
+        if (!live[u]) continue;
+        const ApplyTable &T = A.t[ti[u]];
+        const uint32_t tb = (uint32_t)T.rows * rowb;
+        bload(x[u], make_rsrc(T.w, tb), (uint32_t)row[u] * rowb, D, lane);
+        if (A.opt != 0) bload(a[u], make_rsrc(T.acc, tb), (uint32_t)row[u] * rowb, D, lane);
+        flag[u] = T.flag[row[u]];
+        if (T.start) {
+            c0[u] = T.start[row[u]];
+            c1[u] = T.start[row[u] + 1];
         }
     }
-    Vec gg;
-    if (T.jacobian) {
-        const float n = sqrtf(vdot(x, x));
-        vnormalize_bwd(x, n, g, gg);
-    } else {
-        gg = g;
+    int len = 0;
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        if (!live[u]) continue;
+        const ApplyTable &T = A.t[ti[u]];
+        bload(g[u], make_rsrc(T.grad, (uint32_t)T.rows * rowb), flag[u] ? (uint32_t)row[u] * rowb : kOob, D, lane);
+        len = c1[u] - c0[u] > len ? c1[u] - c0[u] : len;
     }
-    if (A.opt == 0) {
+    // contribution rows (entity table only): the rows' buckets streamed side by side, NC per row at a
+    // time, out-of-range past each bucket's end (zeros), summed in bucket order
+    const auto c_rs = make_rsrc(A.t[0].contrib, 0x7fffffffu);
+    for (int j = 0; j < len; j += NC) {
+        Vec c[RPW][NC];
 #pragma unroll
-        for (int i = 0; i < Vec::N; ++i) x.x[i] = x.x[i] + (-A.lr) * gg.x[i];
-    } else {
+        for (int u = 0; u < RPW; ++u)
 #pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            a.x[i] = a.x[i] + gg.x[i] * gg.x[i];
-            x.x[i] = x.x[i] + (-A.lr) * gg.x[i] / (sqrtf(a.x[i]) + 1e-10f);
+            for (int q = 0; q < NC; ++q)
+                bload(c[u][q], c_rs, c0[u] + j + q < c1[u] ? (uint32_t)(c0[u] + j + q) * rowb : kOob, D, lane);
+#pragma unroll
+        for (int u = 0; u < RPW; ++u)
+#pragma unroll
+            for (int q = 0; q < NC; ++q)
+#pragma unroll
+                for (int i = 0; i < Vec::N; ++i) g[u].x[i] += c[u][q].x[i];
+    }
+#pragma unroll
+    for (int u = 0; u < RPW; ++u) {
+        if (!live[u] || (!flag[u] && c0[u] == c1[u])) continue;   // untouched row: unchanged
+        const ApplyTable &T = A.t[ti[u]];
+        const uint32_t tb = (uint32_t)T.rows * rowb;
+        Vec gg;
+        if (T.jacobian) {
+            const float n = sqrtf(vdot(x[u], x[u]));
+            vnormalize_bwd(x[u], n, g[u], gg);
+        } else {
+            gg = g[u];
         }
-        bstore(a, make_rsrc(T.acc, tbytes), (uint32_t)row * rowb, D, lane);
-    }
-    bstore(x, w_rs, (uint32_t)row * rowb, D, lane);
-    if (flagged) {
-        Vec z;
-        vzero(z);
-        bstore(z, g_rs, (uint32_t)row * rowb, D, lane);
-        if (lane == 0) T.flag[row] = 0;
+        if (A.opt == 0) {
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) x[u].x[i] = x[u].x[i] + (-A.lr) * gg.x[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) {
+                a[u].x[i] = a[u].x[i] + gg.x[i] * gg.x[i];
+                x[u].x[i] = x[u].x[i] + (-A.lr) * gg.x[i] / (sqrtf(a[u].x[i]) + 1e-10f);
+            }
+            bstore(a[u], make_rsrc(T.acc, tb), (uint32_t)row[u] * rowb, D, lane);
+        }
+        bstore(x[u], make_rsrc(T.w, tb), (uint32_t)row[u] * rowb, D, lane);
+        if (flag[u]) {
+            Vec z;
+            vzero(z);
+            bstore(z, make_rsrc(T.grad, tb), (uint32_t)row[u] * rowb, D, lane);
+            if (lane == 0) T.flag[row[u]] = 0;
+        }
     }
 }
 
@@ -362,18 +392,21 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
         int G = 2;
         while (G < chunks && G < 64) G <<= 1;
         const int KCH = (int)((chunks + G - 1) / G);
-        int nc = 4;
+        int nc = 4, rpw = 1;
         if (const char *v = getenv("PT_APPLY_NC")) nc = atoi(v);
+        if (const char *v = getenv("PT_APPLY_RPW")) rpw = atoi(v);
         const int64_t gpb4 = 256 / G;
-        const dim3 grid((unsigned)((rows + gpb4 - 1) / gpb4)), block(256);
-#define PT_APPLYB(G_, K_, N_)                                                              \
-        if (G == G_ && KCH == K_ && nc == N_) {                                           \
-            hipLaunchKernelGGL((dev::k_apply_buf<G_, 4, K_, N_>), grid, block, 0, st, A);   \
-            return hipGetLastError();                                                     \
+        const int64_t groups = (rows + rpw - 1) / rpw;
+        const dim3 grid((unsigned)((groups + gpb4 - 1) / gpb4)), block(256);
+#define PT_APPLYB(G_, K_, N_, R_)                                                              \
+        if (G == G_ && KCH == K_ && nc == N_ && rpw == R_) {                                  \
+            hipLaunchKernelGGL((dev::k_apply_buf<G_, 4, K_, N_, R_>), grid, block, 0, st, A);   \
+            return hipGetLastError();                                                         \
         }
-        PT_APPLYB(2, 1, 4) PT_APPLYB(4, 1, 4) PT_APPLYB(8, 1, 4) PT_APPLYB(16, 1, 4) PT_APPLYB(32, 1, 4)
-        PT_APPLYB(64, 1, 4) PT_APPLYB(64, 1, 8) PT_APPLYB(64, 1, 2) PT_APPLYB(64, 2, 4) PT_APPLYB(64, 3, 4)
-        PT_APPLYB(64, 4, 4)
+        PT_APPLYB(2, 1, 4, 1) PT_APPLYB(4, 1, 4, 1) PT_APPLYB(8, 1, 4, 1) PT_APPLYB(16, 1, 4, 1)
+        PT_APPLYB(32, 1, 4, 1) PT_APPLYB(64, 1, 4, 1) PT_APPLYB(64, 2, 4, 1) PT_APPLYB(64, 3, 4, 1)
+        PT_APPLYB(64, 4, 4, 1) PT_APPLYB(64, 1, 2, 1) PT_APPLYB(64, 1, 4, 2) PT_APPLYB(64, 1, 2, 2)
+        PT_APPLYB(64, 1, 2, 4) PT_APPLYB(64, 1, 1, 4)
 #undef PT_APPLYB
     }
     const int64_t gpb = 256 / s.G;

@@ -371,8 +371,8 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
     const int nper = (neg + S - 1) / S;
     const int k_lo = sub * nper < neg ? sub * nper : neg;
     const int k_hi = k_lo + nper < neg ? k_lo + nper : neg;
-    Vec At, Ah, vpos;
-    vzero(At); vzero(Ah); vzero(vpos);
+    Vec At, Ah, rh, th, bt;   // (v+ = bt - th is re-formed where needed: fewer live registers)
+    vzero(At); vzero(Ah); vzero(rh); vzero(th); vzero(bt);
     float csum = 0.f, lsum = 0.f, ps = 0.f;
     int32_t hp = 0, rp = 0, tp = 0;
     if (active) {
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
         };
         if (w0 < wend) load_chunk(EA, w0);
         // ---- positive forward
-        Vec hh, rh, th, bt;
+        Vec hh, vpos;
         if (nf) {
             vnormalize<true>(H, hh);
             vnormalize<true>(Rr, rh);
@@ -509,7 +509,9 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
     if (!active) return;
     if (lane == 0 && sink.lpart) sink.lpart[b] = lsum;
     if (uni<G>(csum) == 0.f) return;   // no active pair: every accumulator is zero
-    Vec gv, aH, aR, aT;
+    Vec gv, aH, aR, aT, vpos;
+#pragma unroll
+    for (int i = 0; i < Vec::N; ++i) vpos.x[i] = bt.x[i] - th.x[i];
     vpnorm_bwd<true>(vpos, ps, p, csum, gv);
 #pragma unroll
     for (int i = 0; i < Vec::N; ++i) {
