@@ -107,6 +107,15 @@ int desc_to_params(const pt_model_desc *m, pt::StepParams &P) {
     return PT_OK;
 }
 
+// negatives at or above this count take the counting-sort path (PT_CSR=0/1 overrides)
+bool use_csr(int64_t neg) {
+    static int forced = [] {
+        const char *v = getenv("PT_CSR");
+        return v ? atoi(v) : -1;
+    }();
+    return forced >= 0 ? forced != 0 : neg >= 4;
+}
+
 int check_step_args(const pt::StepParams &P, pt_sampler *s, int64_t bs, int64_t neg, const int64_t *bh) {
     PT_CHECK(bs > 0 && neg > 0, PT_EINVAL, "batch_size and neg_ent must be positive");
     if (!bh) {
@@ -114,8 +123,9 @@ int check_step_args(const pt::StepParams &P, pt_sampler *s, int64_t bs, int64_t 
         PT_CHECK(s->g->ent_total <= P.ent_total && s->g->rel_total <= P.rel_total, PT_EINVAL,
                  "graph ids exceed the model tables");
         PT_CHECK(s->g->ent_total > 1, PT_EINVAL, "graph needs at least two entities");
-        const int64_t gpb = 256;   // worst case groups per block (G = 2 -> 128) * 2 safety
-        PT_CHECK((size_t)gpb * (size_t)neg * 8 <= 64 * 1024, PT_ENOTSUP, "neg_ent too large for the LDS draw buffer");
+        pt::StepParams Q = P;
+        Q.batch_size = bs;
+        PT_CHECK(pt::step_fits(Q, neg, use_csr(neg)), PT_ENOTSUP, "neg_ent too large for the LDS draw buffer");
     }
     return PT_OK;
 }
@@ -248,14 +258,6 @@ extern "C" int pt_trainer_update_desc(pt_trainer *t, const pt_model_desc *m) {
     return PT_OK;
 }
 
-// negatives at or above this count take the counting-sort path (PT_CSR=0/1 overrides)
-static bool use_csr(int64_t neg) {
-    static int forced = [] {
-        const char *v = getenv("PT_CSR");
-        return v ? atoi(v) : -1;
-    }();
-    return forced >= 0 ? forced != 0 : neg >= 4;
-}
 
 static const int64_t kCsrChunk = 256;   // steps pre-sampled per sampling/scan launch pair
 

@@ -97,6 +97,7 @@ hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64
                              int bern, int filter, int64_t calls, const CsrWork &w, hipStream_t st);
 hipError_t launch_scan_counts(const CsrWork &w, int64_t n, int64_t calls, uint64_t *states, int64_t threads,
                               int64_t bs, int64_t dpp, hipStream_t st);
+bool step_fits(const StepParams &P, int64_t neg, bool csr);
 hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t *states, int64_t threads, int bern,
                        int filter, const int64_t *bh, const int64_t *bt, const int64_t *br, const StepWorkspace &W,
                        float *loss, hipStream_t st, const CsrWork *csr = nullptr);

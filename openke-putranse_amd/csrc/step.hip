@@ -401,7 +401,7 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
             for (int u = 0; u < NCH; ++u) {
                 const int kk = k0 + u < wend ? k0 + u : wend - 1;
                 const uint32_t e = (uint32_t)(gbcast<G>(rec, kk - w0) >> 1);
-                bload(E[u], ent_rs, e * rowb, D, lane);
+                bload(E[u], ent_rs, (P.dbg & 4) ? kOob : e * rowb, D, lane);
             }
         };
         if (w0 < wend) load_chunk(EA, w0);
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
                 // slot gradient d loss / d e-hat: -g for a corrupted tail, +g for a corrupted head
                 // (g = dL/dv); an inactive pair stores zeros (the reserved slot must be defined)
                 vpnorm_bwd<true>(vk, ns, p, tail_side ? c : -c, gs);
-                bstore(gs, con_rs, slot, D, lane);
+                bstore(gs, con_rs, (P.dbg & 1) ? kOob : slot, D, lane);
                 if (tail_side) {
 #pragma unroll
                     for (int i = 0; i < Vec::N; ++i) At.x[i] -= gs.x[i];
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
     }
     if (!active) return;
     if (lane == 0 && sink.lpart) sink.lpart[b] = lsum;
-    if (uni<G>(csum) == 0.f) return;   // no active pair: every accumulator is zero
+    if (uni<G>(csum) == 0.f || (P.dbg & 2)) return;   // no active pair: every accumulator is zero
     Vec gv, aH, aR, aT, vpos;
 #pragma unroll
     for (int i = 0; i < Vec::N; ++i) vpos.x[i] = bt.x[i] - th.x[i];
@@ -584,8 +584,34 @@ int pick_nch(int64_t neg, int kch) {
     X(2, 1, 2, 1) X(4, 1, 2, 1) X(8, 1, 2, 1) X(16, 1, 2, 1) X(32, 1, 2, 1) X(64, 1, 2, 1)                \
     X(2, 1, 2, 2) X(4, 1, 2, 2) X(8, 1, 2, 2) X(16, 1, 2, 2) X(32, 1, 2, 2) X(64, 1, 2, 2)                \
     X(2, 1, 2, 4) X(4, 1, 2, 4) X(8, 1, 2, 4) X(16, 1, 2, 4) X(32, 1, 2, 4) X(64, 1, 2, 4)                \
-    X(64, 1, 4, 4) X(64, 1, 1, 4) X(64, 1, 2, 8) X(64, 1, 1, 8) X(64, 2, 2, 1) X(64, 2, 2, 2)             \
-    X(64, 2, 2, 4) X(64, 3, 2, 1) X(64, 3, 2, 4) X(64, 4, 2, 1) X(64, 4, 2, 4)
+    X(64, 1, 4, 4) X(64, 1, 1, 4) X(64, 2, 2, 1)             \
+    X(64, 2, 2, 2) X(64, 2, 2, 4) X(64, 3, 2, 1) X(64, 3, 2, 4) X(64, 4, 2, 1) X(64, 4, 2, 4)
+
+// TransE on the counting-sort path with float4 rows takes k_step_csr (PT_STEP_OLD=1: the sub-group
+// kernel k_step_sampled); raw-buffer byte offsets must fit in 31 bits
+static bool csr_fast_path(const StepParams &P) {
+    static const bool old_step = [] {
+        const char *v = getenv("PT_STEP_OLD");
+        return v && atoi(v) != 0;
+    }();
+    const int64_t lim = int64_t(1) << 31;
+    const bool fits31 = (P.ent_total + P.rel_total + P.batch_size * P.neg) * P.dim * 4 < lim;
+    return P.model == 0 && P.dim % 4 == 0 && fits31 && !old_step;
+}
+
+// whether launch_step can take this (P, neg) on the in-kernel-sampled path: k_step_csr has no LDS
+// limit on neg; the sub-group kernel keeps a block's negative records in LDS (64 KB)
+bool step_fits(const StepParams &P0, int64_t neg, bool csr) {
+    StepParams P = P0;
+    P.neg = neg;
+    if (csr && csr_fast_path(P)) return true;
+    const Shape s = pick_shape(P.dim, false);
+    const int S = (neg >= 8 && 256 / s.G >= 4) ? 4 : 1;
+    const int64_t gpb = 256 / s.G, ppb = gpb / S;
+    size_t lds = (size_t)ppb * (size_t)neg * sizeof(int64_t) * (csr ? 2 : 1);
+    if (S > 1) lds += sizeof(float) * ((size_t)gpb * 4 * s.KCH * s.G * s.VEC + (size_t)gpb * 2);
+    return lds <= 64 * 1024;
+}
 
 hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t *states, int64_t threads, int bern,
                        int filter, const int64_t *bh, const int64_t *bt, const int64_t *br, const StepWorkspace &W,
@@ -608,16 +634,9 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
 #undef PT_STEP
         return hipErrorInvalidValue;
     }
-    // TransE on a counting-sort batch with float4 rows: one lane group per positive (k_step_csr);
-    // PT_STEP_OLD=1 keeps the sub-group kernel below, PT_STEP_G / PT_STEP_NCH pick the shape
-    static const bool old_step = [] {
-        const char *v = getenv("PT_STEP_OLD");
-        return v && atoi(v) != 0;
-    }();
-    // (raw-buffer offsets must fit in 31 bits)
-    const int64_t lim = int64_t(1) << 31;
-    const bool fits31 = (P.ent_total + P.rel_total + P.batch_size * P.neg) * P.dim * 4 < lim;
-    if (csr && P.model == 0 && P.dim % 4 == 0 && fits31 && !old_step) {
+    // TransE on a counting-sort batch with float4 rows: k_step_csr (S lane groups per positive);
+    // PT_STEP_G / PT_STEP_S / PT_STEP_NCH override its shape
+    if (csr && csr_fast_path(P)) {
         const int64_t chunks = P.dim / 4;
         int G = 2;
         while (G < chunks && G < 64) G <<= 1;
@@ -632,7 +651,7 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
         if (const char *v = getenv("PT_STEP_NCH")) nch = atoi(v);
 #define PT_CSTEP(G_, K_, N_, S_)                                                                       \
         if (G == G_ && KCH == K_ && nch == N_ && S == S_) {                                          \
-            constexpr int NT_ = S_ * G_ > 256 ? S_ * G_ : 256;                                       \
+            constexpr int NT_ = S_ * G_ >= 256 || 256 % (S_ * G_) != 0 ? S_ * G_ : 256;             \
             const dim3 grid((unsigned)((P.batch_size * S_ * G_ + NT_ - 1) / NT_)), block(NT_);        \
             if (P.p_norm == 1)                                                                       \
                 hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 1, NT_>), grid, block, 0, st, P, sink, *csr); \
@@ -684,10 +703,13 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
             }                                                                                                     \
             return hipGetLastError();                                                                             \
         }
-        for (int pass = 0; pass < 2; ++pass) {   // no double-buffered instance: single buffer
+        // the preferred chunk size first, then any instantiated one (the kernel loops over chunks);
+        // double-buffered instances are tuning experiments only
+        const int cands[6] = {nch, nch, 8, 4, 32, 1};
+        for (int ci = 0; ci < 6; ++ci) {
+            nch = cands[ci];
+            if (ci > 0) db = false;
             PT_SSHAPES(PT_SSTEP)
-            if (!db) break;
-            db = false;
         }
 #undef PT_SSTEP
     }

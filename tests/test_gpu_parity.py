@@ -288,3 +288,60 @@ def test_gpu_ranking_matches_host_ranking(dup):
         for q in range(0, n, 17):
             cidx = oracle.candidates(E, int(h[q] if side == 0 else t[q]))
             np.testing.assert_array_equal(con[q], gl[q][cidx])
+
+
+# Counting-sort (neg >= 4) step / apply kernels across their shapes: float4 rows at every lane-group
+# width (D = 20 -> 8 lanes, 100 -> 32, 200 -> 64, 300 -> 64 x 2 chunks), negatives split over 1, 2 or 4
+# lane groups and over several record windows (neg > G), the VEC=1 kernel (D % 4 != 0), TransH, p in
+# {1, 2}, norm_flag on/off, SGD and Adagrad. Reference: the oracle's float32 steps on the same batches
+# (the GPU sampler is bit-exact with the oracle's), tolerance 2e-5 absolute on the tables (Adagrad:
+# noise-dominated components excluded, see assert_tables_close) and 1e-5 relative on the loss.
+CSR_CASES = [
+    # model, dim, p, norm_flag, opt, bs, neg
+    ("TransE", 20, 1, True, "sgd", 64, 5),
+    ("TransE", 100, 2, False, "adagrad", 48, 12),
+    ("TransE", 200, 2, True, "sgd", 128, 25),
+    ("TransE", 300, 1, True, "adagrad", 40, 30),
+    ("TransE", 64, 2, True, "sgd", 24, 150),
+    ("TransE", 18, 2, True, "sgd", 50, 8),
+    ("TransH", 24, 2, True, "adagrad", 40, 6),
+]
+
+
+@pytest.mark.parametrize("case", CSR_CASES, ids=lambda c: "%s-d%d-p%d-nf%d-%s-neg%d" % (c[0], c[1], c[2], c[3], c[4], c[6]))
+def test_counting_sort_step_matches_oracle(case):
+    from openke.config import Trainer
+    from openke.module.loss import MarginLoss
+    from openke.module.model import TransE, TransH
+    from openke.module.strategy import NegativeSampling
+    model, dim, p, nf, opt, bs, neg = case
+    steps, lr, margin, seed = 3, (0.5 if opt == "sgd" else 0.1), 4.0, 7
+    dl = _loader_path(KG_SMALL, 8, bs, neg, 1, 1, seed)
+    dl.nbatches = steps
+    torch.manual_seed(dim + neg)
+    cls = TransE if model == "TransE" else TransH
+    kge = cls(dl.get_ent_tot(), dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=nf)
+    t0 = _tables(kge)
+    ns = NegativeSampling(model=kge, loss=MarginLoss(margin=margin), batch_size=bs)
+    tr = Trainer(model=ns, data_loader=dl, train_times=1, alpha=lr, use_gpu=True, opt_method=opt)
+    tr.run()
+    kg = oracle.KG.load(KG_SMALL)
+    st = oracle.GlibcRand(seed).rand_reset(8)
+    ent, rel = t0["ent"].copy(), t0["rel"].copy()
+    nv = t0["norm"].copy() if model == "TransH" else None
+    accs = (np.zeros_like(ent), np.zeros_like(rel), None if nv is None else np.zeros_like(nv)) if opt == "adagrad" \
+        else (None, None, None)
+    ill = IllConditioned()
+    loss = 0.0
+    for _ in range(steps):
+        h, t, r, _ = kg.sample(st, 8, bs, neg, 1, 1)
+        for k, a in zip(("ent", "rel", "norm"), accs):
+            ill.before(k, a)
+        loss += oracle.train_step(model, p, nf, opt, lr, margin, ent, rel, nv, accs, h, t, r, bs, neg)
+        for k, a in zip(("ent", "rel", "norm"), accs):
+            ill.after(k, a)
+    np.testing.assert_allclose(tr.last_epoch_loss, loss, rtol=1e-5)
+    got = _tables(kge)
+    orc = {"ent": ent, "rel": rel, "norm": nv}
+    for k, v in got.items():
+        assert_tables_close(v, orc[k], 2e-5, ill.get(k) if opt == "adagrad" else None)
