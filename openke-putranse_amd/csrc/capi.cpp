@@ -58,6 +58,7 @@ struct pt_trainer {
     pt::StepParams P{};
     pt::StepWorkspace W{};
     void *ws_block = nullptr;
+    size_t ws_bytes = 0;   // gradient rows + touched flags (all zero between steps)
     // counting-sort gradient path for large neg (allocated on first use, grown as needed)
     void *csr_block = nullptr;
     size_t csr_cap = 0;
@@ -230,6 +231,7 @@ extern "C" int pt_trainer_create(const pt_model_desc *m, pt_trainer **out) {
     const size_t total = ge + gr + gn + fe + fr + fn;
     PT_HIP(hipMalloc(&t->ws_block, total));
     PT_HIP(hipMemset(t->ws_block, 0, total));
+    t->ws_bytes = total;
     char *b = (char *)t->ws_block;
     t->W.gent = (float *)b; b += ge;
     t->W.grel = (float *)b; b += gr;
@@ -456,6 +458,69 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
         tot[std::get<0>(e)] += ms;
     }
     for (int k = 0; k < 4; ++k) ms4[k] = (float)(tot[k] / (double)steps);
+    if (!use_csr(neg)) return PT_OK;
+    // Counting-sort path: the per-step kernels are re-timed back to back (as a captured epoch runs
+    // them), one event pair per loop instead of one per launch, on the last pre-sampled batch:
+    //   loop 1: `steps` x (forward/backward, apply)  -> T_sa;   loop 2: `steps` x forward/backward -> T_s
+    // ms4[2] = T_s / steps, ms4[3] = (T_sa - T_s) / steps. The tables, Adagrad state, gradient rows and
+    // flags are restored afterwards, so training state is exactly as the measured run left it.
+    pt::StepParams P = t->P;
+    P.batch_size = bs;
+    P.neg = neg;
+    P.inv_count = 1.0f / (float)(bs * neg);
+    const int64_t E = P.ent_total, R = P.rel_total, D = P.dim, dpp = 1 + 2 * neg;
+    std::vector<std::pair<float *, size_t>> keep = {{P.ent, 4 * E * D}, {P.rel, 4 * R * D}};
+    if (P.normv) keep.push_back({P.normv, 4 * R * D});
+    if (P.opt != 0) {
+        keep.push_back({P.ent_acc, 4 * E * D});
+        keep.push_back({P.rel_acc, 4 * R * D});
+        if (P.norm_acc) keep.push_back({P.norm_acc, 4 * R * D});
+    }
+    size_t nb = 0;
+    for (auto &k : keep) nb += k.second;
+    char *bak = nullptr;
+    PT_HIP(hipMalloc(&bak, nb));
+    size_t off = 0;
+    for (auto &k : keep) {
+        PT_HIP(hipMemcpyAsync(bak + off, k.first, k.second, hipMemcpyDeviceToDevice, st));
+        off += k.second;
+    }
+    const pt::DeviceGraph dg = s->g->dev;
+    const pt::CsrWork v = pt::csr_view(t->csr, 0, bs, neg);
+    hipEvent_t ev[4] = {tm.pool[0], tm.pool[1], tm.pool[2], tm.pool[3]};
+    int erc = PT_OK;
+    if (pt::launch_spin(20000, st) != hipSuccess || hipEventRecord(ev[0], st) != hipSuccess) erc = PT_EHIP;
+    for (int64_t i = 0; i < steps && !erc; ++i) {
+        if (pt::launch_step(P, dg, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr, nullptr, t->W,
+                            nullptr, st, &v) != hipSuccess ||
+            pt::launch_apply(P, t->W, nullptr, 0, bs, dpp, nullptr, st, &v) != hipSuccess)
+            erc = PT_EHIP;
+    }
+    if (!erc && (hipEventRecord(ev[1], st) != hipSuccess || pt::launch_spin(20000, st) != hipSuccess ||
+                 hipEventRecord(ev[2], st) != hipSuccess))
+        erc = PT_EHIP;
+    for (int64_t i = 0; i < steps && !erc; ++i) {
+        if (pt::launch_step(P, dg, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr, nullptr, t->W,
+                            nullptr, st, &v) != hipSuccess)
+            erc = PT_EHIP;
+    }
+    if (!erc && hipEventRecord(ev[3], st) != hipSuccess) erc = PT_EHIP;
+    // restore
+    off = 0;
+    for (auto &k : keep) {
+        if (hipMemcpyAsync(k.first, bak + off, k.second, hipMemcpyDeviceToDevice, st) != hipSuccess) erc = PT_EHIP;
+        off += k.second;
+    }
+    if (hipMemsetAsync(t->ws_block, 0, t->ws_bytes, st) != hipSuccess) erc = PT_EHIP;
+    const hipError_t se = hipStreamSynchronize(st);
+    (void)hipFree(bak);
+    if (erc) return pt::fail(erc, "pt_trainer_run_timed: isolation timing launch failed");
+    PT_HIP(se);
+    float t_sa = 0, t_s = 0;
+    PT_HIP(hipEventElapsedTime(&t_sa, ev[0], ev[1]));
+    PT_HIP(hipEventElapsedTime(&t_s, ev[2], ev[3]));
+    ms4[2] = t_s / (float)steps;
+    ms4[3] = (t_sa - t_s) / (float)steps;
     return PT_OK;
 }
 
