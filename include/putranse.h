@@ -97,8 +97,10 @@ int pt_trainer_run(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, 
 /* Measurement hook: `steps` in-kernel-sampled steps launched one by one (no graph) with an event pair
  * around every launch on `stream`. ms4[k] = total duration of kernel kind k divided by `steps`:
  * 0 batch sampling (k_sample_csr, large-neg path only, one launch per chunk of steps), 1 bucket scan
- * (k_scan_counts, idem), 2 fused forward/backward (k_step_sampled), 3 sparse optimizer (k_apply).
- * Synchronizes the stream. */
+ * (k_scan_counts, idem), 2 fused forward/backward (k_step_csr / k_step_sampled), 3 sparse optimizer
+ * (k_apply_buf / k_apply). On the large-neg path kinds 2 and 3 are then re-timed back to back (one
+ * event pair per loop of `steps` launches on the last sampled batch; tables, optimizer state and
+ * gradient rows restored), as the captured epoch runs them. Synchronizes the stream. */
 int pt_trainer_run_timed(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
                          int64_t steps, float *d_losses, float *ms4, void *stream);
 
