@@ -182,6 +182,115 @@ __device__ __forceinline__ float transe_step(const StepParams &P, int64_t hp, in
     return lsum;
 }
 
+// TransH counterpart of transe_step (group_step's TransH algebra with the sampler's one-side negatives):
+// the relation, its normal vector and the uncorrupted side are the positive's, kept on chip; the
+// projected positive rows are re-formed where the backward needs them instead of being held (the
+// universe kernel's register budget). Entity gradients leave raw (projection and normalize Jacobians
+// applied here, they depend on the relation), rel in normalized space, norm_vector in n-hat space.
+template <int G, int VEC, int KCH, typename Sink, typename NegFn>
+__device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, int64_t rp, int64_t tp, int64_t neg,
+                                             NegFn get_neg, const Sink &sink, int lane) {
+    using Vec = V<G, VEC, KCH>;
+    const int D = (int)P.dim;
+    const int p = P.p_norm;
+    const bool nf = P.norm_flag != 0;
+    Vec H, T, rh, nW, hh, th, vpos;
+    vload(H, P.ent + hp * D, D, lane);
+    vload(T, P.ent + tp * D, D, lane);
+    vload(rh, P.rel + rp * D, D, lane);
+    vload(nW, P.normv + rp * D, D, lane);
+    vnormalize(nW, nW);
+    const float hdot = vdot(H, nW), tdot = vdot(T, nW);
+#pragma unroll
+    for (int i = 0; i < Vec::N; ++i) {
+        hh.x[i] = H.x[i] - hdot * nW.x[i];
+        th.x[i] = T.x[i] - tdot * nW.x[i];
+    }
+    float hn = 0.f, tn = 0.f;
+    if (nf) {
+        hn = vnormalize(hh, hh);
+        vnormalize(rh, rh);
+        tn = vnormalize(th, th);
+    }
+#pragma unroll
+    for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
+    const float ps = vpnorm(vpos, p);
+    Vec aH, aT, aR, aW;
+    vzero(aH); vzero(aT); vzero(aR); vzero(aW);
+    float csum = 0.f, lsum = 0.f;
+    const float m = P.margin, inv = P.inv_count;
+    for (int64_t k = 0; k < neg; ++k) {
+        int64_t e;
+        bool tail_side;
+        get_neg(k, e, tail_side);
+        Vec X, xs, xh, vk;
+        vload(X, P.ent + e * D, D, lane);
+        const float ed = vdot(X, nW);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) xs.x[i] = X.x[i] - ed * nW.x[i];
+        float en = 0.f;
+        if (nf) en = vnormalize(xs, xh); else xh = xs;
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i)
+            vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - xh.x[i] : (xh.x[i] + rh.x[i]) - th.x[i];
+        const float ns = vpnorm(vk, p);
+        const float a = ps - ns;
+        lsum += a > -m ? a : -m;
+        const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
+        if (c == 0.f) continue;
+        csum += c;
+        vpnorm_bwd(vk, ns, p, -c, vk);   // vk := d loss / d v_k
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            aR.x[i] += vk.x[i];
+            if (tail_side) aH.x[i] += vk.x[i]; else aT.x[i] -= vk.x[i];
+            xh.x[i] = tail_side ? -vk.x[i] : vk.x[i];   // d / d(normalized projected corrupted row)
+        }
+        Vec gp;
+        if (nf) vnormalize_bwd(xs, en, xh, gp); else gp = xh;
+        const float ng = vdot(nW, gp);
+        Vec gw;
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            xh.x[i] = gp.x[i] - nW.x[i] * ng;
+            gw.x[i] = -(ed * gp.x[i] + ng * X.x[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) aW.x[i] += gw.x[i];
+        sink.ent(e, xh, D, lane);
+    }
+    if (csum != 0.f) {
+        vpnorm_bwd(vpos, ps, p, csum, vpos);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            aH.x[i] += vpos.x[i];
+            aR.x[i] += vpos.x[i];
+            aT.x[i] -= vpos.x[i];
+        }
+    }
+    if (vnonzero(aR)) sink.rel(rp, aR, D, lane);
+    // the positive's two entity rows (a lambda over explicit operands, not a loop selecting arrays by
+    // index: that would take their addresses and move them to scratch)
+    auto finish = [&](const Vec &acc, const Vec &E, float edot, float en, int64_t row) {
+        if (!vnonzero(acc)) return;
+        Vec es, gp;
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) es.x[i] = E.x[i] - edot * nW.x[i];
+        if (nf) vnormalize_bwd(es, en, acc, gp); else gp = acc;
+        const float ng = vdot(nW, gp);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) {
+            es.x[i] = gp.x[i] - nW.x[i] * ng;
+            aW.x[i] -= edot * gp.x[i] + ng * E.x[i];
+        }
+        sink.ent(row, es, D, lane);
+    };
+    finish(aH, H, hdot, hn, hp);
+    finish(aT, T, tdot, tn, tp);
+    if (vnonzero(aW)) sink.norm(rp, aW, D, lane);
+    return lsum;
+}
+
 // Dynamic LDS layout (int32 units; the host sizes it for the largest universe of the launch):
 //   list[list_cap] | flags[E + 2R] or [2R] | head[E] + next[ccap] (contrib) |
 //   batch h, r, t [3][pchunk * bs * (1 + neg)] (pchunk > 0) | rel (+ norm) gradient rows [R][D] floats
@@ -322,11 +431,12 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                             },
                             sink, lane);
                     } else {
-                        lsum = group_step<MODEL, G, VEC, KCH>(
+                        lsum = transh_step<G, VEC, KCH>(
                             P, hp, rp, tp, neg,
-                            [&](int64_t k, int64_t &h, int64_t &t, int64_t &r) {
+                            [&](int64_t k, int64_t &e, bool &tail_side) {
                                 const int64_t o = (k + 1) * bs + b;
-                                h = bh[o]; t = bt[o]; r = br[o];
+                                tail_side = bh[o] == hp;
+                                e = tail_side ? bt[o] : bh[o];
                             },
                             sink, lane);
                     }
@@ -342,14 +452,12 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                             },
                             sink, lane);
                     } else {
-                        lsum = group_step<MODEL, G, VEC, KCH>(
+                        lsum = transh_step<G, VEC, KCH>(
                             P, pd.h, pd.r, pd.t, neg,
-                            [&](int64_t k, int64_t &h, int64_t &t, int64_t &r) {
+                            [&](int64_t k, int64_t &e, bool &tail_side) {
                                 int side;
-                                const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
-                                h = side ? pd.h : e;
-                                t = side ? e : pd.t;
-                                r = pd.r;
+                                e = draw_negative(g, pd, k, bern, filter, &side);
+                                tail_side = side != 0;
                             },
                             sink, lane);
                     }
@@ -366,40 +474,53 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // loads in flight together: the pass is a chain of dependent memory round trips otherwise)
             const int n = s_count;
             constexpr int RB = VEC * KCH > 4 ? 2 : 4;
+            // (guards, not breaks, inside the unrolled loops: the row arrays must stay in registers)
             for (int i0 = grp * RB; i0 < n; i0 += GPB * RB) {
-                Vec x[RB], gs[RB], a[RB];
-                float *wp[RB], *ap[RB];
-                int32_t code[RB];
+                Vec x[RB], gs[RB], a[RB], y[RB];
+                int32_t code[RB], c1[RB];
 #pragma unroll
                 for (int u = 0; u < RB; ++u) {
-                    if (i0 + u >= n) break;
-                    code[u] = s_list[i0 + u];
-                    const int table = code[u] & 3;
-                    const int64_t row = code[u] >> 2;
-                    wp[u] = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
-                    ap[u] = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
-                    vload(x[u], wp[u], (int)D, lane);
-                    if (opt != 0) vload(a[u], ap[u], (int)D, lane);
-                    if ((table == 0 && contrib) || (table > 0 && rel_list)) {
-                        // the row's contributions (linked in LDS), summed in list order
-                        int32_t c = s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row];
-                        vload(gs[u], U.contrib + (int64_t)c * D, (int)D, lane);
-                        for (c = s_next[c]; c >= 0; c = s_next[c]) {
-                            Vec y;
-                            vload(y, U.contrib + (int64_t)c * D, (int)D, lane);
-#pragma unroll
-                            for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y.x[j];
+                    code[u] = i0 + u < n ? s_list[i0 + u] : -1;
+                    c1[u] = -1;
+                    if (code[u] >= 0) {
+                        const int table = code[u] & 3;
+                        const int64_t row = code[u] >> 2;
+                        const float *wp = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
+                        const float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
+                        vload(x[u], wp, (int)D, lane);
+                        if (opt != 0) vload(a[u], ap, (int)D, lane);
+                        if ((table == 0 && contrib) || (table > 0 && rel_list)) {
+                            // the row's contributions (linked in LDS): the first two loads issued with the
+                            // row's own, the rest walked below; summed in list order
+                            const int32_t c0 = s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row];
+                            vload(gs[u], U.contrib + (int64_t)c0 * D, (int)D, lane);
+                            c1[u] = s_next[c0];
+                            if (c1[u] >= 0) vload(y[u], U.contrib + (int64_t)c1[u] * D, (int)D, lane);
+                        } else {
+                            vload(gs[u], (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D,
+                                  (int)D, lane);
                         }
-                    } else {
-                        vload(gs[u], (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D,
-                              (int)D, lane);
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < RB; ++u) {
-                    if (i0 + u >= n) break;
+                    if (code[u] >= 0 && c1[u] >= 0) {
+#pragma unroll
+                        for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
+                        for (int32_t c = s_next[c1[u]]; c >= 0; c = s_next[c]) {
+                            vload(y[u], U.contrib + (int64_t)c * D, (int)D, lane);
+#pragma unroll
+                            for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < RB; ++u) {
+                    if (code[u] < 0) continue;
                     const int table = code[u] & 3;
                     const int64_t row = code[u] >> 2;
+                    float *wp = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
+                    float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
                     // ent rows of TransE and every rel / norm_vector row carry normalized-space gradients
                     const bool jac = table == 0 ? (MODEL == 0 && norm_flag) : (table == 1 ? norm_flag != 0 : true);
                     Vec gg;
@@ -418,9 +539,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                             a[u].x[j] = a[u].x[j] + gg.x[j] * gg.x[j];
                             x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j] / (sqrtf(a[u].x[j]) + 1e-10f);
                         }
-                        vstore(a[u], ap[u], (int)D, lane);
+                        vstore(a[u], ap, (int)D, lane);
                     }
-                    vstore(x[u], wp[u], (int)D, lane);
+                    vstore(x[u], wp, (int)D, lane);
                     if ((table == 0 && contrib) || (table > 0 && rel_list)) {
                         if (lane == 0) s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row] = -1;
                     } else {

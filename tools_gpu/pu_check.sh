@@ -1,0 +1,6 @@
+#!/bin/bash
+# PU GPU tests, then the universe cycle split and bench lines for C3 and C5
+set -u
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_pu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pu_tests.log 2>&1 || exit $?
+bash tools_gpu/uni_prof.sh || exit $?
