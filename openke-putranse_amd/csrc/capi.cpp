@@ -10,6 +10,7 @@
 #include <mutex>
 #include <thread>
 #include <tuple>
+#include <queue>
 #include <vector>
 
 #include "common.h"
@@ -684,13 +685,24 @@ struct pt_universe_set {
     int64_t bern = 0, filter = 0, neg = 1;
     int device = -1;
     void *arena = nullptr;
-    pt::UniverseDev *d_us = nullptr;      // inside the arena, longest-first order
-    int *d_counter = nullptr;             // work-queue counter (inside the arena)
+    pt::UniverseDev *d_us = nullptr;      // inside the arena, by row shape, longest-first inside a shape
+    int *d_counter = nullptr;             // work-queue counters, one per shape group (inside the arena)
+    struct Group {
+        int shape;
+        int64_t off, n;
+        double work;
+        int64_t share = 1;   // workgroups (= CUs) of its launch
+    };
+    std::vector<Group> groups;            // runs of d_us with one shape class (one kernel launch each)
+    std::vector<hipStream_t> streams;     // side streams of the group launches (created on first train)
+    std::vector<hipEvent_t> events;
     pt::UniverseLaunch cfg;
     std::vector<pt::UniverseDev> host;    // same order; loss pointers patched per train call
     std::vector<int64_t> host_loss_off;
     uint64_t *prof = nullptr;             // PT_UNI_PROF=1: [n][4] cycle counters (device)
     ~pt_universe_set() {
+        for (auto e : events) (void)hipEventDestroy(e);
+        for (auto q : streams) (void)hipStreamDestroy(q);
         if (arena) (void)hipFree(arena);
         if (prof) (void)hipFree(prof);
     }
@@ -728,7 +740,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         PT_CHECK(opt == PT_SGD || (J.ent_acc && J.rel_acc && (model == 0 || J.norm_acc)), PT_EINVAL,
                  "Adagrad universe job needs accumulators");
         PT_CHECK(J.threads > 0 && J.threads <= 64, PT_EINVAL, "universe job: threads must be in [1, 64]");
-        PT_CHECK(J.dim > 0 && pt::universe_shape_supported(J.dim), PT_EINVAL, "universe job: unsupported dim");
+        PT_CHECK(J.dim > 0 && pt::universe_shape_supported(J.dim, model), PT_EINVAL, "universe job: unsupported dim");
         PT_CHECK(J.batch_size >= 0 && J.epochs >= 0 && J.nbatches >= 0, PT_EINVAL, "universe job: negative sizes");
         PT_CHECK(neg < 0 || J.neg == neg, PT_EINVAL, "universe jobs must share neg");
         PT_CHECK(J.neg >= 1, PT_EINVAL, "universe job: neg must be >= 1");
@@ -746,7 +758,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     const int64_t us_off = total;
     total += al((int64_t)sizeof(pt::UniverseDev) * std::max<int64_t>(n, 1));
     const int64_t counter_off = total;
-    total += al(sizeof(int));
+    total += al(sizeof(int) * 64);   // one work-queue counter per row shape
     PT_HIP(hipMalloc(&set->arena, (size_t)total));
     char *base = (char *)set->arena;
     PT_HIP(hipMemset(base, 0, (size_t)us_off));
@@ -755,14 +767,67 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     int max_lds = 64 << 10;
     (void)hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, set->device);
     const int64_t lds_budget = std::min<int64_t>(max_lds, 80 << 10) - 1024;
-    // one persistent launch over all universes, longest dependent step chain first (the work queue
-    // then approximates longest-processing-time scheduling over the CUs)
+    // one persistent launch per row shape, its universes longest dependent step chain first (the work
+    // queue then approximates longest-processing-time scheduling over the launch's workgroups)
+    auto work = [&](int64_t i) {
+        return (double)jobs[i].epochs * (double)jobs[i].nbatches * (double)std::max<int64_t>(jobs[i].batch_size, 1);
+    };
     std::vector<int64_t> order((size_t)n);
     for (int64_t i = 0; i < n; ++i) order[i] = i;
+    auto cls_of = [&](int64_t i) { return pt::universe_shape_class(pt::universe_shape_id(jobs[i].dim, model)); };
     std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-        return jobs[a].epochs * jobs[a].nbatches * std::max<int64_t>(jobs[a].batch_size, 1) >
-               jobs[b].epochs * jobs[b].nbatches * std::max<int64_t>(jobs[b].batch_size, 1);
+        const int sa = cls_of(a), sb = cls_of(b);
+        if (sa != sb) return sa < sb;
+        return work(a) > work(b);
     });
+    for (int64_t k = 0; k < n; ++k) {
+        const int sh = cls_of(order[k]);
+        if (set->groups.empty() || set->groups.back().shape != sh) set->groups.push_back({sh, k, 0, 0.0});
+        set->groups.back().n += 1;
+        set->groups.back().work += work(order[k]);
+    }
+    PT_CHECK(set->groups.size() <= 64, PT_EINVAL, "too many universe shape classes");
+    // CU shares: model a universe's time as steps x (1 + rounds of its step's positives over the shape's
+    // lane groups); give every group one CU, then each further CU to the group whose LPT makespan over
+    // its current share is longest (the launches run concurrently, so the slowest group ends the set)
+    {
+        int cus = 0;
+        PT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, set->device));
+        std::vector<std::vector<double>> tg(set->groups.size());
+        for (size_t k = 0; k < set->groups.size(); ++k) {
+            const auto &gr = set->groups[k];
+            for (int64_t q = gr.off; q < gr.off + gr.n; ++q) {
+                const pt_universe_job &J = jobs[order[q]];
+                const int64_t gpb = pt::universe_shape_groups(pt::universe_shape_id(J.dim, model));
+                const int64_t rounds = (std::max<int64_t>(J.batch_size, 1) + gpb - 1) / gpb;
+                tg[k].push_back((double)J.epochs * (double)J.nbatches * (double)(1 + rounds));
+            }
+            std::sort(tg[k].begin(), tg[k].end(), std::greater<double>());
+        }
+        auto makespan = [&](size_t k, int64_t s) {
+            std::priority_queue<double, std::vector<double>, std::greater<double>> m;
+            for (int64_t i = 0; i < s; ++i) m.push(0.0);
+            double end = 0;
+            for (double t : tg[k]) {
+                const double f = m.top() + t;
+                m.pop();
+                m.push(f);
+                end = std::max(end, f);
+            }
+            return end;
+        };
+        std::vector<double> ms(set->groups.size());
+        for (size_t k = 0; k < set->groups.size(); ++k) ms[k] = makespan(k, 1);
+        for (int64_t left = (int64_t)cus - (int64_t)set->groups.size(); left > 0; --left) {
+            size_t best = set->groups.size();
+            for (size_t k = 0; k < set->groups.size(); ++k)
+                if (set->groups[k].share < set->groups[k].n && (best == set->groups.size() || ms[k] > ms[best]))
+                    best = k;
+            if (best == set->groups.size()) break;
+            set->groups[best].share += 1;
+            ms[best] = makespan(best, set->groups[best].share);
+        }
+    }
     set->d_us = (pt::UniverseDev *)(base + us_off);
     set->d_counter = (int *)(base + counter_off);
     set->host.reserve((size_t)n);
@@ -797,7 +862,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         U.prof = set->prof ? set->prof + 4 * (int64_t)set->host.size() : nullptr;
         U.threads = J.threads; U.bs = J.batch_size; U.nbatches = J.nbatches; U.epochs = J.epochs; U.dim = J.dim;
         U.lr = J.lr; U.margin = J.margin;
-        U.shape = pt::universe_shape_id(J.dim);
+        U.shape = pt::universe_shape_id(J.dim, model);
         set->host.push_back(U);
         set->host_loss_off.push_back(loss_of[i]);
         max_bs = std::max(max_bs, J.batch_size);
@@ -859,10 +924,34 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
         set->host[i].losses = d_losses ? d_losses + set->host_loss_off[i] : nullptr;
     PT_HIP(hipMemcpyAsync(set->d_us, set->host.data(), sizeof(pt::UniverseDev) * set->host.size(),
                           hipMemcpyHostToDevice, st));
-    const hipError_t e = pt::launch_universes(set->d_us, (int64_t)set->host.size(), set->d_counter, set->model,
-                                              set->p_norm, set->norm_flag, set->opt, set->neg, (int)set->bern,
-                                              (int)set->filter, set->cfg, st);
-    if (e != hipSuccess) return pt::fail(PT_EHIP, std::string("launch_universes: ") + hipGetErrorString(e));
+    // one launch per shape class, concurrently on a side stream, each over its share of the CUs (set at
+    // creation); joined back into `st`
+    const size_t ng = set->groups.size();
+    while (set->streams.size() + 1 < ng) {
+        hipStream_t q;
+        PT_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+        set->streams.push_back(q);
+    }
+    while (set->events.size() < ng) {
+        hipEvent_t ev;
+        PT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        set->events.push_back(ev);
+    }
+    PT_HIP(hipEventRecord(set->events[0], st));
+    for (size_t k = 1; k < ng; ++k) PT_HIP(hipStreamWaitEvent(set->streams[k - 1], set->events[0], 0));
+    for (size_t k = 0; k < ng; ++k) {
+        const auto &gr = set->groups[k];
+        const int64_t share = gr.share;
+        hipStream_t q = k == 0 ? st : set->streams[k - 1];
+        const hipError_t e = pt::launch_universes(set->d_us + gr.off, gr.n, set->d_counter + k, gr.shape, share,
+                                                  set->model, set->p_norm, set->norm_flag, set->opt, set->neg,
+                                                  (int)set->bern, (int)set->filter, set->cfg, q);
+        if (e != hipSuccess) return pt::fail(PT_EHIP, std::string("launch_universes: ") + hipGetErrorString(e));
+    }
+    for (size_t k = 1; k < ng; ++k) {
+        PT_HIP(hipEventRecord(set->events[k], set->streams[k - 1]));
+        PT_HIP(hipStreamWaitEvent(st, set->events[k], 0));
+    }
     // the host array must outlive the async copy: this call returns only after it has been consumed
     PT_HIP(hipStreamSynchronize(st));
     return PT_OK;

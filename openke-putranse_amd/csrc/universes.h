@@ -40,13 +40,17 @@ struct UniverseLaunch {
 
 // lane-group shape of the universe kernel for dim D (narrower groups than pick_shape) and its id in
 // the kernel's shape switch (-1: unsupported)
-Shape pick_universe_shape(int64_t D);
-int universe_shape_id(int64_t D);
-bool universe_shape_supported(int64_t D);
+Shape pick_universe_shape(int64_t D, bool wide);
+int universe_shape_id(int64_t D, int model);
+bool universe_shape_supported(int64_t D, int model);
 
-// all n universes in one persistent launch: workgroups pull universes from *counter (device int,
-// reset by the launch) in array order (the host sorts longest-first)
-hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, int model, int p_norm, int norm_flag,
-                            int opt, int64_t neg, int bern, int filter, const UniverseLaunch &cfg, hipStream_t st);
+// the n universes of one shape class (d_us[0..n), longest first) in one persistent launch of that
+// class's kernel over `cus` CUs' worth of workgroups: workgroups pull universes from *counter (device
+// int, reset by the launch)
+hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, int cls, int64_t cus, int model,
+                            int p_norm, int norm_flag, int opt, int64_t neg, int bern, int filter,
+                            const UniverseLaunch &cfg, hipStream_t st);
+int universe_shape_class(int shape);
+int universe_shape_groups(int shape);
 
 }  // namespace pt

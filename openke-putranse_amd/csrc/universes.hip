@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "device.h"
 #include "kernels.h"
@@ -584,10 +585,14 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     X(7, 2, 1, 1) X(8, 2, 1, 2) X(9, 2, 1, 4) X(10, 4, 1, 4) X(11, 8, 1, 4) X(12, 16, 1, 4)              \
     X(13, 32, 1, 4) X(14, 64, 1, 4) X(15, 64, 1, 8)
 
-// Persistent work-queue kernel: a workgroup takes universes in the host's longest-first order from an
-// atomic counter until the queue is empty (greedy longest-processing-time list scheduling over the
-// CUs, whatever the mix of universe sizes and row shapes), every universe with its shape's code path.
-template <int MODEL, int NT, int WPE>
+// Persistent work-queue kernel of one shape CLASS (rows of <= 4 floats per lane, or wider): a workgroup
+// takes universes (all of this class, in the host's longest-first order) from an atomic counter until
+// the queue is empty - greedy longest-processing-time list scheduling over the launch's workgroups -
+// and runs each with its shape's code path. Two classes instead of one kernel for every shape: each
+// kernel is register-allocated for its own widest shape (one kernel over all shapes spills the narrow
+// ones' state too), and two launches still run concurrently (a launch per shape would need more
+// hardware queues than a process gets).
+template <int MODEL, int NT, int WPE, int CLS>
 __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__restrict__ us, int64_t n,
                                                        int *__restrict__ next_universe, int p_norm, int norm_flag,
                                                        int opt, int64_t neg, int bern, int filter,
@@ -605,9 +610,10 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
         if (u >= n) break;   // every wave of the workgroup reads the same u: the whole group exits
         const UniverseDev U = us[u];
         switch (U.shape) {
-#define PT_URUN(ID_, G_, V_, K_)                                                                   \
-    case ID_:                                                                                      \
-        universe_run<MODEL, G_, V_, K_, NT>(U, p_norm, norm_flag, opt, neg, bern, filter, cfg, S); \
+#define PT_URUN(ID_, G_, V_, K_)                                                                       \
+    case ID_:                                                                                          \
+        if constexpr ((V_ * K_ <= 4 ? 0 : 1) == CLS)                                                   \
+            universe_run<MODEL, G_, V_, K_, NT>(U, p_norm, norm_flag, opt, neg, bern, filter, cfg, S); \
         break;
             PT_USHAPES(PT_URUN)
 #undef PT_URUN
@@ -620,10 +626,10 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
 
 }  // namespace dev
 
-Shape pick_universe_shape(int64_t D) {
+Shape pick_universe_shape(int64_t D, bool wide) {
     const int VEC = D % 4 == 0 ? 4 : 1;
     const int64_t chunks = (D + VEC - 1) / VEC;
-    const int64_t per_lane = VEC == 4 ? 2 : 4;
+    const int64_t per_lane = (VEC == 4 ? 2 : 4) * (wide ? 2 : 1);
     int G = 2;
     while (G < 64 && (int64_t)G * per_lane < chunks) G <<= 1;
     int KCH = 1;
@@ -631,9 +637,10 @@ Shape pick_universe_shape(int64_t D) {
     return Shape{G, VEC, KCH};
 }
 
-int universe_shape_id(int64_t D) {
+int universe_shape_id(int64_t D, int model) {
+    (void)model;
     if (D <= 0) return -1;
-    const Shape s = pick_universe_shape(D);
+    const Shape s = pick_universe_shape(D, false);
 #define PT_USUP(ID_, G_, V_, K_) \
     if (s.G == G_ && s.VEC == V_ && s.KCH == K_) return ID_;
     PT_USHAPES(PT_USUP)
@@ -641,28 +648,25 @@ int universe_shape_id(int64_t D) {
     return -1;
 }
 
-bool universe_shape_supported(int64_t D) { return universe_shape_id(D) >= 0; }
+bool universe_shape_supported(int64_t D, int model) { return universe_shape_id(D, model) >= 0; }
 
 namespace {
-template <int MODEL, int WPE>
-hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int p_norm, int norm_flag, int opt, int64_t neg,
-                    int bern, int filter, const UniverseLaunch &cfg, hipStream_t st) {
+template <int MODEL, int WPE, int CLS>
+hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int64_t cus, int p_norm, int norm_flag, int opt,
+                    int64_t neg, int bern, int filter, const UniverseLaunch &cfg, hipStream_t st) {
     constexpr int NT = 512;
-    auto kern = dev::k_universes<MODEL, NT, WPE>;
+    auto kern = dev::k_universes<MODEL, NT, WPE, CLS>;
     if (cfg.lds_bytes > (64 << 10)) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)cfg.lds_bytes);
         if (e != hipSuccess) return e;
     }
-    int dev = 0, cus = 0, per_cu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kern), NT,
-                                                         (size_t)cfg.lds_bytes);
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kern), NT,
+                                                                (size_t)cfg.lds_bytes);
     if (e != hipSuccess) return e;
     if (per_cu < 1) per_cu = 1;
-    int64_t grid = (int64_t)cus * per_cu;
+    int64_t grid = cus * per_cu;
     if (grid > n) grid = n;
     if (grid < 1) grid = 1;
     e = hipMemsetAsync(counter, 0, sizeof(int), st);
@@ -673,11 +677,33 @@ hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int p_norm
 }
 }  // namespace
 
-hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, int model, int p_norm, int norm_flag,
-                            int opt, int64_t neg, int bern, int filter, const UniverseLaunch &cfg, hipStream_t st) {
+// shape class of a row shape: 0 = at most 4 floats per lane, 1 = wider (one kernel per class)
+int universe_shape_class(int shape) {
+#define PT_UCLS(ID_, G_, V_, K_) \
+    if (shape == ID_) return V_ * K_ <= 4 ? 0 : 1;
+    PT_USHAPES(PT_UCLS)
+#undef PT_UCLS
+    return 1;
+}
+
+// lane groups of a universe workgroup for a shape (positives of a step processed concurrently)
+int universe_shape_groups(int shape) {
+#define PT_UGPB(ID_, G_, V_, K_) \
+    if (shape == ID_) return 512 / G_;
+    PT_USHAPES(PT_UGPB)
+#undef PT_UGPB
+    return 1;
+}
+
+hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, int cls, int64_t cus, int model,
+                            int p_norm, int norm_flag, int opt, int64_t neg, int bern, int filter,
+                            const UniverseLaunch &cfg, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    return model == 0 ? launch_q<0, 1>(d_us, n, counter, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
-                      : launch_q<1, 1>(d_us, n, counter, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
+    if (cls == 0)
+        return model == 0 ? launch_q<0, 2, 0>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
+                          : launch_q<1, 2, 0>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
+    return model == 0 ? launch_q<0, 2, 1>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
+                      : launch_q<1, 2, 1>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
 }
 
 }  // namespace pt
