@@ -474,7 +474,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // ---- phase B: row updates of the touched rows, RB rows per lane group at a time (all their
             // loads in flight together: the pass is a chain of dependent memory round trips otherwise)
             const int n = s_count;
-            constexpr int RB = VEC * KCH > 4 ? 2 : 4;
+            constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? 2 : 4);
             // (guards, not breaks, inside the unrolled loops: the row arrays must stay in registers)
             for (int i0 = grp * RB; i0 < n; i0 += GPB * RB) {
                 Vec x[RB], gs[RB], a[RB], y[RB];
@@ -583,7 +583,12 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
 #define PT_USHAPES(X)                                                                                  \
     X(0, 2, 4, 1) X(1, 2, 4, 2) X(2, 4, 4, 2) X(3, 8, 4, 2) X(4, 16, 4, 2) X(5, 32, 4, 2) X(6, 64, 4, 2) \
     X(7, 2, 1, 1) X(8, 2, 1, 2) X(9, 2, 1, 4) X(10, 4, 1, 4) X(11, 8, 1, 4) X(12, 16, 1, 4)              \
-    X(13, 32, 1, 4) X(14, 64, 1, 4) X(15, 64, 1, 8)
+    X(13, 32, 1, 4) X(14, 64, 1, 4) X(15, 64, 1, 8)                                                      \
+    X(16, 2, 4, 4) X(17, 4, 4, 4) X(18, 8, 4, 4) X(19, 16, 4, 4) X(20, 32, 4, 4) X(21, 64, 4, 4)        \
+    X(22, 2, 1, 8) X(23, 4, 1, 8) X(24, 8, 1, 8) X(25, 16, 1, 8) X(26, 32, 1, 8)
+
+// shape class (one kernel each): 0 = at most 4 floats per lane, 1 = 8, 2 = 16 (TransE's wide shapes)
+#define PT_UCLASS(V_, K_) ((V_) * (K_) <= 4 ? 0 : ((V_) * (K_) <= 8 ? 1 : 2))
 
 // Persistent work-queue kernel of one shape CLASS (rows of <= 4 floats per lane, or wider): a workgroup
 // takes universes (all of this class, in the host's longest-first order) from an atomic counter until
@@ -612,7 +617,7 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
         switch (U.shape) {
 #define PT_URUN(ID_, G_, V_, K_)                                                                       \
     case ID_:                                                                                          \
-        if constexpr ((V_ * K_ <= 4 ? 0 : 1) == CLS)                                                   \
+        if constexpr (PT_UCLASS(V_, K_) == CLS && (MODEL == 0 || ID_ < 16)) /* TransH: narrow shapes */  \
             universe_run<MODEL, G_, V_, K_, NT>(U, p_norm, norm_flag, opt, neg, bern, filter, cfg, S); \
         break;
             PT_USHAPES(PT_URUN)
@@ -638,9 +643,14 @@ Shape pick_universe_shape(int64_t D, bool wide) {
 }
 
 int universe_shape_id(int64_t D, int model) {
-    (void)model;
     if (D <= 0) return -1;
-    const Shape s = pick_universe_shape(D, false);
+    // TransE (few live rows per step) takes the wide shapes: twice the lane groups, half the rounds of a
+    // step's positives (PT_UNI_NARROW=1: the narrow ones)
+    static const bool narrow = [] {
+        const char *v = getenv("PT_UNI_NARROW");
+        return v && atoi(v) != 0;
+    }();
+    const Shape s = pick_universe_shape(D, model == 0 && !narrow);
 #define PT_USUP(ID_, G_, V_, K_) \
     if (s.G == G_ && s.VEC == V_ && s.KCH == K_) return ID_;
     PT_USHAPES(PT_USUP)
@@ -677,10 +687,10 @@ hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int64_t cu
 }
 }  // namespace
 
-// shape class of a row shape: 0 = at most 4 floats per lane, 1 = wider (one kernel per class)
+// shape class of a row shape (one kernel per class)
 int universe_shape_class(int shape) {
 #define PT_UCLS(ID_, G_, V_, K_) \
-    if (shape == ID_) return V_ * K_ <= 4 ? 0 : 1;
+    if (shape == ID_) return PT_UCLASS(V_, K_);
     PT_USHAPES(PT_UCLS)
 #undef PT_UCLS
     return 1;
@@ -702,8 +712,12 @@ hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, in
     if (cls == 0)
         return model == 0 ? launch_q<0, 2, 0>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
                           : launch_q<1, 2, 0>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
-    return model == 0 ? launch_q<0, 2, 1>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
-                      : launch_q<1, 2, 1>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
+    if (cls == 1)
+        return model == 0 ? launch_q<0, 2, 1>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
+                          : launch_q<1, 2, 1>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
+    if (model == 0)
+        return launch_q<0, 2, 2>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
+    return hipErrorInvalidValue;   // TransH universes use the narrow shapes
 }
 
 }  // namespace pt
