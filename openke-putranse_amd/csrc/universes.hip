@@ -67,6 +67,9 @@ struct UniverseSink {
     int *ccount;         // LDS counter of contribution slots
     int64_t E, R;
     bool rel_list;       // relation / norm_vector rows as contribution lists too
+    // next contribution slot of the lane group's current positive: positive b owns the static slots
+    // [b * per_pos, (b + 1) * per_pos), per_pos = neg + 2 (+2 with relation lists) >= its links
+    mutable int slot = 0;
     __device__ __forceinline__ void touch(int32_t *flag, int64_t row, int table) const {
         if (atomicExch(flag + row, 1) == 0) list[atomicAdd(count, 1)] = (int32_t)(row << 2) | table;
     }
@@ -74,9 +77,7 @@ struct UniverseSink {
     template <int G, int VEC, int KCH>
     __device__ __forceinline__ void link(int32_t *h, int64_t row, int table, const V<G, VEC, KCH> &g, int D,
                                          int lane) const {
-        int c = 0;
-        if (lane == 0) c = atomicAdd(ccount, 1);
-        c = __shfl(c, 0, G);
+        const int c = slot++;   // group-uniform: every lane of the group makes the same calls
         vstore(g, contrib + (int64_t)c * D, D, lane);
         if (lane == 0) {
             const int32_t prev = atomicExch(h + row, c);
@@ -416,6 +417,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // ---- phase A: forward + backward of the step's positives
             for (int64_t b = grp; b < bs; b += GPB) {
                 float lsum;
+                sink.slot = (int)(b * ((rel_list ? 4 : 2) + neg));
                 if (pchunk > 0) {
                     const int32_t *bh = s_bh + cs * seq, *br = s_br + cs * seq, *bt = s_bt + cs * seq;
                     const int64_t hp = bh[b], rp = br[b], tp = bt[b];
