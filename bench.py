@@ -273,7 +273,7 @@ def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
     estimation, Parallel_Universe_Config.py:446-642): per rank pt_lp_min_scores of its universes into
     the key rows, RCCL all_reduce(MIN), pt_rank_rows, pt_lp_metrics. Timed end to end on the device."""
     from openke import _native
-    from openke.config.Parallel_Universe_Config import lp_pairs
+    from openke.config.Parallel_Universe_Config import lp_pair_array, lp_pairs_all
     E = sum(1 for _ in open(os.path.join(path, "entity2id.txt")))
     trip = {f: np.loadtxt(os.path.join(path, f), dtype=np.int64, ndmin=2) for f in
             ("train2id.txt", "valid2id.txt", "test2id.txt")}
@@ -295,21 +295,21 @@ def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
     t0 = time.perf_counter()
     rows = torch.full((len(keys), E), float("inf"), device=dev)
     tup = torch.full((len(keys),), float("inf"), device=dev)
-    lp_us, pairs, dremaps = [], [], []
+    lp_us = []
+    # every universe's local->global entity map in one device array (one copy)
+    moff = np.cumsum([0] + [len(u["em"]) for u in unis])
+    dremaps = torch.from_numpy(np.concatenate([u["em"] for u in unis]) if unis else np.zeros(1, np.int64)).to(dev)
     for slot, u in enumerate(unis):
         U = _native.LpUniverse()
         U.ent, U.rel = u["ent"].data_ptr(), u["rel"].data_ptr()
         U.normv = u["nv"].data_ptr() if u["nv"] is not None else None
         U.ent_total, U.rel_total, U.dim = u["ent"].shape[0], u["rel"].shape[0], u["dim"]
-        dr = torch.from_numpy(u["em"]).to(dev)
-        dremaps.append(dr)
-        U.d_ent_remap = dr.data_ptr()
+        U.d_ent_remap = dremaps.data_ptr() + 8 * int(moff[slot])
         lp_us.append(U)
-        pairs.extend(lp_pairs(slot, u["em"], u["rm"], ka, kr, ks))
-    if pairs:
+    pair_arr, arr_p = lp_pair_array([lp_pairs_all([u["em"] for u in unis], [u["rm"] for u in unis], ka, kr, ks)])
+    if len(pair_arr):
         arr_u = (_native.LpUniverse * len(lp_us))(*lp_us)
-        arr_p = (_native.LpPair * len(pairs))(*[_native.LpPair(*p) for p in pairs])
-        _native.check(L.pt_lp_min_scores(arr_u, len(lp_us), mid, p_norm, 1, arr_p, len(pairs), E, _native.ptr(rows),
+        _native.check(L.pt_lp_min_scores(arr_u, len(lp_us), mid, p_norm, 1, arr_p, len(pair_arr), E, _native.ptr(rows),
                                          _native.ptr(tup), _native.stream()))
     torch.cuda.synchronize()
     t_score = time.perf_counter() - t0
@@ -342,7 +342,7 @@ def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
                                   ranks[3].ctypes.data, n, met.ctypes.data))
     L.pt_known_free(known)
     cand = sum(len(u["em"]) for u in unis)
-    return {"queries": int(n), "keys": len(keys), "pairs_this_rank": len(pairs), "seconds": el,
+    return {"queries": int(n), "keys": len(keys), "pairs_this_rank": len(pair_arr), "seconds": el,
             "score_s": t_score, "min_combine_s": t_comb, "rank_s": el - t_score - t_comb,
             "mrr_mr_hit10_hit3_hit1": [float(x) for x in met[:5]],
             "note": "universe scoring 4D+4 B per (key, universe entity); ranking 4 B per (query, entity)"}

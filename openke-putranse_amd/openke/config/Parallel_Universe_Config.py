@@ -108,7 +108,64 @@ def lp_pairs(slot, ent_remap, rel_remap, key_anchor, key_rel, key_side):
     la = lookup_local(em[eo], eo, key_anchor)
     lr = lookup_local(rm[ro], ro, key_rel)
     sel = np.nonzero((la >= 0) & (lr >= 0))[0]
-    return [(int(k), slot, int(la[k]), int(lr[k]), int(key_side[k])) for k in sel]
+    # int32 [n][5] rows, the memory layout of pt_lp_pair (key, universe, anchor, rel, side)
+    out = np.empty((len(sel), 5), dtype=np.int32)
+    out[:, 0] = sel
+    out[:, 1] = slot
+    out[:, 2] = la[sel]
+    out[:, 3] = lr[sel]
+    out[:, 4] = np.asarray(key_side)[sel]
+    return out
+
+
+def lp_pairs_all(ent_remaps, rel_remaps, key_anchor, key_rel, key_side):
+    """lp_pairs of every universe slot at once (vectorized over universes): the anchor entity's
+    occurrences across all universes (an inverted index by global id) joined with the keys, then the
+    relation membership tested by a sorted (universe, global relation) code. Returns int32 [n][5]
+    rows (key, slot, local anchor, local relation, side), grouped by key."""
+    key_anchor = np.asarray(key_anchor, dtype=np.int64)
+    key_rel = np.asarray(key_rel, dtype=np.int64)
+    key_side = np.asarray(key_side, dtype=np.int64)
+    if not ent_remaps or len(key_anchor) == 0:
+        return np.zeros((0, 5), dtype=np.int32)
+    ne = np.array([len(m) for m in ent_remaps], dtype=np.int64)
+    nr = np.array([len(m) for m in rel_remaps], dtype=np.int64)
+    eg = np.concatenate([np.asarray(m, dtype=np.int64) for m in ent_remaps])          # global entity
+    eu = np.repeat(np.arange(len(ent_remaps), dtype=np.int64), ne)                     # its universe slot
+    el = np.concatenate([np.arange(n, dtype=np.int64) for n in ne])                    # its local id
+    rg = np.concatenate([np.asarray(m, dtype=np.int64) for m in rel_remaps])
+    ru = np.repeat(np.arange(len(rel_remaps), dtype=np.int64), nr)
+    rl = np.concatenate([np.arange(n, dtype=np.int64) for n in nr])
+    o = np.argsort(eg, kind="stable")
+    eg, eu, el = eg[o], eu[o], el[o]
+    lo = np.searchsorted(eg, key_anchor, side="left")
+    hi = np.searchsorted(eg, key_anchor, side="right")
+    cnt = hi - lo
+    k = np.repeat(np.arange(len(key_anchor), dtype=np.int64), cnt)
+    pos = np.repeat(lo - np.cumsum(cnt) + cnt, cnt) + np.arange(int(cnt.sum()), dtype=np.int64)
+    u, la = eu[pos], el[pos]
+    rmax = int(max(rg.max() if len(rg) else 0, key_rel.max() if len(key_rel) else 0)) + 1
+    code = ru * rmax + rg
+    ro = np.argsort(code, kind="stable")
+    code, rlo = code[ro], rl[ro]
+    want = u * rmax + key_rel[k]
+    at = np.searchsorted(code, want)
+    at_c = np.minimum(at, max(len(code) - 1, 0))
+    ok = (at < len(code)) & (code[at_c] == want) if len(code) else np.zeros(len(want), bool)
+    out = np.empty((int(ok.sum()), 5), dtype=np.int32)
+    out[:, 0] = k[ok]
+    out[:, 1] = u[ok]
+    out[:, 2] = la[ok]
+    out[:, 3] = rlo[at_c[ok]]
+    out[:, 4] = key_side[k[ok]]
+    return out
+
+
+def lp_pair_array(parts):
+    """Concatenated lp_pairs blocks as one C-contiguous int32 [n][5] array (pt_lp_pair layout) and the
+    pointer pt_lp_min_scores takes."""
+    arr = np.ascontiguousarray(np.concatenate(parts) if parts else np.zeros((0, 5), np.int32), dtype=np.int32)
+    return arr, arr.ctypes.data_as(ctypes.POINTER(_native.LpPair))
 
 
 class _KeyStore(object):
@@ -504,12 +561,13 @@ class Parallel_Universe_Config(Tester):
             U.d_ent_remap = dr.data_ptr()
             lp_us.append(U)
             model_id, p_norm, norm_flag = kge.native_model, int(kge.p_norm), 1 if kge.norm_flag else 0
-            pairs.extend(lp_pairs(slot, em, rm, st.key_anchor, st.key_rel, st.key_side))
-        if pairs:
+            pairs.append((em, rm))
+        pair_arr, arr_p = lp_pair_array([lp_pairs_all([p[0] for p in pairs], [p[1] for p in pairs], st.key_anchor,
+                                                      st.key_rel, st.key_side)])
+        if len(pair_arr):
             arr_u = (_native.LpUniverse * len(lp_us))(*lp_us)
-            arr_p = (_native.LpPair * len(pairs))(*[_native.LpPair(*p) for p in pairs])
             tup = st.tuple if self.missing_embedding_handling == 'null_vector' else None
-            _native.check(L.pt_lp_min_scores(arr_u, len(lp_us), model_id, p_norm, norm_flag, arr_p, len(pairs),
+            _native.check(L.pt_lp_min_scores(arr_u, len(lp_us), model_id, p_norm, norm_flag, arr_p, len(pair_arr),
                                              self.ent_tot, _native.ptr(st.rows), _native.ptr(tup), _native.stream()))
         min_combine([st.rows, st.tuple])
 

@@ -10,7 +10,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from openke.config.Parallel_Universe_Config import lookup_local, lp_pairs, min_combine, universe_owner
+from openke.config.Parallel_Universe_Config import lp_pairs_all, lookup_local, lp_pairs, min_combine, universe_owner
 
 
 def _free_port():
@@ -90,8 +90,25 @@ def test_lp_pairs_match_naive_selection():
     g2l_r = {int(g): l for l, g in enumerate(rm)}
     want = [(k, 5, g2l_e[int(a)], g2l_r[int(r)], int(s)) for k, (a, r, s) in
             enumerate(zip(key_anchor, key_rel, key_side)) if int(a) in g2l_e and int(r) in g2l_r]
-    assert got == want
+    assert got.dtype == np.int32 and got.shape == (len(want), 5)   # pt_lp_pair rows
+    assert [tuple(int(x) for x in row) for row in got] == want
     assert len(want) > 0
+
+
+def test_lp_pairs_all_matches_per_universe():
+    rng = np.random.default_rng(5)
+    E, R, n_u = 300, 11, 7
+    ems = [rng.choice(E, int(rng.integers(0, 60)), replace=False) for _ in range(n_u)]
+    rms = [rng.choice(R, int(rng.integers(0, 6)), replace=False) for _ in range(n_u)]
+    key_anchor = rng.integers(0, E, 400)
+    key_rel = rng.integers(0, R, 400)
+    key_side = rng.integers(0, 2, 400)
+    want = sorted(tuple(int(x) for x in row) for s in range(n_u)
+                  for row in lp_pairs(s, ems[s], rms[s], key_anchor, key_rel, key_side))
+    got = lp_pairs_all(ems, rms, key_anchor, key_rel, key_side)
+    assert sorted(tuple(int(x) for x in row) for row in got) == want
+    assert len(want) > 0
+    assert len(lp_pairs_all([], [], key_anchor, key_rel, key_side)) == 0
 
 
 def test_lookup_local_absent_and_empty():
