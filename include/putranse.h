@@ -260,6 +260,9 @@ void importTestFiles(void);                          /* Reader.h:246-342 */
 void initTest(void);                                 /* Test.h:23-35 */
 void getHeadBatch(int64_t *ph, int64_t *pt, int64_t *pr);    /* Test.h:37-71 */
 void getTailBatch(int64_t *ph, int64_t *pt, int64_t *pr);    /* Test.h:73-107 */
+/* triple classification (TestDataLoader.sampling_tc): the test triples and one negative each, the coin
+ * and the filtered corruption drawn from sampler thread 0 (getNegTest + getTestBatch, Test.h:576-599) */
+void getTestBatch(int64_t *ph, int64_t *pt, int64_t *pr, int64_t *nh, int64_t *nt, int64_t *nr);
 void testHead(float *con, int64_t lastHead, int64_t type_constrain);   /* Test.h:118-238 */
 void testTail(float *con, int64_t lastTail, int64_t type_constrain);   /* Test.h:240-359 */
 void test_link_prediction(int64_t type_constrain);   /* Test.h:398-504 */

@@ -1393,6 +1393,81 @@ void rank_one(const pt_known &k, int64_t E, int64_t h, int64_t t, int64_t r, int
               int64_t *raw, int64_t *filt);
 }
 
+// ------------------------------------------------------------------ triple classification -------
+namespace {
+// corrupt_head / corrupt_tail with the known-triple filter (Corrupt.h:9-105, filter_flag true) over the
+// training graph's sorted lists on the host: heads = 1 draws a replacement TAIL for (key = h, r) from
+// trainHead, heads = 0 a replacement HEAD for (key = t, r) from trainTail. An entity without training
+// triples makes the reference read trainHead[-1] (its ll is -1): that is the calloc block's header,
+// larger than any entity id, so `tmp < trainHead[ll].t` holds and the draw is returned as is - emulated
+// by reading index -1 as "larger than every id" (index n, never reached by a non-empty list, likewise).
+int64_t host_corrupt(const pt::Graph &g, bool heads, int64_t key, int64_t r, uint64_t &state) {
+    const std::vector<pt::Triple> &L = heads ? g.head : g.tail;
+    const std::vector<int64_t> &lef = heads ? g.lef_head : g.lef_tail, &rig = heads ? g.rig_head : g.rig_tail;
+    const int64_t n = (int64_t)L.size();
+    auto val = [&](int64_t k) -> int64_t {
+        if (k < 0 || k >= n) return INT64_MAX / 4;
+        return heads ? L[(size_t)k].t : L[(size_t)k].h;
+    };
+    int64_t lo = lef[(size_t)key] - 1, hi = rig[(size_t)key], mid;
+    while (lo + 1 < hi) {
+        mid = (lo + hi) >> 1;
+        if (L[(size_t)mid].r >= r) hi = mid; else lo = mid;
+    }
+    const int64_t ll = hi;
+    lo = lef[(size_t)key];
+    hi = rig[(size_t)key] + 1;
+    while (lo + 1 < hi) {
+        mid = (lo + hi) >> 1;
+        if (L[(size_t)mid].r <= r) lo = mid; else hi = mid;
+    }
+    const int64_t rr = lo;
+    state = state * 25214903917ULL + 11ULL;   // randd (Random.h:18-22)
+    const int64_t tmp = (int64_t)(state % (uint64_t)(g.ent_total - (rr - ll + 1)));
+    if (tmp < val(ll)) return tmp;
+    if (tmp > val(rr) - rr + ll - 1) return tmp + rr - ll + 1;
+    lo = ll;
+    hi = rr + 1;
+    while (lo + 1 < hi) {
+        mid = (lo + hi) >> 1;
+        if (val(mid) - mid + ll - 1 < tmp) lo = mid; else hi = mid;
+    }
+    return tmp + lo - ll + 1;
+}
+}  // namespace
+
+// getTestBatch (Test.h:576-599): the test triples and one negative each - a coin from sampler thread 0
+// (randd(0) % 1000 < 500) picks corrupt_head(0, h, r) (new tail) or corrupt_tail(0, t, r) (new head).
+// The stream is the process-global sampler's thread 0 (device-resident here: read, advanced, written
+// back), so the negatives continue the same random sequence as in the reference.
+extern "C" void getTestBatch(int64_t *ph, int64_t *pt_, int64_t *pr, int64_t *nh, int64_t *nt, int64_t *nr) {
+    Legacy &l = L();
+    std::lock_guard<std::mutex> lk(l.mu);
+    pt::Graph *g = l.train.get();
+    if (!g || g->ent_total < 2) {
+        legacy_err(pt::fail(PT_ESTATE, "getTestBatch: importTrainFiles() first"));
+        return;
+    }
+    uint64_t s0 = l.states.empty() ? 0 : l.states[0];
+    if (l.sampler_ready && hipMemcpy(&s0, l.sampler.d_states, sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) {
+        legacy_err(pt::fail(PT_EHIP, "getTestBatch: reading the sampler state failed"));
+        return;
+    }
+    for (size_t i = 0; i < l.test.size(); ++i) {
+        const pt::Triple &q = l.test[i];
+        pt::Triple neg = q;
+        s0 = s0 * 25214903917ULL + 11ULL;
+        if ((int64_t)(s0 % 1000ULL) < 500) neg.t = host_corrupt(*g, true, q.h, q.r, s0);
+        else neg.h = host_corrupt(*g, false, q.t, q.r, s0);
+        ph[i] = q.h; pt_[i] = q.t; pr[i] = q.r;
+        nh[i] = neg.h; nt[i] = neg.t; nr[i] = neg.r;
+    }
+    if (!l.states.empty()) l.states[0] = s0;
+    if (l.sampler_ready &&
+        hipMemcpy(l.sampler.d_states, &s0, sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
+        legacy_err(pt::fail(PT_EHIP, "getTestBatch: writing the sampler state failed"));
+}
+
 extern "C" void initTest(void) {
     Legacy &l = L();
     l.last_head = l.last_tail = 0;

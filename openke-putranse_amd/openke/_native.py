@@ -129,6 +129,7 @@ SIGNATURES = {
     "initTest": (None, []),
     "getHeadBatch": (None, [c_vp, c_vp, c_vp]),
     "getTailBatch": (None, [c_vp, c_vp, c_vp]),
+    "getTestBatch": (None, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "testHead": (None, [c_vp, c_i64, c_i64]),
     "testTail": (None, [c_vp, c_i64, c_i64]),
     "test_link_prediction": (None, [c_i64]),

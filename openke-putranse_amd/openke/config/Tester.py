@@ -108,5 +108,75 @@ class Tester(object):
         print(hit10)
         return mrr, mr, hit10, hit3, hit1
 
+    # ---------------------------------------------------------------- triple classification -----
+    # Tester.py:95-191. Scores come from the model's GPU predict (one launch per batch); the threshold
+    # search and accuracy are the reference's sorted sweeps, restated vectorized over the same
+    # np.argsort order (identical results, ties included).
+    def determine_classification_cross_table_values(self, res, threshold):
+        pred = res[:, 1] < threshold
+        ans = res[:, 0] == 1
+        print("True Positives :{}".format(int(np.sum(pred & ans))))
+        print("True Negatives :{}".format(int(np.sum(~pred & ~ans))))
+        print("False Positives :{}".format(int(np.sum(pred & ~ans))))
+        print("False Negatives :{}".format(int(np.sum(~pred & ans))))
+
+    def get_best_threshlod(self, score, ans):
+        res = np.concatenate([ans.reshape(-1, 1), score.reshape(-1, 1)], axis=-1)
+        order = np.argsort(score)
+        res = res[order]
+        total_all = float(len(score))
+        total_true = np.sum(ans)
+        total_false = total_all - total_true
+        if len(res) == 0:
+            return None, 0.0
+        # res_current at index i = (2 * #positives in res[:i+1] + total_false - i - 1) / total_all; the
+        # loop keeps the first strict maximum above 0
+        cur = np.cumsum(res[:, 0] == 1).astype(np.float64)
+        idx = np.arange(len(res), dtype=np.float64)
+        val = (2 * cur + total_false - idx - 1) / total_all
+        best = int(np.argmax(val))
+        if not val[best] > 0.0:
+            return None, 0.0
+        return res[best, 1], float(val[best])
+
     def run_triple_classification(self, threshlod=None, data_iterator=None):
-        raise NotImplementedError("triple classification is outside the accelerated path")
+        self.lib.initTest()
+        score = []
+        ans = []
+        if data_iterator is None:
+            self.data_loader.set_sampling_mode('classification')
+            data_iterator = self.data_loader
+        for pos_ins, neg_ins in data_iterator:
+            res_pos = self.test_one_step(pos_ins)
+            ans = ans + [1 for _ in range(len(res_pos))]
+            score.append(res_pos)
+            res_neg = self.test_one_step(neg_ins)
+            ans = ans + [0 for _ in range(len(res_neg))]
+            score.append(res_neg)
+        score = np.concatenate(score, axis=-1)
+        ans = np.array(ans)
+        if threshlod is None:
+            threshlod, _ = self.get_best_threshlod(score, ans)
+        res = np.concatenate([ans.reshape(-1, 1), score.reshape(-1, 1)], axis=-1)
+        order = np.argsort(score)
+        res = res[order]
+        total_all = float(len(score))
+        total_true = np.sum(ans)
+        total_false = total_all - total_true
+        # special handling of parallel-universe scores that are all +inf (Tester.py:166-173)
+        if threshlod == float("inf") and len(score[score == float("inf")]) == len(score):
+            if total_true == 0:
+                return 1.0, threshlod
+            if total_false == 0:
+                return 0.0, threshlod
+            elif total_false == total_true:
+                return 0.5, threshlod
+        acc = 0
+        above = np.nonzero(res[:, 1] > threshlod)[0] if threshlod is not None else np.zeros(0, dtype=np.int64)
+        if len(above):
+            index = int(above[0])
+            total_current = float(np.sum(res[:index, 0] == 1))
+            acc = (2 * total_current + total_false - index) / total_all
+        if threshlod is not None:
+            self.determine_classification_cross_table_values(res, threshlod)
+        return acc, threshlod

@@ -1,5 +1,7 @@
 # coding:utf-8
-"""Link-prediction data loader (mirror of openke/data/TestDataLoader.py of the reference).
+"""Evaluation data loader (mirror of openke/data/TestDataLoader.py of the reference): link-prediction
+batches (sampling_lp) and triple-classification batches (sampling_tc: the test triples and one filtered
+negative each from the library's getTestBatch, Test.h:576-599).
 
 read() has the reference's side effects on the global context (re-seeding the sampler with its
 random_seed, default 4, and re-importing the training set, TestDataLoader.py:276-290)."""
@@ -64,6 +66,9 @@ class TestDataLoader(object):
             self.test_h = np.zeros(E, dtype=np.int64)
             self.test_t = np.zeros(E, dtype=np.int64)
             self.test_r = np.zeros(E, dtype=np.int64)
+            n = self.testTotal
+            self.test_pos_h, self.test_pos_t, self.test_pos_r = (np.zeros(n, dtype=np.int64) for _ in range(3))
+            self.test_neg_h, self.test_neg_t, self.test_neg_r = (np.zeros(n, dtype=np.int64) for _ in range(3))
         elif self.mode == 'valid':
             self.validTotal = self.lib.getValidTotal()
             self.valid_h = np.zeros(E, dtype=np.int64)
@@ -89,7 +94,15 @@ class TestDataLoader(object):
         return res
 
     def sampling_tc(self):
-        raise NotImplementedError("triple classification is outside the accelerated path")
+        """TestDataLoader.py:186-205: every test triple and one negative (the same buffers each call)."""
+        if self.mode != 'test':
+            raise NotImplementedError("triple classification samples the test split (the reference's only mode)")
+        self.lib.getTestBatch(self._addr(self.test_pos_h), self._addr(self.test_pos_t), self._addr(self.test_pos_r),
+                              self._addr(self.test_neg_h), self._addr(self.test_neg_t), self._addr(self.test_neg_r))
+        return [
+            {"batch_h": self.test_pos_h, "batch_t": self.test_pos_t, "batch_r": self.test_pos_r, "mode": "normal"},
+            {"batch_h": self.test_neg_h, "batch_t": self.test_neg_t, "batch_r": self.test_neg_r, "mode": "normal"},
+        ]
 
     def eval_triples(self):
         """(h, t, r) int64 arrays of this loader's split in the reference's ranking order."""
@@ -125,4 +138,5 @@ class TestDataLoader(object):
                 self.lib.validInit()
                 eval_total = self.validTotal
             return TestDataSampler(eval_total, self.sampling_lp)
-        raise NotImplementedError("triple classification is outside the accelerated path")
+        self.lib.initTest()
+        return TestDataSampler(1, self.sampling_tc)

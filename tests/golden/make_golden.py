@@ -71,6 +71,13 @@ LP_CASES = [
 ]
 
 
+TC_CASES = [
+    # name, model, dim, p_norm, torch_seed
+    ("c1", "TransE", 16, 1, 31),
+    ("c2", "TransH", 12, 2, 32),
+]
+
+
 def _import_reference(tmp):
     dst = os.path.join(tmp, "openke")
     if not os.path.exists(dst):
@@ -236,12 +243,34 @@ def case_lp(out, name, model, dim, p, tseed):
                         metrics=np.array(res, dtype=np.float64), **tables)
 
 
+def case_tc(out, name, model, dim, p, tseed):
+    """Tester.run_triple_classification on a random-init model (Tester.py:142-191), then one more
+    getTestBatch call of the same loader (the negatives continue the thread-0 stream)."""
+    import torch
+    from openke.config import Tester
+    from openke.data import TestDataLoader
+    from openke.module.model import TransE, TransH
+    test_dl = TestDataLoader(DATASETS["small"], "classification")
+    torch.manual_seed(tseed)
+    cls = TransE if model == "TransE" else TransH
+    kge = cls(ent_tot=test_dl.get_ent_tot(), rel_tot=test_dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=True)
+    tables = {k.split(".")[0]: v.detach().numpy().copy() for k, v in kge.state_dict().items()
+              if "embeddings" in k or "norm_vector" in k}
+    tester = Tester(model=kge, data_loader=test_dl, use_gpu=False)
+    acc, thr = tester.run_triple_classification()
+    pos, neg = next(iter(test_dl))
+    np.savez_compressed(out, model=model, dim=dim, p_norm=p, torch_seed=tseed, acc=float(acc), threshold=float(thr),
+                        pos_h=pos["batch_h"].copy(), pos_t=pos["batch_t"].copy(), pos_r=pos["batch_r"].copy(),
+                        neg_h=neg["batch_h"].copy(), neg_t=neg["batch_t"].copy(), neg_r=neg["batch_r"].copy(),
+                        **tables)
+
+
 def run_case(kind, args_json, out, tmp):
     args = json.loads(args_json)
     _import_reference(tmp)
     _silence()
     {"glibc": case_glibc, "sampler": case_sampler, "train": case_train, "universes": case_universes,
-     "lp": case_lp}[kind](out, *args)
+     "lp": case_lp, "tc": case_tc}[kind](out, *args)
 
 
 def main():
@@ -255,6 +284,7 @@ def main():
     jobs += [("train", list(c), "train_%s.npz" % c[0]) for c in TRAIN_CASES]
     jobs += [("universes", list(c), "universes_%s.npz" % c[0]) for c in UNIVERSE_CASES]
     jobs += [("lp", list(c), "lp_%s.npz" % c[0]) for c in LP_CASES]
+    jobs += [("tc", list(c), "tc_%s.npz" % c[0]) for c in TC_CASES]
     only = sys.argv[1:]
     for kind, args, fname in jobs:
         if only and not any(fname.startswith(o) for o in only):

@@ -345,3 +345,31 @@ def test_counting_sort_step_matches_oracle(case):
     orc = {"ent": ent, "rel": rel, "norm": nv}
     for k, v in got.items():
         assert_tables_close(v, orc[k], 2e-5, ill.get(k) if opt == "adagrad" else None)
+
+
+@pytest.mark.parametrize("path", golden("tc_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_triple_classification_matches_reference(path):
+    """Tester.run_triple_classification (Tester.py:142-191) with the classification loader: the GPU
+    scores, the reference's threshold sweep and accuracy; then the next getTestBatch negatives
+    (filtered corruption on sampler thread 0, Test.h:576-599) bit-exact with the reference's."""
+    from openke.config import Tester
+    from openke.data import TestDataLoader
+    from openke.module.model import TransE, TransH
+    z = load(path)
+    dl = TestDataLoader(KG_SMALL, "classification")
+    cls = TransE if str(z["model"]) == "TransE" else TransH
+    kge = cls(ent_tot=dl.get_ent_tot(), rel_tot=dl.get_rel_tot(), dim=int(z["dim"]), p_norm=int(z["p_norm"]),
+              norm_flag=True)
+    with torch.no_grad():
+        kge.ent_embeddings.weight.copy_(torch.from_numpy(z["ent_embeddings"]))
+        kge.rel_embeddings.weight.copy_(torch.from_numpy(z["rel_embeddings"]))
+        if hasattr(kge, "norm_vector"):
+            kge.norm_vector.weight.copy_(torch.from_numpy(z["norm_vector"]))
+    tester = Tester(model=kge, data_loader=dl, use_gpu=True)
+    acc, thr = tester.run_triple_classification()
+    assert abs(acc - float(z["acc"])) < 1e-12, (acc, float(z["acc"]))
+    np.testing.assert_allclose(float(thr), float(z["threshold"]), rtol=1e-5)
+    pos, neg = next(iter(dl))
+    for k in ("h", "t", "r"):
+        np.testing.assert_array_equal(pos["batch_" + k], z["pos_" + k])
+        np.testing.assert_array_equal(neg["batch_" + k], z["neg_" + k])
