@@ -657,7 +657,54 @@ class Parallel_Universe_Config(Tester):
     def test_one_step(self, data):
         if data['mode'] in ('head_batch', 'tail_batch'):
             return self.global_energy_estimation(data)
-        raise NotImplementedError("triple classification ('normal' mode) is outside the accelerated path")
+        if data['mode'] != 'normal':
+            raise ValueError("unknown evaluation mode %r" % (data['mode'],))
+        # Parallel_Universe_Config.py:714-731. The reference unpacks `head, tail, rel = batch_h[i],
+        # batch_r[i], batch_t[i]` and calls predict_triple(head, rel, tail): the triple it scores is
+        # (h, relation = batch_t[i], tail = batch_r[i]). Kept as is (results identical to the reference).
+        bh = np.asarray(data['batch_h'], dtype=np.int64)
+        bt = np.asarray(data['batch_t'], dtype=np.int64)
+        br = np.asarray(data['batch_r'], dtype=np.int64)
+        heads, rels, tails = bh, bt, br
+        score = self._predict_triples(heads, rels, tails)
+        if self.missing_embedding_handling == "null_vector":
+            for i in np.nonzero(score == np.inf)[0]:
+                a = self.predict_tuple(int(heads[i]), int(rels[i]), mode="tail_batch")
+                b = self.predict_tuple(int(tails[i]), int(rels[i]), mode="head_batch")
+                score[i] = a if a < b else b
+        return score
+
+    def _predict_triples(self, heads, rels, tails):
+        """predict_triple for many triples (Parallel_Universe_Config.py:413-442): min over the universes
+        holding the head, the relation and the tail of that universe's score, +inf where none; one GPU
+        predict launch per universe over all of its triples."""
+        out = np.full(len(heads), np.inf, dtype=np.float32)
+        per_u = defaultdict(list)
+        for i in range(len(heads)):
+            for u in self.gather_embedding_spaces(int(heads[i]), int(rels[i]), int(tails[i])):
+                if u in self.trained_embedding_spaces:
+                    per_u[u].append(i)
+        for u in sorted(per_u):
+            idx = np.asarray(per_u[u], dtype=np.int64)
+            em, rm, eg, eo, rg, ro = self._remaps(u)
+            sp = self.trained_embedding_spaces[u]
+            s = sp.predict({"batch_h": lookup_local(eg, eo, heads[idx]), "batch_t": lookup_local(eg, eo, tails[idx]),
+                            "batch_r": lookup_local(rg, ro, rels[idx]), "mode": "normal"})
+            out[idx] = np.minimum(out[idx], np.asarray(s, dtype=np.float32).reshape(-1))
+        return out
+
+    def predict_tuple(self, ent_id, rel_id, mode):
+        """Parallel_Universe_Config.py:390-411: min over the universes holding the entity and the relation
+        of the null-vector tuple score."""
+        best = float("inf")
+        for u in self.gather_embedding_spaces(ent_id, rel_id):
+            sp = self.trained_embedding_spaces.get(u)
+            if sp is None:
+                continue
+            s = float(self.calc_tuple_score(self.entity_id_mappings[u][ent_id], self.relation_id_mappings[u][rel_id],
+                                            mode, sp).reshape(-1)[0])
+            best = s if s < best else best
+        return best
 
     def run_link_prediction(self, type_constrain=False):
         if type_constrain:
@@ -679,7 +726,11 @@ class Parallel_Universe_Config(Tester):
         return mrr, mr, hit10, hit3, hit1
 
     def run_triple_classification(self, threshlod=None):
-        raise NotImplementedError("triple classification is outside the accelerated path")
+        # Parallel_Universe_Config.py:745-749 (the static split; the incremental-file variants are outside
+        # the accelerated path)
+        acc, threshlod = super().run_triple_classification(threshlod)
+        print("Accuracy is: {}".format(acc))
+        return acc, threshlod
 
     def reset_evaluation_helpers(self):
         self.current_validated_universes = 0

@@ -140,7 +140,7 @@ class Tester(object):
         return res[best, 1], float(val[best])
 
     def run_triple_classification(self, threshlod=None, data_iterator=None):
-        self.lib.initTest()
+        (getattr(self, "lib", None) or _native.lib()).initTest()
         score = []
         ans = []
         if data_iterator is None:

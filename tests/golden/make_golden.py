@@ -214,6 +214,12 @@ def case_universes(out, name, model, dim, p, n_univ, min_tc, max_tc, epochs, see
         dl.reset_universe()
     mrr_etc = pu_lp(pu)
     rec["lp"] = np.array(mrr_etc, dtype=np.float64)
+    # triple classification over the universes (Parallel_Universe_Config.py:745-749 -> Tester.py:142-191)
+    # from a fixed C RNG state (the negatives come from sampler thread 0)
+    pu.set_random_seed(4321)
+    acc, thr = pu.run_triple_classification()
+    rec["tc_acc"] = float(acc)
+    rec["tc_threshold"] = float(thr) if thr is not None else np.nan
     np.savez_compressed(out, model=model, dim=dim, p_norm=p, min_tc=min_tc, max_tc=max_tc, epochs=epochs, seed=seed,
                         **rec)
 

@@ -334,3 +334,22 @@ def test_universe_job_validation_errors():
     with pytest.raises(_native.NativeError):
         _native.check(L.pt_universes_train(arr, 1, 0, 1, 1, _native.PT_ADAGRAD, 0, 0, None, _native.stream()))
     assert b"null" in L.pt_last_error()
+
+
+@pytest.mark.parametrize("path", golden("universes_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_pu_triple_classification_matches_reference(path, tmp_path):
+    """run_triple_classification over the reference's trained universes from a fixed C RNG state (the
+    negatives come from sampler thread 0): accuracy and threshold == the reference's. The reference
+    scores 'normal' triples as (h, relation = batch_t, tail = batch_r) (its test_one_step unpacking,
+    Parallel_Universe_Config.py:718), which the drop-in keeps."""
+    z = load(path)
+    pu = _pu(z, tmp_path)
+    _inject_reference_universes(pu, z)
+    pu.set_random_seed(4321)
+    acc, thr = pu.run_triple_classification()
+    assert acc == float(z["tc_acc"]), (acc, float(z["tc_acc"]))
+    want = float(z["tc_threshold"])
+    if np.isinf(want) or np.isnan(want):
+        assert (thr is None and np.isnan(want)) or float(thr) == want, (thr, want)
+    else:
+        np.testing.assert_allclose(float(thr), want, rtol=1e-5)
