@@ -452,11 +452,15 @@ def main():
     # per-step kernels launched one by one with an event pair around each; per-chunk sampling/scan
     # launches amortised over the steps they serve
     ms4 = (ctypes.c_float * 4)()
-    n_t = min(50, args.steps)
+    n_t = min(256, args.steps)   # the timed run's chunking (sampling launches cover up to 256 steps)
     tl = torch.zeros(n_t, device=dev)
     _native.check(L.pt_trainer_run_timed(tr._native, sampler, bs, neg, bern, filt, n_t, _native.ptr(tl), ms4,
                                          _native.stream()))
-    names = ["k_sample_csr", "k_scan_counts", "k_step_csr", "k_apply_buf"]
+    # fused LDS sampling + sort (then the stream advance) once a chunk holds >= 96 steps, else the
+    # two-pass form (capi.cpp kSampleSortMinCalls)
+    fused = n_t >= 96 and os.environ.get("PT_SAMPLE_TWO_PASS", "0") in ("", "0")
+    names = (["k_sample_sort", "k_advance"] if fused else ["k_sample_csr", "k_scan_counts"]) + \
+        ["k_step_csr", "k_apply_buf"]
     per_kernel = {n: float(v) for n, v in zip(names, ms4) if v > 0}
     bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
     achieved = bytes_step / (sum(per_kernel.values()) * 1e-3) / 1e9

@@ -65,6 +65,7 @@ struct pt_trainer {
     size_t csr_cap = 0;
     pt::CsrWork csr{};
     int64_t csr_bs = 0, csr_neg = 0, csr_chunk = 0;   // layout the workspace was carved for
+    bool csr_fused = false;                             // k_sample_sort plan fits LDS
     int64_t lpart_cap = 0;                             // W.lpart capacity (positives)
     int device = -1;
     hipStream_t cap = nullptr;
@@ -263,6 +264,9 @@ extern "C" int pt_trainer_update_desc(pt_trainer *t, const pt_model_desc *m) {
 
 
 static const int64_t kCsrChunk = 256;   // steps pre-sampled per sampling/scan launch pair
+// the fused sampling kernel runs one workgroup per call (~260 us each at C2, latency-bound draws), so it
+// only beats the two-pass form (~3.1 us per call) once a chunk fills enough CUs
+static const int64_t kSampleSortMinCalls = 96;
 
 // Workspace of the counting-sort path, carved once per (bs, neg): room for a chunk of pre-sampled
 // steps (<= kCsrChunk, fewer when a step's arrays are large) plus one step's gradient rows. A new
@@ -300,6 +304,10 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     t->csr_bs = bs;
     t->csr_neg = neg;
     t->csr_chunk = chunk;
+    // sampling + counting sort fused in LDS when its plan fits (sets the kernel's LDS attribute here,
+    // outside any stream capture); PT_SAMPLE_TWO_PASS=1 forces the two-pass form
+    const char *tp = getenv("PT_SAMPLE_TWO_PASS");
+    t->csr_fused = !(tp && atoi(tp) != 0) && pt::sample_sort_prepare(bs, E, ss);
     return PT_OK;
 }
 
@@ -359,9 +367,17 @@ static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, in
         const int64_t chunk = t->csr_chunk;
         for (int64_t c0 = 0; c0 < steps; c0 += chunk) {
             const int64_t calls = std::min(chunk, steps - c0);
-            PT_TIMED(0, pt::launch_sample_csr(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls,
-                                              t->csr, st));
-            PT_TIMED(1, pt::launch_scan_counts(t->csr, P.ent_total, calls, s->d_states, s->threads, bs, dpp, st));
+            // sampling + counting sort in LDS, one workgroup per call (then the stream advance), or the
+            // two-pass form (global-atomic counts, separate scan) when the LDS plan does not fit
+            if (t->csr_fused && calls >= kSampleSortMinCalls) {
+                PT_TIMED(0, pt::launch_sample_sort(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter,
+                                                   calls, P.ent_total, t->csr, st));
+                PT_TIMED(1, pt::launch_advance(s->d_states, s->threads, bs, dpp * calls, st));
+            } else {
+                PT_TIMED(0, pt::launch_sample_csr(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls,
+                                                  t->csr, st));
+                PT_TIMED(1, pt::launch_scan_counts(t->csr, P.ent_total, calls, s->d_states, s->threads, bs, dpp, st));
+            }
             for (int64_t j = 0; j < calls; ++j) {
                 const pt::CsrWork v = pt::csr_view(t->csr, j, bs, neg);
                 float *loss = d_losses ? d_losses + c0 + j : nullptr;

@@ -95,6 +95,12 @@ hipError_t launch_spin(int64_t us, hipStream_t st);
 hipError_t launch_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t dpp, hipStream_t st);
 hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                              int bern, int filter, int64_t calls, const CsrWork &w, hipStream_t st);
+// one workgroup per call: sampling + LDS counting sort + scan; the streams are NOT advanced (launch_advance).
+// sample_sort_prepare: whether the LDS plan fits for (bs, n) (and the kernel's LDS limit is raised);
+// otherwise use launch_sample_csr + launch_scan_counts
+bool sample_sort_prepare(int64_t bs, int64_t n, int64_t start_stride);
+hipError_t launch_sample_sort(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
+                              int bern, int filter, int64_t calls, int64_t n, const CsrWork &w, hipStream_t st);
 hipError_t launch_scan_counts(const CsrWork &w, int64_t n, int64_t calls, uint64_t *states, int64_t threads,
                               int64_t bs, int64_t dpp, hipStream_t st);
 bool step_fits(const StepParams &P, int64_t neg, bool csr);

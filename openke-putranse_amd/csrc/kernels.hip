@@ -85,6 +85,73 @@ __global__ __launch_bounds__(256) void k_sample_csr(DeviceGraph g, const uint64_
     w.off[o] = atomicAdd(&w.cnt[call * w.cnt_stride + e], 1);
 }
 
+// Sampling + counting sort of one sampled call per workgroup, entirely in LDS (when the bucket counts
+// and the call's positives fit): the positives are drawn once (not once per slot), every slot's
+// negative reserves its rank with an LDS atomic, the counts are scanned in LDS and every slot's
+// destination resolved - the same pos / neg / start / destination arrays as k_sample_csr +
+// k_scan_counts, without the 52,000 returning global atomics per call and the second pass.
+// The sampler streams are read only; the caller advances them afterwards (k_advance).
+__global__ __launch_bounds__(1024) void k_sample_sort(DeviceGraph g, const uint64_t *__restrict__ states,
+                                                      int64_t threads, int64_t bs, int64_t neg, int bern, int filter,
+                                                      int64_t n, CsrWork w) {
+    extern __shared__ __attribute__((aligned(16))) int32_t lds[];
+    __shared__ int32_t wtot[16];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t call = blockIdx.x;
+    int32_t *cnt = lds;                                                  // [n] counts, then starts
+    int32_t *pi = lds + ((n + 3) & ~int64_t(3));                         // [bs][8]: h r t hr_lo hr_hi tr_lo tr_hi -
+    uint64_t *ps = reinterpret_cast<uint64_t *>(pi + 8 * bs);            // [bs] stream state after the index draw
+    for (int64_t i = tid; i < n; i += 1024) cnt[i] = 0;
+    const int64_t dpp = 1 + 2 * neg;
+    for (int64_t b = tid; b < bs; b += 1024) {
+        const PosDraw pd = draw_positive(g, states, threads, bs, b, dpp, call);
+        int32_t *q = pi + 8 * b;
+        q[0] = (int32_t)pd.h; q[1] = (int32_t)pd.r; q[2] = (int32_t)pd.t;
+        q[3] = pd.hr_lo; q[4] = pd.hr_hi; q[5] = pd.tr_lo; q[6] = pd.tr_hi;
+        ps[b] = pd.s1;
+        w.pos[call * bs + b] = make_int4((int)pd.h, (int)pd.r, (int)pd.t, 0);
+    }
+    __syncthreads();
+    const int64_t slots = bs * neg;
+    int32_t *nrec = w.neg + call * slots;
+    int32_t *noff = w.off + call * slots;
+    for (int64_t o = tid; o < slots; o += 1024) {
+        const int64_t b = o / neg, k = o - b * neg;
+        const int32_t *q = pi + 8 * b;
+        const PosDraw pd{q[0], q[1], q[2], q[3], q[4], q[5], q[6], ps[b]};
+        int side;
+        const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
+        nrec[o] = (int32_t)((e << 1) | side);
+        noff[o] = atomicAdd(&cnt[e], 1);
+    }
+    __syncthreads();
+    // exclusive scan of cnt[0, n): contiguous chunks per thread, wave shuffles, LDS wave totals
+    const int64_t per = (n + 1023) / 1024;
+    const int64_t lo = tid * per, hi = lo + per < n ? lo + per : n;
+    int32_t tsum = 0;
+    for (int64_t i = lo; i < hi; ++i) tsum += cnt[i];
+    int32_t incl = tsum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wtot[wid] = incl;
+    __syncthreads();
+    int32_t run = incl - tsum;
+    for (int q = 0; q < wid; ++q) run += wtot[q];
+    int32_t *start = w.start + call * w.start_stride;
+    for (int64_t i = lo; i < hi; ++i) {
+        const int32_t c = cnt[i];
+        cnt[i] = run;
+        start[i] = run;
+        run += c;
+    }
+    if (tid == 1023) start[n] = run;   // the last thread's chunk ends at n (or is empty): run = total
+    __syncthreads();
+    for (int64_t o = tid; o < slots; o += 1024) noff[o] = cnt[nrec[o] >> 1] + noff[o];
+}
+
 // exclusive scan of the bucket sizes (one workgroup of 1024 threads, tiles of 16384 counts: 16
 // contiguous counts per thread, wave shuffles for the thread totals, LDS for the 16 wave totals),
 // zeroing the counts for the next step; also advances the sampler streams by this call's draws
@@ -415,6 +482,26 @@ hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64
     const int64_t n = calls * bs * (neg + 1);
     hipLaunchKernelGGL(dev::k_sample_csr, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, states, threads, bs,
                        neg, bern, filter, calls, w);
+    return hipGetLastError();
+}
+
+static size_t sample_sort_lds(int64_t bs, int64_t n) {
+    return 4 * (size_t)((n + 3) & ~int64_t(3)) + 40 * (size_t)bs;   // counts + (h r t hr tr) + stream state
+}
+static const size_t kSampleSortLds = 150 * 1024;
+
+bool sample_sort_prepare(int64_t bs, int64_t n, int64_t start_stride) {
+    if (sample_sort_lds(bs, n) > kSampleSortLds || n + 1 > start_stride || n >= (int64_t(1) << 30)) return false;
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_sample_sort),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSampleSortLds) == hipSuccess;
+}
+
+hipError_t launch_sample_sort(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
+                              int bern, int filter, int64_t calls, int64_t n, const CsrWork &w, hipStream_t st) {
+    const size_t lds = sample_sort_lds(bs, n);
+    if (lds > kSampleSortLds || n + 1 > w.start_stride) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(dev::k_sample_sort, dim3((unsigned)calls), dim3(1024), lds, st, g, states, threads, bs, neg,
+                       bern, filter, n, w);
     return hipGetLastError();
 }
 

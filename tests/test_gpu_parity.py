@@ -373,3 +373,46 @@ def test_triple_classification_matches_reference(path):
     for k in ("h", "t", "r"):
         np.testing.assert_array_equal(pos["batch_" + k], z["pos_" + k])
         np.testing.assert_array_equal(neg["batch_" + k], z["neg_" + k])
+
+
+# The fused LDS sampling + counting-sort kernel (k_sample_sort, taken once a run pre-samples >= 96 steps
+# in one chunk) against the two-pass form (k_sample_csr + k_scan_counts, PT_SAMPLE_TWO_PASS=1) and the
+# oracle over 120 steps: both forms draw the same batches (the per-step losses agree to float rounding:
+# only the order of the gradient sums inside an entity's bucket may differ) and land on the oracle's
+# tables. Tolerance: 1e-5 relative on every step's loss, 1e-4 absolute on the tables after 120 SGD steps.
+@pytest.mark.parametrize("model", ["TransE", "TransH"])
+def test_fused_sample_sort_matches_two_pass_and_oracle(model, monkeypatch):
+    from openke.config import Trainer
+    from openke.module.loss import MarginLoss
+    from openke.module.model import TransE, TransH
+    from openke.module.strategy import NegativeSampling
+    dim, p, bs, neg, steps, lr, margin, seed = 20, 1, 64, 5, 120, 0.05, 4.0, 5
+    cls = TransE if model == "TransE" else TransH
+    runs = {}
+    for two_pass in ("0", "1"):
+        monkeypatch.setenv("PT_SAMPLE_TWO_PASS", two_pass)
+        dl = _loader_path(KG_SMALL, 8, bs, neg, 1, 1, seed)
+        dl.nbatches = steps
+        torch.manual_seed(19)
+        kge = cls(dl.get_ent_tot(), dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=True)
+        t0 = _tables(kge)
+        ns = NegativeSampling(model=kge, loss=MarginLoss(margin=margin), batch_size=bs)
+        tr = Trainer(model=ns, data_loader=dl, train_times=1, alpha=lr, use_gpu=True, opt_method="sgd")
+        tr.run()
+        runs[two_pass] = (tr.last_epoch_loss, _tables(kge), t0)
+    (lf, tf, t0), (lt, tt, _) = runs["0"], runs["1"]
+    np.testing.assert_allclose(lf, lt, rtol=1e-5)
+    kg = oracle.KG.load(KG_SMALL)
+    st = oracle.GlibcRand(seed).rand_reset(8)
+    ent, rel = t0["ent"].copy(), t0["rel"].copy()
+    nv = t0["norm"].copy() if model == "TransH" else None
+    loss = 0.0
+    for _ in range(steps):
+        h, t, r, _ = kg.sample(st, 8, bs, neg, 1, 1)
+        loss += oracle.train_step(model, p, True, "sgd", lr, margin, ent, rel, nv, (None, None, None), h, t, r,
+                                  bs, neg)
+    np.testing.assert_allclose(lf, loss, rtol=1e-5)
+    orc = {"ent": ent, "rel": rel, "norm": nv}
+    for k in tf:
+        np.testing.assert_allclose(tf[k], tt[k], atol=1e-4, rtol=0)
+        np.testing.assert_allclose(tf[k], orc[k], atol=1e-4, rtol=0)

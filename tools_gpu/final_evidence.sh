@@ -18,3 +18,6 @@ for wl in c3 c4 c5; do step bench_$wl 400 python bench.py --workload $wl --steps
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 step prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-c3
 step prof_c3 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --workload c3 --steps 2 --warmup 1 --no-cpu-baseline
+bash tools_gpu/pmc.sh c2 --no-c3 || exit $?
+python3 tools_gpu/parse_pmc.py gpurun_out/pmc gpurun_out/pmc_c2.json > gpurun_out/pmc_summary.json 2>&1
+echo "pmc done" >> gpurun_out/steps.log

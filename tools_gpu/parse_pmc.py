@@ -34,7 +34,7 @@ print(json.dumps(out, indent=1))
 # FETCH_SIZE / WRITE_SIZE are kilobytes; on gfx950 FETCH_SIZE counts half the bytes of wide coalesced
 # reads, so it is doubled; WRITE_SIZE is exact for streaming stores and float atomics)
 if len(sys.argv) > 2:
-    step_kernels = ("k_sample_csr", "k_scan_counts", "k_step_csr", "k_step_sampled", "k_apply")
+    step_kernels = ("k_sample_csr", "k_scan_counts", "k_sample_sort", "k_advance", "k_step_csr", "k_step_sampled", "k_apply")
     fetch = write = 0.0
     steps = 0
     for k, d in vals.items():
@@ -49,7 +49,7 @@ if len(sys.argv) > 2:
                "fetch_kb_per_step_raw": fetch / steps, "write_kb_per_step": write / steps,
                "steps_counted": steps,
                "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py; "
-                         "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B summed over k_sample_csr, k_scan_counts, "
+                         "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B summed over k_sample_sort, k_advance, k_sample_csr, k_scan_counts, "
                          "k_step_csr, k_apply_buf dispatches / k_step_csr dispatches",
                "per_kernel": {k.split("(")[0][-60:]: {cn: sum(v) / len(v) for cn, v in d.items()}
                               for k, d in vals.items() if any(s in k for s in step_kernels)}}
