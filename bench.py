@@ -227,7 +227,9 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True):
            "steps": args.c3_steps, "warmup": args.c3_warmup, "s_per_step": el / args.c3_steps,
            "universes_per_gpu": len(own), "host_universe_build_s": build_s,
            "roofline": {"bound": "latency (per-universe dependent step chain)", "achieved_per_gpu": achieved,
-                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}}
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                        "note": "algorithmic bytes per wall second vs HBM peak; a universe's tables, state and "
+                                "contribution slots live in LDS, so frac > 1 (C4) means on-chip service, not HBM"}}
     if do_lp:
         out["link_prediction"] = universe_link_prediction(L, path, unis, mid, p_norm, ws, dev)
     L.pt_graph_free(g)
