@@ -257,6 +257,20 @@ __device__ __forceinline__ int64_t corrupt_in_run(const int32_t *__restrict__ va
     return tmp + l - lo + 1;
 }
 
+// corrupt_in_run with vals[lo] / vals[hi] already loaded (vlo / vhi): identical result and stream use
+__device__ __forceinline__ int64_t corrupt_in_run_pre(const int32_t *__restrict__ vals, int64_t lo, int64_t hi,
+                                                      int64_t vlo, int64_t vhi, int64_t E, uint64_t &s) {
+    const int64_t tmp = rand_max(s, E - (hi - lo + 1));
+    if (tmp < vlo) return tmp;
+    if (tmp > vhi - hi + lo - 1) return tmp + hi - lo + 1;
+    int64_t l = lo, r = hi + 1;
+    while (l + 1 < r) {
+        const int64_t mid = (l + r) >> 1;
+        if (vals[mid] - mid + lo - 1 < tmp) l = mid; else r = mid;
+    }
+    return tmp + l - lo + 1;
+}
+
 // state of the sampler stream that produces positive b of call `call` after the current states
 // (Base.cpp:200-207 split: thread id owns positives [id*per, min((id+1)*per, bs)) of every call)
 __device__ __forceinline__ uint64_t positive_state(const uint64_t *states, int64_t threads, int64_t bs, int64_t b,

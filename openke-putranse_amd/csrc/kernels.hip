@@ -99,28 +99,45 @@ __global__ __launch_bounds__(1024) void k_sample_sort(DeviceGraph g, const uint6
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int64_t call = blockIdx.x;
     int32_t *cnt = lds;                                                  // [n] counts, then starts
-    int32_t *pi = lds + ((n + 3) & ~int64_t(3));                         // [bs][8]: h r t hr_lo hr_hi tr_lo tr_hi -
-    uint64_t *ps = reinterpret_cast<uint64_t *>(pi + 8 * bs);            // [bs] stream state after the index draw
+    // per positive [12] int32: prob bits, hr_lo hr_hi tr_lo tr_hi, then (filter) the run bounds'
+    // values head_t[hr_lo] head_t[hr_hi] tail_h[tr_lo] tail_h[tr_hi] or (no filter) h t, pad, stream state
+    // after the index draw (8 B): every slot's draw needs global memory only inside a run's binary search
+    int32_t *pi = lds + ((n + 3) & ~int64_t(3));
     for (int64_t i = tid; i < n; i += 1024) cnt[i] = 0;
     const int64_t dpp = 1 + 2 * neg;
     for (int64_t b = tid; b < bs; b += 1024) {
         const PosDraw pd = draw_positive(g, states, threads, bs, b, dpp, call);
-        int32_t *q = pi + 8 * b;
-        q[0] = (int32_t)pd.h; q[1] = (int32_t)pd.r; q[2] = (int32_t)pd.t;
-        q[3] = pd.hr_lo; q[4] = pd.hr_hi; q[5] = pd.tr_lo; q[6] = pd.tr_hi;
-        ps[b] = pd.s1;
+        int32_t *q = pi + 12 * b;
+        q[0] = __float_as_int(bern ? g.bern_prob[pd.r] : 500.f);
+        q[1] = pd.hr_lo; q[2] = pd.hr_hi; q[3] = pd.tr_lo; q[4] = pd.tr_hi;
+        if (filter) {
+            q[5] = g.head_t[pd.hr_lo]; q[6] = g.head_t[pd.hr_hi];
+            q[7] = g.tail_h[pd.tr_lo]; q[8] = g.tail_h[pd.tr_hi];
+        } else {
+            q[5] = (int32_t)pd.h; q[6] = (int32_t)pd.t; q[7] = 0; q[8] = 0;
+        }
+        *reinterpret_cast<uint64_t *>(q + 10) = pd.s1;
         w.pos[call * bs + b] = make_int4((int)pd.h, (int)pd.r, (int)pd.t, 0);
     }
     __syncthreads();
     const int64_t slots = bs * neg;
+    const int64_t E = g.ent_total;
     int32_t *nrec = w.neg + call * slots;
     int32_t *noff = w.off + call * slots;
     for (int64_t o = tid; o < slots; o += 1024) {
         const int64_t b = o / neg, k = o - b * neg;
-        const int32_t *q = pi + 8 * b;
-        const PosDraw pd{q[0], q[1], q[2], q[3], q[4], q[5], q[6], ps[b]};
-        int side;
-        const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
+        const int32_t *q = pi + 12 * b;
+        // draw_negative with the per-positive constants from LDS (same stream offsets and arithmetic)
+        uint64_t s = lcg_jump(*reinterpret_cast<const uint64_t *>(q + 10), (uint64_t)(2 * k));
+        const int side = (float)(lcg_next(s) % 1000ULL) < __int_as_float(q[0]) ? 1 : 0;
+        int64_t e;
+        if (filter) {
+            e = side ? corrupt_in_run_pre(g.head_t, q[1], q[2], q[5], q[6], E, s)
+                     : corrupt_in_run_pre(g.tail_h, q[3], q[4], q[7], q[8], E, s);
+        } else {
+            const int64_t tmp = rand_max(s, E - 1), skip = side ? q[5] : q[6];
+            e = tmp < skip ? tmp : tmp + 1;
+        }
         nrec[o] = (int32_t)((e << 1) | side);
         noff[o] = atomicAdd(&cnt[e], 1);
     }
@@ -486,9 +503,9 @@ hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64
 }
 
 static size_t sample_sort_lds(int64_t bs, int64_t n) {
-    return 4 * (size_t)((n + 3) & ~int64_t(3)) + 40 * (size_t)bs;   // counts + (h r t hr tr) + stream state
+    return 4 * (size_t)((n + 3) & ~int64_t(3)) + 48 * (size_t)bs;   // counts + per-positive records
 }
-static const size_t kSampleSortLds = 150 * 1024;
+static const size_t kSampleSortLds = 160 * 1024 - 256;   // leaves room for the static wave totals
 
 bool sample_sort_prepare(int64_t bs, int64_t n, int64_t start_stride) {
     if (sample_sort_lds(bs, n) > kSampleSortLds || n + 1 > start_stride || n >= (int64_t(1) << 30)) return false;
