@@ -124,8 +124,11 @@ __global__ __launch_bounds__(1024) void k_sample_sort(DeviceGraph g, const uint6
     const int64_t E = g.ent_total;
     int32_t *nrec = w.neg + call * slots;
     int32_t *noff = w.off + call * slots;
-    for (int64_t o = tid; o < slots; o += 1024) {
-        const int64_t b = o / neg, k = o - b * neg;
+    // slot o = b * neg + k walked with an incremental (b, k) instead of a 64-bit division per slot
+    const int32_t neg32 = (int32_t)neg, db = 1024 / neg32, dk = 1024 - db * neg32;
+    int32_t b = tid / neg32, k = tid - b * neg32;
+    for (int64_t o = tid; o < slots; o += 1024, b += db, k += dk) {
+        if (k >= neg32) { k -= neg32; ++b; }
         const int32_t *q = pi + 12 * b;
         // draw_negative with the per-positive constants from LDS (same stream offsets and arithmetic)
         uint64_t s = lcg_jump(*reinterpret_cast<const uint64_t *>(q + 10), (uint64_t)(2 * k));
