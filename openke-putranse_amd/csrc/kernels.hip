@@ -85,6 +85,46 @@ __global__ __launch_bounds__(256) void k_sample_csr(DeviceGraph g, const uint64_
     w.off[o] = atomicAdd(&w.cnt[call * w.cnt_stride + e], 1);
 }
 
+// One negative slot's draw from its positive's LDS record (k_sample_sort): the coin and the corruption
+// draw of draw_negative with the same stream offsets and arithmetic; when the drawn index falls inside the
+// known-entity run, the binary search over it (corrupt_in_run) is left to the caller (search = true,
+// l / r the open bounds; an inactive search has l + 1 == r on a valid index).
+struct SlotDraw {
+    const int32_t *vals;
+    int64_t tmp, e, lo, l, r;
+    int side;
+    bool search;
+};
+
+__device__ __forceinline__ SlotDraw slot_prepare(const int32_t *q, int32_t k, int64_t E, int filter,
+                                                 const DeviceGraph &g) {
+    SlotDraw d;
+    uint64_t s = lcg_jump(*reinterpret_cast<const uint64_t *>(q + 10), (uint64_t)(2 * k));
+    d.side = (float)(lcg_next(s) % 1000ULL) < __int_as_float(q[0]) ? 1 : 0;
+    d.search = false;
+    d.vals = g.head_t;
+    if (filter) {
+        d.vals = d.side ? g.head_t : g.tail_h;
+        const int64_t lo = d.side ? q[1] : q[3], hi = d.side ? q[2] : q[4];
+        const int64_t vlo = d.side ? q[5] : q[7], vhi = d.side ? q[6] : q[8];
+        d.tmp = rand_max(s, E - (hi - lo + 1));
+        d.lo = lo;
+        d.l = lo;
+        d.r = lo + 1;
+        if (d.tmp < vlo) d.e = d.tmp;
+        else if (d.tmp > vhi - hi + lo - 1) d.e = d.tmp + hi - lo + 1;
+        else { d.search = true; d.r = hi + 1; d.e = 0; }
+    } else {
+        d.tmp = rand_max(s, E - 1);
+        const int64_t skip = d.side ? q[5] : q[6];
+        d.e = d.tmp < skip ? d.tmp : d.tmp + 1;
+        d.lo = 0;
+        d.l = 0;
+        d.r = 1;
+    }
+    return d;
+}
+
 // Sampling + counting sort of one sampled call per workgroup, entirely in LDS (when the bucket counts
 // and the call's positives fit): the positives are drawn once (not once per slot), every slot's
 // negative reserves its rank with an LDS atomic, the counts are scanned in LDS and every slot's
@@ -124,25 +164,35 @@ __global__ __launch_bounds__(1024) void k_sample_sort(DeviceGraph g, const uint6
     const int64_t E = g.ent_total;
     int32_t *nrec = w.neg + call * slots;
     int32_t *noff = w.off + call * slots;
-    // slot o = b * neg + k walked with an incremental (b, k) instead of a 64-bit division per slot
+    // slots o and o + 1024 per iteration (o = b * neg + k, walked with incremental (b, k) instead of a 64-bit
+    // division per slot); their runs' binary searches advance in lock step so both gathers are in flight
+    // together. A missing second slot repeats the first one's draw and writes nothing.
     const int32_t neg32 = (int32_t)neg, db = 1024 / neg32, dk = 1024 - db * neg32;
     int32_t b = tid / neg32, k = tid - b * neg32;
-    for (int64_t o = tid; o < slots; o += 1024, b += db, k += dk) {
-        if (k >= neg32) { k -= neg32; ++b; }
-        const int32_t *q = pi + 12 * b;
-        // draw_negative with the per-positive constants from LDS (same stream offsets and arithmetic)
-        uint64_t s = lcg_jump(*reinterpret_cast<const uint64_t *>(q + 10), (uint64_t)(2 * k));
-        const int side = (float)(lcg_next(s) % 1000ULL) < __int_as_float(q[0]) ? 1 : 0;
-        int64_t e;
-        if (filter) {
-            e = side ? corrupt_in_run_pre(g.head_t, q[1], q[2], q[5], q[6], E, s)
-                     : corrupt_in_run_pre(g.tail_h, q[3], q[4], q[7], q[8], E, s);
-        } else {
-            const int64_t tmp = rand_max(s, E - 1), skip = side ? q[5] : q[6];
-            e = tmp < skip ? tmp : tmp + 1;
+    for (int64_t o = tid; o < slots; o += 2048) {
+        int32_t b2 = b + db, k2 = k + dk;
+        if (k2 >= neg32) { k2 -= neg32; ++b2; }
+        const bool two = o + 1024 < slots;
+        SlotDraw d0 = slot_prepare(pi + 12 * b, k, E, filter, g);
+        SlotDraw d1 = slot_prepare(pi + 12 * (two ? b2 : b), two ? k2 : k, E, filter, g);
+        for (;;) {
+            const bool a0 = d0.l + 1 < d0.r, a1 = d1.l + 1 < d1.r;
+            if (!(a0 || a1)) break;
+            const int64_t m0 = a0 ? (d0.l + d0.r) >> 1 : d0.l, m1 = a1 ? (d1.l + d1.r) >> 1 : d1.l;
+            const int64_t v0 = d0.vals[m0], v1 = d1.vals[m1];
+            if (a0) { if (v0 - m0 + d0.lo - 1 < d0.tmp) d0.l = m0; else d0.r = m0; }
+            if (a1) { if (v1 - m1 + d1.lo - 1 < d1.tmp) d1.l = m1; else d1.r = m1; }
         }
-        nrec[o] = (int32_t)((e << 1) | side);
-        noff[o] = atomicAdd(&cnt[e], 1);
+        const int64_t e0 = d0.search ? d0.tmp + d0.l - d0.lo + 1 : d0.e;
+        nrec[o] = (int32_t)((e0 << 1) | d0.side);
+        noff[o] = atomicAdd(&cnt[e0], 1);
+        if (two) {
+            const int64_t e1 = d1.search ? d1.tmp + d1.l - d1.lo + 1 : d1.e;
+            nrec[o + 1024] = (int32_t)((e1 << 1) | d1.side);
+            noff[o + 1024] = atomicAdd(&cnt[e1], 1);
+        }
+        b = b2 + db; k = k2 + dk;
+        if (k >= neg32) { k -= neg32; ++b; }
     }
     __syncthreads();
     // exclusive scan of cnt[0, n): contiguous chunks per thread, wave shuffles, LDS wave totals
