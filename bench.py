@@ -458,12 +458,11 @@ def main():
     tl = torch.zeros(n_t, device=dev)
     _native.check(L.pt_trainer_run_timed(tr._native, sampler, bs, neg, bern, filt, n_t, _native.ptr(tl), ms4,
                                          _native.stream()))
-    # fused LDS sampling + sort (then the stream advance) once a chunk holds >= 96 steps, else the
-    # two-pass form (capi.cpp kSampleSortMinCalls)
-    fused = n_t >= 96 and os.environ.get("PT_SAMPLE_TWO_PASS", "0") in ("", "0")
-    names = (["k_sample_sort", "k_advance"] if fused else ["k_sample_csr", "k_scan_counts"]) + \
-        ["k_step_csr", "k_apply_buf"]
-    per_kernel = {n: float(v) for n, v in zip(names, ms4) if v > 0}
+    # the sampling kernels of the path the library took for this chunking (pt_trainer_last_path)
+    path = L.pt_trainer_last_path(tr._native)
+    step_names = ["k_step_csr", "k_apply_buf"] if path != _native.PT_PATH_SAMPLED else ["k_step_sampled", "k_apply"]
+    names = list(_native.PATH_KERNELS.get(path, ("sampling", "bucket scan"))) + step_names
+    per_kernel = {n: float(v) for n, v in zip(names, ms4) if n and v > 0}
     bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
     achieved = bytes_step / (sum(per_kernel.values()) * 1e-3) / 1e9
 

@@ -103,6 +103,20 @@ int pt_trainer_run(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, 
  * gradient rows restored), as the captured epoch runs them. Synchronizes the stream. */
 int pt_trainer_run_timed(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
                          int64_t steps, float *d_losses, float *ms4, void *stream);
+/* Sampling path the last enqueued in-kernel-sampled chunk took (for reports): kinds 0/1 of ms4 are then
+ * PT_PATH_FUSED: k_sample_sort + k_advance; PT_PATH_PART: k_sample_part + k_resolve; PT_PATH_TWO_PASS:
+ * k_sample_csr + k_scan_counts; PT_PATH_SAMPLED: none (small neg: the step kernel samples). -1 before any. */
+enum { PT_PATH_TWO_PASS = 0, PT_PATH_FUSED = 1, PT_PATH_PART = 2, PT_PATH_SAMPLED = 3 };
+int pt_trainer_last_path(const pt_trainer *t);
+/* Sample `calls` consecutive steps into the counting-sort batch layout the large-neg step kernels read,
+ * by path `path` (PT_PATH_FUSED / PT_PATH_PART / PT_PATH_TWO_PASS, or -1 = the automatic choice), advance
+ * the sampler streams, and copy the batches to HOST arrays (synchronizes): h_pos [calls][bs][3] (h, r, t
+ * of each positive), h_neg [calls][bs*neg] (corrupted entity << 1 | 1 when the tail was replaced, slot
+ * b*neg + k = negative k of positive b, Base.cpp:216-232), h_dst [calls][bs*neg] (the slot's row in its
+ * entity's bucket: h_start[e] <= dst < h_start[e+1]), h_start [calls][ent_total + 1]. */
+int pt_trainer_sample_csr(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
+                          int64_t calls, int32_t path, int32_t *h_pos, int32_t *h_neg, int32_t *h_dst,
+                          int32_t *h_start, void *stream);
 
 /* ------------------------------------------------------------------ scoring ------------------ */
 /* scores = ||h + r - t||_p as model.predict computes them (TransE.py:46-74, TransH.py:52-93):

@@ -66,6 +66,8 @@ struct pt_trainer {
     pt::CsrWork csr{};
     int64_t csr_bs = 0, csr_neg = 0, csr_chunk = 0;   // layout the workspace was carved for
     bool csr_fused = false;                             // k_sample_sort plan fits LDS
+    bool csr_part = false;                              // k_sample_part prepared (its LDS limit raised)
+    int last_path = -1;                                 // sampling path of the last enqueued chunk (PT_PATH_*)
     int64_t lpart_cap = 0;                             // W.lpart capacity (positives)
     int device = -1;
     hipStream_t cap = nullptr;
@@ -77,8 +79,10 @@ struct pt_trainer {
     ~pt_trainer() {
         drop_graphs();
         if (cap) (void)hipStreamDestroy(cap);
+
         if (ws_block) (void)hipFree(ws_block);
         if (csr_block) (void)hipFree(csr_block);
+        if (csr.prof) (void)hipFree(csr.prof);
         if (W.lpart) (void)hipFree(W.lpart);
     }
 };
@@ -264,9 +268,40 @@ extern "C" int pt_trainer_update_desc(pt_trainer *t, const pt_model_desc *m) {
 
 
 static const int64_t kCsrChunk = 256;   // steps pre-sampled per sampling/scan launch pair
-// the fused sampling kernel runs one workgroup per call (~260 us each at C2, latency-bound draws), so it
-// only beats the two-pass form (~3.1 us per call) once a chunk fills enough CUs
+// the fused sampling kernel runs one workgroup per call (~200 us each at C2, latency-bound draws), so it
+// only beats the split form once a chunk fills enough CUs on its own
 static const int64_t kSampleSortMinCalls = 96;
+// the split sampler (k_sample_part) runs ceil(kPartTarget / calls) workgroups per call
+static const int64_t kPartTarget = 512;
+
+// Sampling path for a chunk of `calls` steps: PT_SAMPLE_MODE = fused | part | twopass forces one (where
+// its plan fits; PT_SAMPLE_TWO_PASS=1 is the old switch for twopass); by default the fused kernel for
+// chunks of >= kSampleSortMinCalls steps, the split sampler below that.
+static int sample_mode() {
+    const char *tp = getenv("PT_SAMPLE_TWO_PASS");
+    if (tp && atoi(tp) != 0) return PT_PATH_TWO_PASS;
+    const char *v = getenv("PT_SAMPLE_MODE");
+    if (!v) return -1;
+    if (!strcmp(v, "fused")) return PT_PATH_FUSED;
+    if (!strcmp(v, "part")) return PT_PATH_PART;
+    if (!strcmp(v, "twopass")) return PT_PATH_TWO_PASS;
+    return -1;
+}
+static int64_t part_count(int64_t calls, int64_t bs) {
+    int64_t p = (kPartTarget + calls - 1) / calls;
+    if (const char *v = getenv("PT_PART_COUNT")) p = atoll(v);
+    if (p < 2) p = 2;
+    return p > bs ? bs : p;
+}
+static int choose_path(const pt_trainer *t, int64_t calls, int64_t bs, int64_t neg, int forced) {
+    const bool part_ok = t->csr_part && pt::sample_part_fits(bs, neg, t->P.ent_total, part_count(calls, bs));
+    if (forced == PT_PATH_FUSED && t->csr_fused) return PT_PATH_FUSED;
+    if (forced == PT_PATH_PART && part_ok) return PT_PATH_PART;
+    if (forced == PT_PATH_TWO_PASS) return PT_PATH_TWO_PASS;
+    if (t->csr_fused && calls >= kSampleSortMinCalls) return PT_PATH_FUSED;
+    if (part_ok) return PT_PATH_PART;
+    return PT_PATH_TWO_PASS;
+}
 
 // Workspace of the counting-sort path, carved once per (bs, neg): room for a chunk of pre-sampled
 // steps (<= kCsrChunk, fewer when a step's arrays are large) plus one step's gradient rows. A new
@@ -276,12 +311,13 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     const int64_t E = t->P.ent_total, D = t->P.dim;
     const int64_t cs = (E + 3) & ~int64_t(3), ss = (E + 4) & ~int64_t(3);
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t per_call = 16 * bs + 8 * bs * neg + 4 * cs + 4 * ss + 1024;
+    const size_t per_call = 16 * bs + 8 * bs * neg + 4 * cs + 4 * ss + 4 + 1024;
     int64_t chunk = (int64_t)std::max<size_t>(1, ((size_t)512 << 20) / per_call);
     chunk = std::min(chunk, kCsrChunk);
     const size_t a_pos = al(16 * bs * chunk), a_neg = al(4 * bs * neg * chunk), a_off = a_neg,
-                 a_cnt = al(4 * cs * chunk), a_start = al(4 * ss * chunk), a_con = al(4 * bs * neg * D);
-    const size_t need = a_pos + a_neg + a_off + a_cnt + a_start + a_con;
+                 a_cnt = al(4 * cs * chunk), a_start = al(4 * ss * chunk), a_tick = al(4 * chunk),
+                 a_con = al(4 * bs * neg * D);
+    const size_t need = a_pos + a_neg + a_off + a_cnt + a_start + a_tick + a_con;
     PT_HIP(hipDeviceSynchronize());   // queued work may still use the old carving
     t->drop_graphs();
     if (need > t->csr_cap) {
@@ -298,16 +334,22 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     t->csr.off = (int32_t *)b; b += a_off;
     t->csr.cnt = (int32_t *)b; b += a_cnt;
     t->csr.start = (int32_t *)b; b += a_start;
+    t->csr.tick = (int32_t *)b; b += a_tick;
     t->csr.contrib = (float *)b;
     t->csr.cnt_stride = cs;
     t->csr.start_stride = ss;
     t->csr_bs = bs;
     t->csr_neg = neg;
     t->csr_chunk = chunk;
-    // sampling + counting sort fused in LDS when its plan fits (sets the kernel's LDS attribute here,
-    // outside any stream capture); PT_SAMPLE_TWO_PASS=1 forces the two-pass form
-    const char *tp = getenv("PT_SAMPLE_TWO_PASS");
-    t->csr_fused = !(tp && atoi(tp) != 0) && pt::sample_sort_prepare(bs, E, ss);
+    // sampling + counting sort in LDS (one workgroup per call, or split over parts) when the plans fit
+    // (sets the kernels' LDS attributes here, outside any stream capture)
+    t->csr_fused = pt::sample_sort_prepare(bs, neg, E, ss);
+    t->csr_part = pt::sample_part_prepare(bs, neg, E, std::min<int64_t>(bs, kPartTarget));
+    if (const char *dd = getenv("PT_PART_DBG")) t->csr.dbg = atoi(dd);
+    // PT_PART_PROF=1: phase timestamps of the split sampler (reported by pt_trainer_run_timed)
+    if (const char *pp = getenv("PT_PART_PROF")) {
+        if (atoi(pp) != 0 && !t->csr.prof) PT_HIP(hipMalloc(&t->csr.prof, sizeof(uint64_t) * 8 * kCsrChunk * 1024));
+    }
     return PT_OK;
 }
 
@@ -351,6 +393,31 @@ struct Timing {
         if (tm && tm->end(st)) return PT_EHIP;                \
     } while (0)
 
+// Sample `calls` consecutive steps into the counting-sort workspace (pos / neg / destination / start,
+// calls <= csr_chunk): sampling + counting sort in LDS, one workgroup per call (then the stream advance)
+// or split over parts per call (then the destination resolve + stream advance), or the two-pass form
+// (global-atomic counts, separate scan) when no LDS plan fits. `forced` = PT_PATH_* or -1 (automatic).
+static int enqueue_sample_chunk(pt_trainer *t, pt_sampler *s, const pt::CsrWork &w, int64_t bs, int64_t neg,
+                                int64_t bern, int64_t filter, int64_t calls, int forced, hipStream_t st, Timing *tm) {
+    const pt::DeviceGraph dg = s->g->dev;
+    const int64_t dpp = 1 + 2 * neg;
+    const int path = choose_path(t, calls, bs, neg, forced);
+    t->last_path = path;
+    if (path == PT_PATH_FUSED) {
+        PT_TIMED(0, pt::launch_sample_sort(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls,
+                                           t->P.ent_total, w, st));
+        PT_TIMED(1, pt::launch_advance(s->d_states, s->threads, bs, dpp * calls, st));
+    } else if (path == PT_PATH_PART) {
+        PT_TIMED(0, pt::launch_sample_part(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls,
+                                           part_count(calls, bs), t->P.ent_total, w, st));
+        PT_TIMED(1, pt::launch_resolve(w, bs, neg, calls, s->d_states, s->threads, st));
+    } else {
+        PT_TIMED(0, pt::launch_sample_csr(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls, w, st));
+        PT_TIMED(1, pt::launch_scan_counts(w, t->P.ent_total, calls, s->d_states, s->threads, bs, dpp, st));
+    }
+    return PT_OK;
+}
+
 // Enqueue `steps` in-kernel-sampled steps; step i adds its loss to d_losses[i]. Large neg takes the
 // counting-sort path: one sampling + one scan launch per chunk of up to kCsrChunk steps (the batch
 // stream does not depend on the tables, so it is drawn ahead), then k_step + k_apply per step.
@@ -367,17 +434,8 @@ static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, in
         const int64_t chunk = t->csr_chunk;
         for (int64_t c0 = 0; c0 < steps; c0 += chunk) {
             const int64_t calls = std::min(chunk, steps - c0);
-            // sampling + counting sort in LDS, one workgroup per call (then the stream advance), or the
-            // two-pass form (global-atomic counts, separate scan) when the LDS plan does not fit
-            if (t->csr_fused && calls >= kSampleSortMinCalls) {
-                PT_TIMED(0, pt::launch_sample_sort(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter,
-                                                   calls, P.ent_total, t->csr, st));
-                PT_TIMED(1, pt::launch_advance(s->d_states, s->threads, bs, dpp * calls, st));
-            } else {
-                PT_TIMED(0, pt::launch_sample_csr(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls,
-                                                  t->csr, st));
-                PT_TIMED(1, pt::launch_scan_counts(t->csr, P.ent_total, calls, s->d_states, s->threads, bs, dpp, st));
-            }
+            int rc = enqueue_sample_chunk(t, s, t->csr, bs, neg, bern, filter, calls, sample_mode(), st, tm);
+            if (rc) return rc;
             for (int64_t j = 0; j < calls; ++j) {
                 const pt::CsrWork v = pt::csr_view(t->csr, j, bs, neg);
                 float *loss = d_losses ? d_losses + c0 + j : nullptr;
@@ -387,6 +445,7 @@ static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, in
             }
         }
     } else {
+        t->last_path = PT_PATH_SAMPLED;
         for (int64_t i = 0; i < steps; ++i) {
             float *loss = d_losses ? d_losses + i : nullptr;
             PT_TIMED(2, pt::launch_step(P, dg, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr,
@@ -475,6 +534,38 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
         tot[std::get<0>(e)] += ms;
     }
     for (int k = 0; k < 4; ++k) ms4[k] = (float)(tot[k] / (double)steps);
+    if (t->csr.prof && t->last_path == PT_PATH_PART) {   // split sampler phases of the last chunk
+        const int64_t calls = std::min<int64_t>(steps, t->csr_chunk), parts = part_count(calls, bs);
+        std::vector<uint64_t> pr((size_t)(8 * calls * parts));
+        PT_HIP(hipMemcpy(pr.data(), t->csr.prof, 8 * pr.size(), hipMemcpyDeviceToHost));
+        uint64_t t0 = ~0ull, tend = 0;
+        double ph[7] = {0}, mx[7] = {0};
+        int64_t n_last = 0;
+        double last5 = 0, last6 = 0;
+        for (int64_t i = 0; i < calls * parts; ++i) t0 = std::min(t0, pr[8 * i]);
+        for (int64_t i = 0; i < calls * parts; ++i) {
+            const uint64_t *q = &pr[8 * i];
+            for (int k = 1; k <= 4; ++k) {
+                ph[k] += (double)(q[k] - q[k - 1]);
+                mx[k] = std::max(mx[k], (double)(q[k] - t0));
+            }
+            mx[0] = std::max(mx[0], (double)(q[0] - t0));
+            if (q[7]) {
+                ++n_last;
+                last5 += (double)(q[5] - q[4]);
+                last6 += (double)(q[6] - q[5]);
+                tend = std::max(tend, q[6]);
+            }
+        }
+        const double n = (double)(calls * parts);
+        fprintf(stderr,
+                "part-prof calls %ld parts %ld: avg us positives %.2f slots %.2f reserve %.2f rank+ticket %.2f | "
+                "last exchange %.2f scan %.2f | latest start %.2f, phase ends (max from first start) %.2f %.2f %.2f "
+                "%.2f, kernel end %.2f\n",
+                (long)calls, (long)parts, ph[1] / n / 100, ph[2] / n / 100, ph[3] / n / 100, ph[4] / n / 100,
+                last5 / std::max<int64_t>(n_last, 1) / 100, last6 / std::max<int64_t>(n_last, 1) / 100, mx[0] / 100,
+                mx[1] / 100, mx[2] / 100, mx[3] / 100, mx[4] / 100, (double)(tend - t0) / 100);
+    }
     if (!use_csr(neg)) return PT_OK;
     // Counting-sort path: the per-step kernels are re-timed back to back (as a captured epoch runs
     // them), one event pair per loop instead of one per launch, on the last pre-sampled batch:
@@ -538,6 +629,45 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
     PT_HIP(hipEventElapsedTime(&t_s, ev[2], ev[3]));
     ms4[2] = t_s / (float)steps;
     ms4[3] = (t_sa - t_s) / (float)steps;
+    return PT_OK;
+}
+
+extern "C" int pt_trainer_last_path(const pt_trainer *t) { return t ? t->last_path : -1; }
+
+extern "C" int pt_trainer_sample_csr(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern,
+                                     int64_t filter, int64_t calls, int32_t path, int32_t *h_pos, int32_t *h_neg,
+                                     int32_t *h_dst, int32_t *h_start, void *stream) {
+    PT_CHECK(t && s && h_pos && h_neg && h_dst && h_start, PT_EINVAL, "pt_trainer_sample_csr: null argument");
+    PT_CHECK(calls > 0, PT_EINVAL, "pt_trainer_sample_csr: calls must be positive");
+    PT_CHECK(path >= -1 && path <= PT_PATH_PART, PT_EINVAL, "pt_trainer_sample_csr: path must be -1 or PT_PATH_*");
+    int rc = prepare_sampled(t, s, bs, neg, calls);
+    if (rc) return rc;
+    if (!t->csr_block) {   // small neg runs the in-step sampler; carve the counting-sort workspace anyway
+        rc = ensure_csr(t, bs, neg);
+        if (rc) return rc;
+    }
+    PT_CHECK(calls <= t->csr_chunk, PT_EINVAL, "pt_trainer_sample_csr: calls exceeds the workspace chunk");
+    if (path == PT_PATH_FUSED) PT_CHECK(t->csr_fused, PT_ENOTSUP, "fused sampling plan does not fit LDS");
+    if (path == PT_PATH_PART)
+        PT_CHECK(t->csr_part && pt::sample_part_fits(bs, neg, t->P.ent_total, part_count(calls, bs)), PT_ENOTSUP,
+                 "split sampling plan does not fit LDS");
+    hipStream_t st = (hipStream_t)stream;
+    rc = enqueue_sample_chunk(t, s, t->csr, bs, neg, bern, filter, calls, path, st, nullptr);
+    if (rc) return rc;
+    const pt::CsrWork &w = t->csr;
+    const int64_t E = t->P.ent_total, slots = bs * neg;
+    std::vector<int4> pos((size_t)(calls * bs));
+    PT_HIP(hipMemcpyAsync(pos.data(), w.pos, sizeof(int4) * pos.size(), hipMemcpyDeviceToHost, st));
+    PT_HIP(hipMemcpyAsync(h_neg, w.neg, 4 * (size_t)(calls * slots), hipMemcpyDeviceToHost, st));
+    PT_HIP(hipMemcpyAsync(h_dst, w.off, 4 * (size_t)(calls * slots), hipMemcpyDeviceToHost, st));
+    PT_HIP(hipMemcpy2DAsync(h_start, 4 * (size_t)(E + 1), w.start, 4 * (size_t)w.start_stride, 4 * (size_t)(E + 1),
+                            (size_t)calls, hipMemcpyDeviceToHost, st));
+    PT_HIP(hipStreamSynchronize(st));
+    for (size_t i = 0; i < pos.size(); ++i) {
+        h_pos[3 * i] = pos[i].x;
+        h_pos[3 * i + 1] = pos[i].y;
+        h_pos[3 * i + 2] = pos[i].z;
+    }
     return PT_OK;
 }
 

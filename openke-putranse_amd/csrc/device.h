@@ -240,35 +240,54 @@ __device__ __forceinline__ void vpnorm_bwd(const V<G, VEC, KCH> &v, float nv, in
 // ---------------------------------------------------------------- sampler --------------------
 __device__ __forceinline__ int64_t rand_max(uint64_t &s, int64_t x) { return (int64_t)(lcg_next(s) % (uint64_t)x); }
 
+// Boundary search of the filtered corruption (Corrupt.h:43-55). The reference bisects for the largest m
+// in its open interval with f(m) = vals[m] - m + lo - 1 < tmp. vals (the known partners of a run) is
+// strictly increasing, so f is nondecreasing and that boundary is unique: any probe order that keeps
+// f(l) < tmp <= f(r) ends at the same l. Probes interpolate between (l, f(l)) and (r, f(r)) - the
+// entity ids of a run are spread over [0, E), so long runs take ~log log n dependent loads instead of
+// log n - with a bisection step after any step that did not halve the interval (at most 2 log n).
+struct RunSearch {
+    const int32_t *vals;
+    int32_t lo, l, r, fl, fr, tmp;
+    bool bis;
+};
+
+// closed run [lo, hi] with f(lo) < tmp <= f(hi) (the reference's two early exits already failed)
+__device__ __forceinline__ RunSearch run_search(const int32_t *vals, int32_t lo, int32_t hi, int32_t vlo, int32_t vhi,
+                                                int32_t tmp) {
+    return RunSearch{vals, lo, lo, hi, vlo - 1, vhi - hi + lo - 1, tmp, false};
+}
+__device__ __forceinline__ bool rs_open(const RunSearch &q) { return q.l + 1 < q.r; }
+__device__ __forceinline__ int32_t rs_probe(const RunSearch &q) {
+    if (q.bis) return (q.l + q.r) >> 1;
+    const float frac = __fdividef((float)(q.tmp - q.fl), (float)(q.fr - q.fl));
+    const int32_t m = q.l + (int32_t)(frac * (float)(q.r - q.l));
+    return m <= q.l ? q.l + 1 : (m >= q.r ? q.r - 1 : m);
+}
+__device__ __forceinline__ void rs_update(RunSearch &q, int32_t m, int32_t v) {
+    const int32_t f = v - m + q.lo - 1, width = q.r - q.l;
+    if (f < q.tmp) { q.l = m; q.fl = f; } else { q.r = m; q.fr = f; }
+    q.bis = 2 * (q.r - q.l) > width;
+}
+// the corrupted entity once the search is closed
+__device__ __forceinline__ int64_t rs_entity(const RunSearch &q) { return (int64_t)q.tmp + q.l - q.lo + 1; }
+
 // Filtered corruption (Corrupt.h:27-56 / :75-104): `vals` is the searched column of the sorted list
 // (trainHead[].t for corrupt_head, trainTail[].h for corrupt_tail) and [lo, hi] the run of known
 // partners of the positive's (entity, relation) - the [ll, rr] of the reference's two binary searches,
-// precomputed per triple (TripleRec). The draw and the final search are the reference's.
+// precomputed per triple (TripleRec). The draw, the early exits and the boundary are the reference's.
 __device__ __forceinline__ int64_t corrupt_in_run(const int32_t *__restrict__ vals, int64_t lo, int64_t hi, int64_t E,
                                                   uint64_t &s) {
     const int64_t tmp = rand_max(s, E - (hi - lo + 1));
-    if (tmp < vals[lo]) return tmp;
-    if (tmp > vals[hi] - hi + lo - 1) return tmp + hi - lo + 1;
-    int64_t l = lo, r = hi + 1;
-    while (l + 1 < r) {
-        const int64_t mid = (l + r) >> 1;
-        if (vals[mid] - mid + lo - 1 < tmp) l = mid; else r = mid;
-    }
-    return tmp + l - lo + 1;
-}
-
-// corrupt_in_run with vals[lo] / vals[hi] already loaded (vlo / vhi): identical result and stream use
-__device__ __forceinline__ int64_t corrupt_in_run_pre(const int32_t *__restrict__ vals, int64_t lo, int64_t hi,
-                                                      int64_t vlo, int64_t vhi, int64_t E, uint64_t &s) {
-    const int64_t tmp = rand_max(s, E - (hi - lo + 1));
+    const int32_t vlo = vals[lo], vhi = vals[hi];
     if (tmp < vlo) return tmp;
     if (tmp > vhi - hi + lo - 1) return tmp + hi - lo + 1;
-    int64_t l = lo, r = hi + 1;
-    while (l + 1 < r) {
-        const int64_t mid = (l + r) >> 1;
-        if (vals[mid] - mid + lo - 1 < tmp) l = mid; else r = mid;
+    RunSearch q = run_search(vals, (int32_t)lo, (int32_t)hi, vlo, vhi, (int32_t)tmp);
+    while (rs_open(q)) {
+        const int32_t m = rs_probe(q);
+        rs_update(q, m, vals[m]);
     }
-    return tmp + l - lo + 1;
+    return rs_entity(q);
 }
 
 // state of the sampler stream that produces positive b of call `call` after the current states

@@ -39,6 +39,10 @@ struct CsrWork {
     int32_t *cnt = nullptr;     // [calls][cnt_stride] bucket sizes (zero between uses)
     int32_t *start = nullptr;   // [calls][start_stride] exclusive prefix of cnt (E+1 used)
     float *contrib = nullptr;   // [bs*neg][dim] gradient rows of the corrupted entities (one step)
+    int32_t *tick = nullptr;    // [calls] parts of a call done (k_sample_part; zero between uses)
+    uint64_t *prof = nullptr;   // PT_PART_PROF=1 only: [workgroup][8] phase timestamps of k_sample_part
+    int dbg = 0;                // timing experiments only (PT_PART_DBG; results then wrong): bit 0 no run
+                                // search, bit 1 no stream jump, bit 2 no 64-bit modulo
     int64_t cnt_stride = 0, start_stride = 0;
 };
 
@@ -96,11 +100,22 @@ hipError_t launch_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t
 hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                              int bern, int filter, int64_t calls, const CsrWork &w, hipStream_t st);
 // one workgroup per call: sampling + LDS counting sort + scan; the streams are NOT advanced (launch_advance).
-// sample_sort_prepare: whether the LDS plan fits for (bs, n) (and the kernel's LDS limit is raised);
+// sample_sort_prepare: whether the LDS plan fits for (bs, neg, n) (and the kernel's LDS limit is raised);
 // otherwise use launch_sample_csr + launch_scan_counts
-bool sample_sort_prepare(int64_t bs, int64_t n, int64_t start_stride);
+bool sample_sort_prepare(int64_t bs, int64_t neg, int64_t n, int64_t start_stride);
 hipError_t launch_sample_sort(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                               int bern, int filter, int64_t calls, int64_t n, const CsrWork &w, hipStream_t st);
+// `parts` workgroups per call: sampling + LDS counting sort of each part, call-wide buckets reserved with
+// one atomic per touched bucket, the last part scans; then launch_resolve (destinations + stream advance).
+// sample_part_fits: whether the LDS plan of `parts` parts per call fits; sample_part_prepare: the same,
+// and raises the kernel's LDS limit (call outside any stream capture)
+bool sample_part_fits(int64_t bs, int64_t neg, int64_t n, int64_t parts);
+bool sample_part_prepare(int64_t bs, int64_t neg, int64_t n, int64_t parts);
+hipError_t launch_sample_part(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
+                              int bern, int filter, int64_t calls, int64_t parts, int64_t n, const CsrWork &w,
+                              hipStream_t st);
+hipError_t launch_resolve(const CsrWork &w, int64_t bs, int64_t neg, int64_t calls, uint64_t *states, int64_t threads,
+                          hipStream_t st);
 hipError_t launch_scan_counts(const CsrWork &w, int64_t n, int64_t calls, uint64_t *states, int64_t threads,
                               int64_t bs, int64_t dpp, hipStream_t st);
 bool step_fits(const StepParams &P, int64_t neg, bool csr);

@@ -85,44 +85,68 @@ __global__ __launch_bounds__(256) void k_sample_csr(DeviceGraph g, const uint64_
     w.off[o] = atomicAdd(&w.cnt[call * w.cnt_stride + e], 1);
 }
 
-// One negative slot's draw from its positive's LDS record (k_sample_sort): the coin and the corruption
-// draw of draw_negative with the same stream offsets and arithmetic; when the drawn index falls inside the
-// known-entity run, the binary search over it (corrupt_in_run) is left to the caller (search = true,
-// l / r the open bounds; an inactive search has l + 1 == r on a valid index).
+// One negative slot's draw from its positive's LDS record (k_sample_sort, k_sample_part): the coin and the
+// corruption draw of draw_negative with the same stream offsets and arithmetic; when the drawn index
+// falls inside the known-entity run, the boundary search over it (corrupt_in_run) is left to the caller
+// (q open; otherwise q is closed and e is the entity).
 struct SlotDraw {
-    const int32_t *vals;
-    int64_t tmp, e, lo, l, r;
+    RunSearch q;
+    int64_t e;
     int side;
     bool search;
 };
 
+// jump maps of the LCG by 2k draws for k < kJumpTab, staged in LDS once per workgroup: a slot's stream
+// start is then one 64-bit multiply-add away from its positive's state instead of a square-and-multiply
+// loop (the loop remains for k >= kJumpTab)
+constexpr int kJumpTab = 256;
+__device__ __forceinline__ int32_t jump_tab_len(int64_t neg) { return neg < kJumpTab ? (int32_t)neg : kJumpTab; }
+template <int NT>
+__device__ __forceinline__ void jump_tab_fill(Affine *jt, int64_t neg, int tid) {
+    for (int32_t k = tid; k < jump_tab_len(neg); k += NT) jt[k] = lcg_power((uint64_t)(2 * k));
+}
+
 __device__ __forceinline__ SlotDraw slot_prepare(const int32_t *q, int32_t k, int64_t E, int filter,
-                                                 const DeviceGraph &g) {
+                                                 const DeviceGraph &g, const Affine *jt, int dbg = 0) {
     SlotDraw d;
-    uint64_t s = lcg_jump(*reinterpret_cast<const uint64_t *>(q + 10), (uint64_t)(2 * k));
+    const uint64_t s1 = *reinterpret_cast<const uint64_t *>(q + 10);
+    uint64_t s;
+    if (dbg & 2) s = s1 + k;
+    else if (k < kJumpTab) { const Affine m = jt[k]; s = m.a * s1 + m.c; }
+    else s = lcg_jump(s1, (uint64_t)(2 * k));
     d.side = (float)(lcg_next(s) % 1000ULL) < __int_as_float(q[0]) ? 1 : 0;
     d.search = false;
-    d.vals = g.head_t;
+    d.q.l = 0;
+    d.q.r = 1;   // closed
     if (filter) {
-        d.vals = d.side ? g.head_t : g.tail_h;
-        const int64_t lo = d.side ? q[1] : q[3], hi = d.side ? q[2] : q[4];
-        const int64_t vlo = d.side ? q[5] : q[7], vhi = d.side ? q[6] : q[8];
-        d.tmp = rand_max(s, E - (hi - lo + 1));
-        d.lo = lo;
-        d.l = lo;
-        d.r = lo + 1;
-        if (d.tmp < vlo) d.e = d.tmp;
-        else if (d.tmp > vhi - hi + lo - 1) d.e = d.tmp + hi - lo + 1;
-        else { d.search = true; d.r = hi + 1; d.e = 0; }
+        const int32_t *vals = d.side ? g.head_t : g.tail_h;
+        const int32_t lo = d.side ? q[1] : q[3], hi = d.side ? q[2] : q[4];
+        const int32_t vlo = d.side ? q[5] : q[7], vhi = d.side ? q[6] : q[8];
+        const int64_t tmp = (dbg & 4) ? (int64_t)((uint32_t)lcg_next(s) & 8191) : rand_max(s, E - (hi - lo + 1));
+        if (tmp < vlo) d.e = tmp;
+        else if (tmp > vhi - hi + lo - 1) d.e = tmp + hi - lo + 1;
+        else if (dbg & 1) d.e = tmp;
+        else { d.search = true; d.q = run_search(vals, lo, hi, vlo, vhi, (int32_t)tmp); d.e = 0; }
     } else {
-        d.tmp = rand_max(s, E - 1);
+        const int64_t tmp = rand_max(s, E - 1);
         const int64_t skip = d.side ? q[5] : q[6];
-        d.e = d.tmp < skip ? d.tmp : d.tmp + 1;
-        d.lo = 0;
-        d.l = 0;
-        d.r = 1;
+        d.e = tmp < skip ? tmp : tmp + 1;
     }
     return d;
+}
+
+// two slots' boundary searches stepped in lock step (both gathers in flight together)
+__device__ __forceinline__ void slot_search2(SlotDraw &d0, SlotDraw &d1) {
+    for (;;) {
+        const bool a0 = rs_open(d0.q), a1 = rs_open(d1.q);
+        if (!(a0 || a1)) break;
+        const int32_t m0 = a0 ? rs_probe(d0.q) : 0, m1 = a1 ? rs_probe(d1.q) : 0;
+        const int32_t v0 = a0 ? d0.q.vals[m0] : 0, v1 = a1 ? d1.q.vals[m1] : 0;   // only open searches load
+        if (a0) rs_update(d0.q, m0, v0);
+        if (a1) rs_update(d1.q, m1, v1);
+    }
+    if (d0.search) d0.e = rs_entity(d0.q);
+    if (d1.search) d1.e = rs_entity(d1.q);
 }
 
 // Sampling + counting sort of one sampled call per workgroup, entirely in LDS (when the bucket counts
@@ -138,12 +162,14 @@ __global__ __launch_bounds__(1024) void k_sample_sort(DeviceGraph g, const uint6
     __shared__ int32_t wtot[16];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int64_t call = blockIdx.x;
-    int32_t *cnt = lds;                                                  // [n] counts, then starts
+    Affine *jt = reinterpret_cast<Affine *>(lds);                        // [jump_tab_len(neg)] jump maps
+    int32_t *cnt = lds + 4 * jump_tab_len(neg);                          // [n] counts, then starts
     // per positive [12] int32: prob bits, hr_lo hr_hi tr_lo tr_hi, then (filter) the run bounds'
     // values head_t[hr_lo] head_t[hr_hi] tail_h[tr_lo] tail_h[tr_hi] or (no filter) h t, pad, stream state
-    // after the index draw (8 B): every slot's draw needs global memory only inside a run's binary search
-    int32_t *pi = lds + ((n + 3) & ~int64_t(3));
+    // after the index draw (8 B): every slot's draw needs global memory only inside a run's boundary search
+    int32_t *pi = cnt + ((n + 3) & ~int64_t(3));
     for (int64_t i = tid; i < n; i += 1024) cnt[i] = 0;
+    jump_tab_fill<1024>(jt, neg, tid);
     const int64_t dpp = 1 + 2 * neg;
     for (int64_t b = tid; b < bs; b += 1024) {
         const PosDraw pd = draw_positive(g, states, threads, bs, b, dpp, call);
@@ -165,29 +191,23 @@ __global__ __launch_bounds__(1024) void k_sample_sort(DeviceGraph g, const uint6
     int32_t *nrec = w.neg + call * slots;
     int32_t *noff = w.off + call * slots;
     // slots o and o + 1024 per iteration (o = b * neg + k, walked with incremental (b, k) instead of a 64-bit
-    // division per slot); their runs' binary searches advance in lock step so both gathers are in flight
-    // together. A missing second slot repeats the first one's draw and writes nothing.
+    // division per slot); their runs' boundary searches advance in lock step so both gathers are in
+    // flight together. A missing second slot (past the end) draws and writes nothing.
     const int32_t neg32 = (int32_t)neg, db = 1024 / neg32, dk = 1024 - db * neg32;
     int32_t b = tid / neg32, k = tid - b * neg32;
     for (int64_t o = tid; o < slots; o += 2048) {
         int32_t b2 = b + db, k2 = k + dk;
         if (k2 >= neg32) { k2 -= neg32; ++b2; }
         const bool two = o + 1024 < slots;
-        SlotDraw d0 = slot_prepare(pi + 12 * b, k, E, filter, g);
-        SlotDraw d1 = slot_prepare(pi + 12 * (two ? b2 : b), two ? k2 : k, E, filter, g);
-        for (;;) {
-            const bool a0 = d0.l + 1 < d0.r, a1 = d1.l + 1 < d1.r;
-            if (!(a0 || a1)) break;
-            const int64_t m0 = a0 ? (d0.l + d0.r) >> 1 : d0.l, m1 = a1 ? (d1.l + d1.r) >> 1 : d1.l;
-            const int64_t v0 = d0.vals[m0], v1 = d1.vals[m1];
-            if (a0) { if (v0 - m0 + d0.lo - 1 < d0.tmp) d0.l = m0; else d0.r = m0; }
-            if (a1) { if (v1 - m1 + d1.lo - 1 < d1.tmp) d1.l = m1; else d1.r = m1; }
-        }
-        const int64_t e0 = d0.search ? d0.tmp + d0.l - d0.lo + 1 : d0.e;
+        SlotDraw d0 = slot_prepare(pi + 12 * b, k, E, filter, g, jt);
+        SlotDraw d1 = slot_prepare(pi + 12 * (two ? b2 : b), two ? k2 : k, E, filter, g, jt);
+        if (!two) { d1.q.l = 0; d1.q.r = 1; d1.search = false; }   // no second slot: its search stays closed
+        slot_search2(d0, d1);
+        const int64_t e0 = d0.e;
         nrec[o] = (int32_t)((e0 << 1) | d0.side);
         noff[o] = atomicAdd(&cnt[e0], 1);
         if (two) {
-            const int64_t e1 = d1.search ? d1.tmp + d1.l - d1.lo + 1 : d1.e;
+            const int64_t e1 = d1.e;
             nrec[o + 1024] = (int32_t)((e1 << 1) | d1.side);
             noff[o + 1024] = atomicAdd(&cnt[e1], 1);
         }
@@ -220,6 +240,193 @@ __global__ __launch_bounds__(1024) void k_sample_sort(DeviceGraph g, const uint6
     if (tid == 1023) start[n] = run;   // the last thread's chunk ends at n (or is empty): run = total
     __syncthreads();
     for (int64_t o = tid; o < slots; o += 1024) noff[o] = cnt[nrec[o] >> 1] + noff[o];
+}
+
+// LDS bucket rank of entity e: 16-bit packed counts (two buckets per word; a part never holds 65536
+// slots, so a half never carries into the other) or plain 32-bit counts
+template <bool PACK>
+__device__ __forceinline__ int32_t lds_rank(int32_t *cnt, int64_t e) {
+    if constexpr (PACK) {
+        const int sh = (int)(e & 1) << 4;
+        return (atomicAdd(&cnt[e >> 1], 1 << sh) >> sh) & 0xffff;
+    } else {
+        return atomicAdd(&cnt[e], 1);
+    }
+}
+template <bool PACK>
+__device__ __forceinline__ int32_t lds_bucket(const int32_t *cnt, int64_t e) {
+    if constexpr (PACK) return (cnt[e >> 1] >> ((int)(e & 1) << 4)) & 0xffff;
+    else return cnt[e];
+}
+
+// Split sampling + counting sort: `parts` workgroups per sampled call (grid calls x parts), so a chunk
+// of few steps still fills the chip (k_sample_sort runs one workgroup per call). Part p owns positives
+// [p*bs/parts, (p+1)*bs/parts) of its call and all their slots. It draws them exactly as k_sample_sort
+// does (positives once, per-positive constants in LDS, two slots per thread with lock-step run
+// searches) and ranks every slot in an LDS count of its corrupted entity (16-bit packed counts when a
+// call has < 65536 slots; the call's global counts are then packed the same way). It then reserves
+// each touched bucket's range in the call's global counts with ONE returning atomic per touched count
+// word and turns its slots' LDS ranks into ranks inside the call-wide buckets. The part whose ticket add comes last exchanges the global counts with zeros (atomics on
+// both sides: every part's adds are seen, and the counts are clear for the next chunk) and scans them
+// into start[]. k_resolve then adds start[entity] to every slot's rank (its destination row) and
+// advances the sampler streams, which this kernel only reads.
+template <int NT, bool PACK>
+__global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, const uint64_t *__restrict__ states,
+                                                    int64_t threads, int64_t bs, int64_t neg, int bern, int filter,
+                                                    int64_t parts, CsrWork w) {
+    extern __shared__ __attribute__((aligned(16))) int32_t lds[];
+    __shared__ int32_t wtot[NT / 64];
+    __shared__ int32_t is_last;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t call = blockIdx.x / parts, part = blockIdx.x - call * parts;
+    const int64_t b0 = part * bs / parts, b1 = (part + 1) * bs / parts;
+    const int64_t E = g.ent_total;
+    const int64_t cwords = PACK ? (E + 1) >> 1 : E;
+    uint64_t *prof = w.prof ? w.prof + 8 * (int64_t)blockIdx.x : nullptr;
+#define PT_PHASE(i) if (prof && tid == 0) prof[i] = wall_clock64()
+    PT_PHASE(0);
+    Affine *jt = reinterpret_cast<Affine *>(lds);        // [jump_tab_len(neg)] jump maps
+    int32_t *cnt = lds + 4 * jump_tab_len(neg);
+    int32_t *pi = cnt + ((cwords + 3) & ~int64_t(3));    // [b1 - b0][12] positive records (k_sample_sort)
+    for (int64_t i = tid; i < cwords; i += NT) cnt[i] = 0;
+    jump_tab_fill<NT>(jt, neg, tid);
+    const int64_t dpp = 1 + 2 * neg;
+    for (int64_t b = b0 + tid; b < b1; b += NT) {
+        const PosDraw pd = draw_positive(g, states, threads, bs, b, dpp, call);
+        int32_t *q = pi + 12 * (b - b0);
+        q[0] = __float_as_int(bern ? g.bern_prob[pd.r] : 500.f);
+        q[1] = pd.hr_lo; q[2] = pd.hr_hi; q[3] = pd.tr_lo; q[4] = pd.tr_hi;
+        if (filter) {
+            q[5] = g.head_t[pd.hr_lo]; q[6] = g.head_t[pd.hr_hi];
+            q[7] = g.tail_h[pd.tr_lo]; q[8] = g.tail_h[pd.tr_hi];
+        } else {
+            q[5] = (int32_t)pd.h; q[6] = (int32_t)pd.t; q[7] = 0; q[8] = 0;
+        }
+        *reinterpret_cast<uint64_t *>(q + 10) = pd.s1;
+        w.pos[call * bs + b] = make_int4((int)pd.h, (int)pd.r, (int)pd.t, 0);
+    }
+    __syncthreads();
+    PT_PHASE(1);
+    const int64_t slots = bs * neg;
+    int32_t *nrec = w.neg + call * slots;
+    int32_t *noff = w.off + call * slots;
+    const int64_t o0 = b0 * neg, o1 = b1 * neg;
+    // thread tid takes slots o0 + tid + NT*m (m = 0, 1, ...): pairs (o, o + NT) per iteration, (b, k)
+    // relative to b0 walked incrementally
+    const int32_t neg32 = (int32_t)neg, db = NT / neg32, dk = NT - db * neg32;
+    int32_t b = tid / neg32, k = tid - b * neg32;
+    for (int64_t o = o0 + tid; o < o1; o += 2 * NT) {
+        int32_t b2 = b + db, k2 = k + dk;
+        if (k2 >= neg32) { k2 -= neg32; ++b2; }
+        const bool two = o + NT < o1;
+        SlotDraw d0 = slot_prepare(pi + 12 * b, k, E, filter, g, jt, w.dbg);
+        SlotDraw d1 = slot_prepare(pi + 12 * (two ? b2 : b), two ? k2 : k, E, filter, g, jt, w.dbg);
+        if (!two) { d1.q.l = 0; d1.q.r = 1; d1.search = false; }
+        slot_search2(d0, d1);
+        const int64_t e0 = d0.e;
+        nrec[o] = (int32_t)((e0 << 1) | d0.side);
+        noff[o] = lds_rank<PACK>(cnt, e0);
+        if (two) {
+            const int64_t e1 = d1.e;
+            nrec[o + NT] = (int32_t)((e1 << 1) | d1.side);
+            noff[o + NT] = lds_rank<PACK>(cnt, e1);
+        }
+        b = b2 + db; k = k2 + dk;
+        if (k >= neg32) { k -= neg32; ++b; }
+    }
+    __syncthreads();
+    PT_PHASE(2);
+    // reserve this part's range in every touched call-wide bucket with one returning atomic per count
+    // word (packed: the call's global counts are packed the same way, each half < 65536, so one add
+    // reserves both buckets); the LDS word becomes the bases. Batches of 8 words per thread keep the
+    // atomics in flight together (a returned value is only waited for at its LDS write).
+    int32_t *gcnt = w.cnt + call * w.cnt_stride;
+    for (int64_t i0 = tid; i0 < cwords; i0 += 8 * NT) {
+        int32_t v[8], r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t i = i0 + u * NT;
+            v[u] = i < cwords ? cnt[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = v[u] ? atomicAdd(&gcnt[i0 + u * NT], v[u]) : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (v[u]) cnt[i0 + u * NT] = r[u];
+    }
+    __syncthreads();
+    PT_PHASE(3);
+    // the slots this thread wrote above (same thread, same addresses): rank inside the call-wide bucket
+    for (int64_t o = o0 + tid; o < o1; o += NT) noff[o] += lds_bucket<PACK>(cnt, nrec[o] >> 1);
+    // every wave's count atomics have returned (their values were used): count this part done
+    __syncthreads();
+    if (tid == 0) is_last = atomicAdd(&w.tick[call], 1) == (int32_t)(parts - 1);
+    __syncthreads();
+    PT_PHASE(4);
+    if (prof && tid == 0) prof[7] = is_last;
+    if (!is_last) return;
+    if (tid == 0) w.tick[call] = 0;   // read again only by a later launch
+    // last part: the call's bucket sizes, exchanged with zeros (atomics on both sides: every part's adds
+    // are seen, and the counts are clear for the next chunk) into LDS, 8 exchanges in flight per thread
+    for (int64_t i0 = tid; i0 < cwords; i0 += 8 * NT) {
+        int32_t r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = i0 + u * NT < cwords ? atomicExch(&gcnt[i0 + u * NT], 0) : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u * NT < cwords) cnt[i0 + u * NT] = r[u];
+    }
+    __syncthreads();
+    PT_PHASE(5);
+    // exclusive scan over the entities into start[]: contiguous words per thread, wave shuffles, LDS
+    // wave totals (k_sample_sort's scan on the packed or plain words)
+    int32_t *start = w.start + call * w.start_stride;
+    const int64_t per = (cwords + NT - 1) / NT;
+    const int64_t lo = tid * per, hi = lo + per < cwords ? lo + per : cwords;
+    int32_t tsum = 0;
+    for (int64_t i = lo; i < hi; ++i) {
+        const int32_t v = cnt[i];
+        tsum += PACK ? (v & 0xffff) + (int32_t)((uint32_t)v >> 16) : v;
+    }
+    int32_t incl = tsum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wtot[wid] = incl;
+    __syncthreads();
+    int32_t run = incl - tsum;
+    for (int q = 0; q < wid; ++q) run += wtot[q];
+    for (int64_t i = lo; i < hi; ++i) {
+        const int32_t v = cnt[i];
+        if constexpr (PACK) {
+            start[2 * i] = run;
+            run += v & 0xffff;
+            if (2 * i + 1 < E) start[2 * i + 1] = run;
+            run += (int32_t)((uint32_t)v >> 16);
+        } else {
+            start[i] = run;
+            run += v;
+        }
+    }
+    if (tid == NT - 1) start[E] = run;   // the last thread's chunk ends at the end (or is empty): run = total
+    PT_PHASE(6);
+#undef PT_PHASE
+}
+
+// destination rows of the split sampler's slots: rank inside the bucket + start[entity]; block (0, 0)
+// advances the sampler streams past all `calls` calls' draws
+__global__ __launch_bounds__(256) void k_resolve(CsrWork w, int64_t slots, uint64_t *states, int64_t threads,
+                                                 int64_t bs, int64_t dpp, int64_t calls) {
+    const int64_t call = blockIdx.y;
+    if (blockIdx.x == 0 && call == 0 && threadIdx.x < 64)
+        advance_states(states, threads, bs, dpp * calls, (int)threadIdx.x);
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= slots) return;
+    const int32_t *start = w.start + call * w.start_stride;
+    const int64_t o = call * slots + i;
+    w.off[o] += start[w.neg[o] >> 1];
 }
 
 // exclusive scan of the bucket sizes (one workgroup of 1024 threads, tiles of 16384 counts: 16
@@ -555,23 +762,93 @@ hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64
     return hipGetLastError();
 }
 
-static size_t sample_sort_lds(int64_t bs, int64_t n) {
-    return 4 * (size_t)((n + 3) & ~int64_t(3)) + 48 * (size_t)bs;   // counts + per-positive records
+static size_t jump_tab_bytes(int64_t neg) { return 16 * (size_t)(neg < 256 ? neg : 256); }   // kJumpTab
+static size_t sample_sort_lds(int64_t bs, int64_t neg, int64_t n) {
+    // jump maps + counts + per-positive records
+    return jump_tab_bytes(neg) + 4 * (size_t)((n + 3) & ~int64_t(3)) + 48 * (size_t)bs;
 }
 static const size_t kSampleSortLds = 160 * 1024 - 256;   // leaves room for the static wave totals
 
-bool sample_sort_prepare(int64_t bs, int64_t n, int64_t start_stride) {
-    if (sample_sort_lds(bs, n) > kSampleSortLds || n + 1 > start_stride || n >= (int64_t(1) << 30)) return false;
+bool sample_sort_prepare(int64_t bs, int64_t neg, int64_t n, int64_t start_stride) {
+    if (sample_sort_lds(bs, neg, n) > kSampleSortLds || n + 1 > start_stride || n >= (int64_t(1) << 30)) return false;
     return hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_sample_sort),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSampleSortLds) == hipSuccess;
 }
 
 hipError_t launch_sample_sort(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                               int bern, int filter, int64_t calls, int64_t n, const CsrWork &w, hipStream_t st) {
-    const size_t lds = sample_sort_lds(bs, n);
+    const size_t lds = sample_sort_lds(bs, neg, n);
     if (lds > kSampleSortLds || n + 1 > w.start_stride) return hipErrorInvalidValue;
     hipLaunchKernelGGL(dev::k_sample_sort, dim3((unsigned)calls), dim3(1024), lds, st, g, states, threads, bs, neg,
                        bern, filter, n, w);
+    return hipGetLastError();
+}
+
+// split sampler: threads per workgroup (PT_PART_NT = 256 | 512 | 1024 for tuning), LDS plan
+static int part_nt() {
+    static const int nt = [] {
+        const char *v = getenv("PT_PART_NT");
+        const int x = v ? atoi(v) : 512;
+        return x == 256 || x == 1024 ? x : 512;
+    }();
+    return nt;
+}
+static bool part_pack(int64_t bs, int64_t neg) { return bs * neg < 65536; }
+static size_t sample_part_lds(int64_t bs, int64_t neg, int64_t n, int64_t parts) {
+    const int64_t cw = part_pack(bs, neg) ? (n + 1) >> 1 : n;
+    const int64_t np = (bs + parts - 1) / parts + 1;   // positives of the largest part
+    return jump_tab_bytes(neg) + 4 * (size_t)((cw + 3) & ~int64_t(3)) + 48 * (size_t)np;
+}
+
+template <int NT, bool PACK>
+static hipError_t part_attr() {
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_sample_part<NT, PACK>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSampleSortLds);
+}
+
+bool sample_part_fits(int64_t bs, int64_t neg, int64_t n, int64_t parts) {
+    return parts >= 1 && parts <= bs && neg >= 1 && sample_part_lds(bs, neg, n, parts) <= kSampleSortLds &&
+           n < (int64_t(1) << 30) && bs * neg < (int64_t(1) << 30);
+}
+
+bool sample_part_prepare(int64_t bs, int64_t neg, int64_t n, int64_t parts) {
+    if (!sample_part_fits(bs, neg, n, parts)) return false;
+    const bool pk = part_pack(bs, neg);
+    switch (part_nt()) {
+        case 256: return (pk ? part_attr<256, true>() : part_attr<256, false>()) == hipSuccess;
+        case 1024: return (pk ? part_attr<1024, true>() : part_attr<1024, false>()) == hipSuccess;
+        default: return (pk ? part_attr<512, true>() : part_attr<512, false>()) == hipSuccess;
+    }
+}
+
+hipError_t launch_sample_part(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
+                              int bern, int filter, int64_t calls, int64_t parts, int64_t n, const CsrWork &w,
+                              hipStream_t st) {
+    if (!sample_part_fits(bs, neg, n, parts) || n + 1 > w.start_stride || n > w.cnt_stride || !w.tick)
+        return hipErrorInvalidValue;
+    const size_t lds = sample_part_lds(bs, neg, n, parts);
+    const dim3 grid((unsigned)(calls * parts));
+    const bool pk = part_pack(bs, neg);
+#define PT_PART(NT_)                                                                                           \
+    if (part_nt() == NT_) {                                                                                  \
+        if (pk)                                                                                              \
+            hipLaunchKernelGGL((dev::k_sample_part<NT_, true>), grid, dim3(NT_), lds, st, g, states, threads, \
+                               bs, neg, bern, filter, parts, w);                                              \
+        else                                                                                                 \
+            hipLaunchKernelGGL((dev::k_sample_part<NT_, false>), grid, dim3(NT_), lds, st, g, states, threads, \
+                               bs, neg, bern, filter, parts, w);                                              \
+        return hipGetLastError();                                                                            \
+    }
+    PT_PART(256) PT_PART(512) PT_PART(1024)
+#undef PT_PART
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_resolve(const CsrWork &w, int64_t bs, int64_t neg, int64_t calls, uint64_t *states, int64_t threads,
+                          hipStream_t st) {
+    const int64_t slots = bs * neg;
+    const dim3 grid((unsigned)((slots + 255) / 256), (unsigned)calls);
+    hipLaunchKernelGGL(dev::k_resolve, grid, dim3(256), 0, st, w, slots, states, threads, bs, 1 + 2 * neg, calls);
     return hipGetLastError();
 }
 

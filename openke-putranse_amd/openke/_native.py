@@ -19,6 +19,10 @@ c_f32p = ctypes.POINTER(ctypes.c_float)
 
 PT_TRANSE, PT_TRANSH = 0, 1
 PT_SGD, PT_ADAGRAD = 0, 1
+# sampling paths of the counting-sort (large neg) step (include/putranse.h PT_PATH_*)
+PT_PATH_TWO_PASS, PT_PATH_FUSED, PT_PATH_PART, PT_PATH_SAMPLED = 0, 1, 2, 3
+PATH_KERNELS = {PT_PATH_TWO_PASS: ("k_sample_csr", "k_scan_counts"), PT_PATH_FUSED: ("k_sample_sort", "k_advance"),
+                PT_PATH_PART: ("k_sample_part", "k_resolve"), PT_PATH_SAMPLED: (None, None)}
 
 
 class NativeError(RuntimeError):
@@ -67,6 +71,9 @@ SIGNATURES = {
     "pt_trainer_step": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "pt_trainer_run": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "pt_trainer_run_timed": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "pt_trainer_last_path": (ctypes.c_int, [c_vp]),
+    "pt_trainer_sample_csr": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, ctypes.c_int32, c_vp,
+                                             c_vp, c_vp, c_vp, c_vp]),
     "pt_score": (ctypes.c_int, [ctypes.POINTER(ModelDesc), c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "pt_score_queries": (ctypes.c_int, [ctypes.POINTER(ModelDesc), c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "pt_score_rows": (ctypes.c_int, [ctypes.POINTER(ModelDesc), c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),

@@ -264,9 +264,11 @@ static int64_t corrupt_plain(const okg *g, int64_t skip, uint64_t *s) {
     return tmp < skip ? tmp : tmp + 1;
 }
 
-/* getBatch (Base.cpp:185-264) for every sampler thread in turn; threads write disjoint slices. */
-void oracle_sampling(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
-                     int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y) {
+/* getBatch (Base.cpp:185-264) for every sampler thread in turn; threads write disjoint slices.
+ * side (optional, NULL = not recorded): side[b + (k+1)*bs] = 1 when the coin of Base.cpp:219-222 chose
+ * corrupt_head (the TAIL replaced), 0 when it chose corrupt_tail (the head replaced). */
+void oracle_sampling_sides(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
+                           int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y, int8_t *side) {
     for (int64_t id = 0; id < threads; ++id) {
         int64_t lef, rig;
         if (bs % threads == 0) {
@@ -286,7 +288,9 @@ void oracle_sampling(const okg *g, uint64_t *states, int64_t threads, int64_t bs
             int64_t last = bs;
             for (int64_t k = 0; k < neg; ++k) {
                 if (bern) prob = 1000 * g->right_mean[p.r] / (g->right_mean[p.r] + g->left_mean[p.r]);
-                if ((float)(lcg_next(s) % 1000) < prob) {
+                const int tail_side = (float)(lcg_next(s) % 1000) < prob;
+                if (side) side[b + last] = (int8_t)tail_side;
+                if (tail_side) {
                     h[b + last] = p.h;
                     t[b + last] = filter ? corrupt_filtered(g, 1, p.h, p.r, s) : corrupt_plain(g, p.h, s);
                     r[b + last] = p.r;
@@ -300,6 +304,11 @@ void oracle_sampling(const okg *g, uint64_t *states, int64_t threads, int64_t bs
             }
         }
     }
+}
+
+void oracle_sampling(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
+                     int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y) {
+    oracle_sampling_sides(g, states, threads, bs, neg, bern, filter, h, t, r, y, NULL);
 }
 
 /* ---------------------------------------------------------------- universe construction ------- */

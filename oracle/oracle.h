@@ -46,6 +46,8 @@ void oracle_rand_reset(orand_t *g, int64_t threads, uint64_t *states);
 /* sampling + getBatch, mode 0, neg_rel 0 (Base.cpp:185-310) */
 void oracle_sampling(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
                      int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y);
+void oracle_sampling_sides(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
+                           int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y, int8_t *side);
 
 /* getParallelUniverse (UniverseConstructor.h:327-397): returns the universe graph (local ids, helpers
  * built as loadUniverseHelpers does) and writes local->global maps (sized >= E and >= R). */

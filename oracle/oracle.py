@@ -44,6 +44,8 @@ def lib():
         L.orand_next.argtypes = [ctypes.c_void_p]
         L.oracle_rand_reset.argtypes = [ctypes.c_void_p, ctypes.c_int64, u64p]
         L.oracle_sampling.argtypes = [ctypes.c_void_p, u64p] + [ctypes.c_int64] * 5 + [i64p, i64p, i64p, f32p]
+        L.oracle_sampling_sides.argtypes = [ctypes.c_void_p, u64p] + [ctypes.c_int64] * 5 + \
+            [i64p, i64p, i64p, f32p, ctypes.c_void_p]
         L.oracle_universe.restype = ctypes.c_void_p
         L.oracle_universe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_float, i64p, i64p]
         L.oracle_train_step.restype = ctypes.c_float
@@ -123,13 +125,16 @@ class KG:
         rm = np.array([lib().okg_right_mean(self.h, i) for i in range(R)], dtype=np.float32)
         return lm, rm
 
-    def sample(self, states, threads, bs, neg, bern, filt):
+    def sample(self, states, threads, bs, neg, bern, filt, sides=False):
+        """One sampling() call (Base.cpp:266-310). sides=True also returns int8[seq]: 1 where the tail
+        was replaced (corrupt_head), 0 where the head was (positions [0, bs) stay 0)."""
         seq = bs * (1 + neg)
         h, t, r = (np.zeros(seq, dtype=np.int64) for _ in range(3))
         y = np.zeros(seq, dtype=np.float32)
-        lib().oracle_sampling(self.h, _p(states, u64p), threads, bs, neg, bern, filt, _p(h, i64p), _p(t, i64p),
-                              _p(r, i64p), _p(y, f32p))
-        return h, t, r, y
+        side = np.zeros(seq, dtype=np.int8)
+        lib().oracle_sampling_sides(self.h, _p(states, u64p), threads, bs, neg, bern, filt, _p(h, i64p),
+                                    _p(t, i64p), _p(r, i64p), _p(y, f32p), side.ctypes.data if sides else None)
+        return (h, t, r, y, side) if sides else (h, t, r, y)
 
     def universe(self, rng, tc, balance):
         em = np.full(max(self.ent_total, 1), -1, dtype=np.int64)
