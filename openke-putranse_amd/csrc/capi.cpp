@@ -314,9 +314,15 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     const size_t per_call = 16 * bs + 8 * bs * neg + 4 * cs + 4 * ss + 4 + 1024;
     int64_t chunk = (int64_t)std::max<size_t>(1, ((size_t)512 << 20) / per_call);
     chunk = std::min(chunk, kCsrChunk);
+    // the step's gradient rows of the corrupted entities: per-positive base rows + per-slot (positive,
+    // scale) when k_step_csr takes the base-row form, else one contribution row per slot
+    pt::StepParams Q = t->P;
+    Q.batch_size = bs;
+    Q.neg = neg;
+    const bool base = pt::step_base_ok(Q);
     const size_t a_pos = al(16 * bs * chunk), a_neg = al(4 * bs * neg * chunk), a_off = a_neg,
-                 a_cnt = al(4 * cs * chunk), a_start = al(4 * ss * chunk), a_tick = al(4 * chunk),
-                 a_con = al(4 * bs * neg * D);
+                 a_cnt = al(4 * cs * chunk), a_start = al(4 * ss * chunk), a_tick = al(4 * chunk + 4),
+                 a_con = base ? al(4 * bs * 3 * D) + al(8 * bs * neg) : al(4 * bs * neg * D);
     const size_t need = a_pos + a_neg + a_off + a_cnt + a_start + a_tick + a_con;
     PT_HIP(hipDeviceSynchronize());   // queued work may still use the old carving
     t->drop_graphs();
@@ -335,7 +341,15 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     t->csr.cnt = (int32_t *)b; b += a_cnt;
     t->csr.start = (int32_t *)b; b += a_start;
     t->csr.tick = (int32_t *)b; b += a_tick;
-    t->csr.contrib = (float *)b;
+    if (base) {
+        t->csr.contrib = nullptr;
+        t->csr.bases = (float *)b; b += al(4 * bs * 3 * D);
+        t->csr.info = (int2 *)b;
+    } else {
+        t->csr.contrib = (float *)b;
+        t->csr.bases = nullptr;
+        t->csr.info = nullptr;
+    }
     t->csr.cnt_stride = cs;
     t->csr.start_stride = ss;
     t->csr_bs = bs;
@@ -397,12 +411,13 @@ struct Timing {
 // calls <= csr_chunk): sampling + counting sort in LDS, one workgroup per call (then the stream advance)
 // or split over parts per call (then the destination resolve + stream advance), or the two-pass form
 // (global-atomic counts, separate scan) when no LDS plan fits. `forced` = PT_PATH_* or -1 (automatic).
-static int enqueue_sample_chunk(pt_trainer *t, pt_sampler *s, const pt::CsrWork &w, int64_t bs, int64_t neg,
+static int enqueue_sample_chunk(pt_trainer *t, pt_sampler *s, pt::CsrWork &w, int64_t bs, int64_t neg,
                                 int64_t bern, int64_t filter, int64_t calls, int forced, hipStream_t st, Timing *tm) {
     const pt::DeviceGraph dg = s->g->dev;
     const int64_t dpp = 1 + 2 * neg;
     const int path = choose_path(t, calls, bs, neg, forced);
     t->last_path = path;
+    w.rank_only = path == PT_PATH_PART;   // the split sampler leaves bucket ranks (the step resolves them)
     if (path == PT_PATH_FUSED) {
         PT_TIMED(0, pt::launch_sample_sort(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls,
                                            t->P.ent_total, w, st));
@@ -410,7 +425,6 @@ static int enqueue_sample_chunk(pt_trainer *t, pt_sampler *s, const pt::CsrWork 
     } else if (path == PT_PATH_PART) {
         PT_TIMED(0, pt::launch_sample_part(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls,
                                            part_count(calls, bs), t->P.ent_total, w, st));
-        PT_TIMED(1, pt::launch_resolve(w, bs, neg, calls, s->d_states, s->threads, st));
     } else {
         PT_TIMED(0, pt::launch_sample_csr(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls, w, st));
         PT_TIMED(1, pt::launch_scan_counts(w, t->P.ent_total, calls, s->d_states, s->threads, bs, dpp, st));
@@ -422,8 +436,9 @@ static int enqueue_sample_chunk(pt_trainer *t, pt_sampler *s, const pt::CsrWork 
 // counting-sort path: one sampling + one scan launch per chunk of up to kCsrChunk steps (the batch
 // stream does not depend on the tables, so it is drawn ahead), then k_step + k_apply per step.
 static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
-                       int64_t steps, float *d_losses, hipStream_t st, Timing *tm = nullptr) {
+                       int64_t steps, float *d_losses, hipStream_t st, Timing *tm = nullptr, bool assign = false) {
     pt::StepParams P = t->P;
+    P.loss_assign = assign ? 1 : 0;   // d_losses[i] = step i's loss (no zeroing pass needed)
     P.batch_size = bs;
     P.neg = neg;
     P.inv_count = 1.0f / (float)(bs * neg);
@@ -524,7 +539,7 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
     // hold the stream in a short spin kernel while the host enqueues every measured launch, so each
     // kernel starts as soon as its predecessor ends (no host-side gaps inside an event pair)
     PT_HIP(pt::launch_spin(20000, st));
-    rc = enqueue_run(t, s, bs, neg, bern, filter, steps, d_losses, st, &tm);
+    rc = enqueue_run(t, s, bs, neg, bern, filter, steps, d_losses, st, &tm, true);
     if (rc) return rc;
     PT_HIP(hipStreamSynchronize(st));
     double tot[4] = {0, 0, 0, 0};
@@ -663,6 +678,10 @@ extern "C" int pt_trainer_sample_csr(pt_trainer *t, pt_sampler *s, int64_t bs, i
     PT_HIP(hipMemcpy2DAsync(h_start, 4 * (size_t)(E + 1), w.start, 4 * (size_t)w.start_stride, 4 * (size_t)(E + 1),
                             (size_t)calls, hipMemcpyDeviceToHost, st));
     PT_HIP(hipStreamSynchronize(st));
+    if (w.rank_only)   // split sampler: ranks inside the buckets -> destination rows
+        for (int64_t c = 0; c < calls; ++c)
+            for (int64_t o = 0; o < slots; ++o)
+                h_dst[c * slots + o] += h_start[c * (E + 1) + (h_neg[c * slots + o] >> 1)];
     for (size_t i = 0; i < pos.size(); ++i) {
         h_pos[3 * i] = pos[i].x;
         h_pos[3 * i + 1] = pos[i].y;
@@ -683,8 +702,7 @@ extern "C" int pt_trainer_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t 
         hipGraph_t graph;
         PT_HIP(hipStreamBeginCapture(t->cap, hipStreamCaptureModeThreadLocal));
         int erc = PT_OK;
-        if (hipMemsetAsync(d_losses, 0, sizeof(float) * (size_t)steps, t->cap) != hipSuccess) erc = PT_EHIP;
-        if (!erc) erc = enqueue_run(t, s, bs, neg, bern, filter, steps, d_losses, t->cap);
+        erc = enqueue_run(t, s, bs, neg, bern, filter, steps, d_losses, t->cap, nullptr, true);
         hipError_t ce = hipStreamEndCapture(t->cap, &graph);
         if (erc) return erc;
         PT_HIP(ce);

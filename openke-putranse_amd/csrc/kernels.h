@@ -16,6 +16,7 @@ struct StepParams {
     float *ent_acc, *rel_acc, *norm_acc;
     int64_t batch_size, neg;
     float inv_count;   // 1 / (batch_size * neg)
+    int loss_assign = 0;   // the apply pass stores the step's loss (=) instead of adding it (+=)
     int dbg = 0;       // timing experiments only (PT_STEP_DBG): bit 0 skip corrupted-row stores, bit 1 skip
                        // positive-row atomics, bit 2 skip negative row loads (results are then wrong)
 };
@@ -35,11 +36,19 @@ struct StepWorkspace {
 struct CsrWork {
     int4 *pos = nullptr;        // [calls][bs] (h, r, t, -)
     int32_t *neg = nullptr;     // [calls][bs*neg] entity << 1 | tail_side
-    int32_t *off = nullptr;     // [calls][bs*neg] rank inside the entity's bucket
+    int32_t *off = nullptr;     // [calls][bs*neg] destination row of the slot in the counting-sort order
+                                // (rank_only: its rank inside the entity's bucket; the step adds start[e])
     int32_t *cnt = nullptr;     // [calls][cnt_stride] bucket sizes (zero between uses)
     int32_t *start = nullptr;   // [calls][start_stride] exclusive prefix of cnt (E+1 used)
     float *contrib = nullptr;   // [bs*neg][dim] gradient rows of the corrupted entities (one step)
-    int32_t *tick = nullptr;    // [calls] parts of a call done (k_sample_part; zero between uses)
+    // base-row form (TransE, float4 rows): instead of contribution rows the step stores, per positive,
+    // its normalized rows [bs][3][dim] = (h-hat + r-hat, r-hat, t-hat) and, per slot at its destination,
+    // (positive << 1 | tail side, slot scale); the apply pass re-forms each slot's gradient row from them
+    float *bases = nullptr;
+    int2 *info = nullptr;       // [bs*neg]
+    int32_t *tick = nullptr;    // [calls + 1] parts of a call done, then calls done (k_sample_part; zero
+                                // between uses)
+    int rank_only = 0;          // off[] holds bucket ranks (k_sample_part) instead of destinations
     uint64_t *prof = nullptr;   // PT_PART_PROF=1 only: [workgroup][8] phase timestamps of k_sample_part
     int dbg = 0;                // timing experiments only (PT_PART_DBG; results then wrong): bit 0 no run
                                 // search, bit 1 no stream jump, bit 2 no 64-bit modulo
@@ -106,19 +115,21 @@ bool sample_sort_prepare(int64_t bs, int64_t neg, int64_t n, int64_t start_strid
 hipError_t launch_sample_sort(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                               int bern, int filter, int64_t calls, int64_t n, const CsrWork &w, hipStream_t st);
 // `parts` workgroups per call: sampling + LDS counting sort of each part, call-wide buckets reserved with
-// one atomic per touched bucket, the last part scans; then launch_resolve (destinations + stream advance).
+// one atomic per touched count word, the last part of a call scans, the last call advances the streams;
+// off[] holds bucket ranks (the caller sets CsrWork::rank_only for the step kernels).
 // sample_part_fits: whether the LDS plan of `parts` parts per call fits; sample_part_prepare: the same,
 // and raises the kernel's LDS limit (call outside any stream capture)
 bool sample_part_fits(int64_t bs, int64_t neg, int64_t n, int64_t parts);
 bool sample_part_prepare(int64_t bs, int64_t neg, int64_t n, int64_t parts);
-hipError_t launch_sample_part(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
+hipError_t launch_sample_part(const DeviceGraph &g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                               int bern, int filter, int64_t calls, int64_t parts, int64_t n, const CsrWork &w,
                               hipStream_t st);
-hipError_t launch_resolve(const CsrWork &w, int64_t bs, int64_t neg, int64_t calls, uint64_t *states, int64_t threads,
-                          hipStream_t st);
 hipError_t launch_scan_counts(const CsrWork &w, int64_t n, int64_t calls, uint64_t *states, int64_t threads,
                               int64_t bs, int64_t dpp, hipStream_t st);
 bool step_fits(const StepParams &P, int64_t neg, bool csr);
+// whether the counting-sort step for (P with its batch_size / neg) runs k_step_csr and can take the base-row
+// form (CsrWork::bases / info instead of contribution rows); opt-in with PT_STEP_BASE=1
+bool step_base_ok(const StepParams &P);
 hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t *states, int64_t threads, int bern,
                        int filter, const int64_t *bh, const int64_t *bt, const int64_t *br, const StepWorkspace &W,
                        float *loss, hipStream_t st, const CsrWork *csr = nullptr);

@@ -149,6 +149,28 @@ __device__ __forceinline__ void slot_search2(SlotDraw &d0, SlotDraw &d1) {
     if (d1.search) d1.e = rs_entity(d1.q);
 }
 
+// SL slots' boundary searches in lock step
+template <int SL>
+__device__ __forceinline__ void slot_searchN(SlotDraw (&d)[SL]) {
+    for (;;) {
+        bool a[SL], any = false;
+#pragma unroll
+        for (int i = 0; i < SL; ++i) { a[i] = rs_open(d[i].q); any |= a[i]; }
+        if (!any) break;
+        int32_t m[SL], v[SL];
+#pragma unroll
+        for (int i = 0; i < SL; ++i) m[i] = a[i] ? rs_probe(d[i].q) : 0;
+#pragma unroll
+        for (int i = 0; i < SL; ++i) v[i] = a[i] ? d[i].q.vals[m[i]] : 0;   // only open searches load
+#pragma unroll
+        for (int i = 0; i < SL; ++i)
+            if (a[i]) rs_update(d[i].q, m[i], v[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+        if (d[i].search) d[i].e = rs_entity(d[i].q);
+}
+
 // Sampling + counting sort of one sampled call per workgroup, entirely in LDS (when the bucket counts
 // and the call's positives fit): the positives are drawn once (not once per slot), every slot's
 // negative reserves its rank with an LDS atomic, the counts are scanned in LDS and every slot's
@@ -268,10 +290,10 @@ __device__ __forceinline__ int32_t lds_bucket(const int32_t *cnt, int64_t e) {
 // each touched bucket's range in the call's global counts with ONE returning atomic per touched count
 // word and turns its slots' LDS ranks into ranks inside the call-wide buckets. The part whose ticket add comes last exchanges the global counts with zeros (atomics on
 // both sides: every part's adds are seen, and the counts are clear for the next chunk) and scans them
-// into start[]. k_resolve then adds start[entity] to every slot's rank (its destination row) and
-// advances the sampler streams, which this kernel only reads.
-template <int NT, bool PACK>
-__global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, const uint64_t *__restrict__ states,
+// into start[]; the last call's last part then advances the sampler streams. off[] keeps the ranks
+// (CsrWork::rank_only): the step kernel adds start[entity] when it loads a slot's record.
+template <int NT, bool PACK, int SL>
+__global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *states,
                                                     int64_t threads, int64_t bs, int64_t neg, int bern, int filter,
                                                     int64_t parts, CsrWork w) {
     extern __shared__ __attribute__((aligned(16))) int32_t lds[];
@@ -315,24 +337,26 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, const uint64_
     // relative to b0 walked incrementally
     const int32_t neg32 = (int32_t)neg, db = NT / neg32, dk = NT - db * neg32;
     int32_t b = tid / neg32, k = tid - b * neg32;
-    for (int64_t o = o0 + tid; o < o1; o += 2 * NT) {
-        int32_t b2 = b + db, k2 = k + dk;
-        if (k2 >= neg32) { k2 -= neg32; ++b2; }
-        const bool two = o + NT < o1;
-        SlotDraw d0 = slot_prepare(pi + 12 * b, k, E, filter, g, jt, w.dbg);
-        SlotDraw d1 = slot_prepare(pi + 12 * (two ? b2 : b), two ? k2 : k, E, filter, g, jt, w.dbg);
-        if (!two) { d1.q.l = 0; d1.q.r = 1; d1.search = false; }
-        slot_search2(d0, d1);
-        const int64_t e0 = d0.e;
-        nrec[o] = (int32_t)((e0 << 1) | d0.side);
-        noff[o] = lds_rank<PACK>(cnt, e0);
-        if (two) {
-            const int64_t e1 = d1.e;
-            nrec[o + NT] = (int32_t)((e1 << 1) | d1.side);
-            noff[o + NT] = lds_rank<PACK>(cnt, e1);
+    for (int64_t o = o0 + tid; o < o1; o += SL * NT) {
+        // SL slots o + i*NT per iteration, their run searches in lock step; a slot past the end draws nothing
+        SlotDraw d[SL];
+        int32_t bi = b, ki = k;
+#pragma unroll
+        for (int i = 0; i < SL; ++i) {
+            const bool live = o + i * NT < o1;
+            d[i] = slot_prepare(pi + 12 * (live ? bi : b), live ? ki : k, E, filter, g, jt, w.dbg);
+            if (!live) { d[i].q.l = 0; d[i].q.r = 1; d[i].search = false; }
+            bi += db; ki += dk;
+            if (ki >= neg32) { ki -= neg32; ++bi; }
         }
-        b = b2 + db; k = k2 + dk;
-        if (k >= neg32) { k -= neg32; ++b; }
+        slot_searchN<SL>(d);
+#pragma unroll
+        for (int i = 0; i < SL; ++i) {
+            if (o + i * NT >= o1) break;
+            nrec[o + i * NT] = (int32_t)((d[i].e << 1) | d[i].side);
+            noff[o + i * NT] = lds_rank<PACK>(cnt, d[i].e);
+        }
+        b = bi; k = ki;
     }
     __syncthreads();
     PT_PHASE(2);
@@ -413,20 +437,14 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, const uint64_
     if (tid == NT - 1) start[E] = run;   // the last thread's chunk ends at the end (or is empty): run = total
     PT_PHASE(6);
 #undef PT_PHASE
-}
-
-// destination rows of the split sampler's slots: rank inside the bucket + start[entity]; block (0, 0)
-// advances the sampler streams past all `calls` calls' draws
-__global__ __launch_bounds__(256) void k_resolve(CsrWork w, int64_t slots, uint64_t *states, int64_t threads,
-                                                 int64_t bs, int64_t dpp, int64_t calls) {
-    const int64_t call = blockIdx.y;
-    if (blockIdx.x == 0 && call == 0 && threadIdx.x < 64)
-        advance_states(states, threads, bs, dpp * calls, (int)threadIdx.x);
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= slots) return;
-    const int32_t *start = w.start + call * w.start_stride;
-    const int64_t o = call * slots + i;
-    w.off[o] += start[w.neg[o] >> 1];
+    // the last call's last part advances the sampler streams past every call's draws: every part of every
+    // call read them (positive draws) before its count atomics and tickets
+    __syncthreads();
+    if (tid == 0) is_last = atomicAdd(&w.tick[gridDim.x / parts], 1) == (int32_t)(gridDim.x / parts - 1);
+    __syncthreads();
+    if (!is_last) return;
+    if (tid == 0) w.tick[gridDim.x / parts] = 0;
+    if (tid < 64) advance_states(states, threads, bs, dpp * (int64_t)(gridDim.x / parts), tid);
 }
 
 // exclusive scan of the bucket sizes (one workgroup of 1024 threads, tiles of 16384 counts: 16
@@ -800,9 +818,18 @@ static size_t sample_part_lds(int64_t bs, int64_t neg, int64_t n, int64_t parts)
     return jump_tab_bytes(neg) + 4 * (size_t)((cw + 3) & ~int64_t(3)) + 48 * (size_t)np;
 }
 
+// lock-step slots per thread: 4 when a part holds >= 3 slots per thread, else 2
+static int part_sl(int64_t bs, int64_t neg, int64_t parts) {
+    const int64_t per = (bs + parts - 1) / parts * neg;
+    return per >= 3 * part_nt() ? 4 : 2;
+}
+
 template <int NT, bool PACK>
 static hipError_t part_attr() {
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_sample_part<NT, PACK>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_sample_part<NT, PACK, 2>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSampleSortLds);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_sample_part<NT, PACK, 4>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSampleSortLds);
 }
 
@@ -821,7 +848,7 @@ bool sample_part_prepare(int64_t bs, int64_t neg, int64_t n, int64_t parts) {
     }
 }
 
-hipError_t launch_sample_part(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
+hipError_t launch_sample_part(const DeviceGraph &g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                               int bern, int filter, int64_t calls, int64_t parts, int64_t n, const CsrWork &w,
                               hipStream_t st) {
     if (!sample_part_fits(bs, neg, n, parts) || n + 1 > w.start_stride || n > w.cnt_stride || !w.tick)
@@ -829,27 +856,18 @@ hipError_t launch_sample_part(const DeviceGraph &g, const uint64_t *states, int6
     const size_t lds = sample_part_lds(bs, neg, n, parts);
     const dim3 grid((unsigned)(calls * parts));
     const bool pk = part_pack(bs, neg);
-#define PT_PART(NT_)                                                                                           \
-    if (part_nt() == NT_) {                                                                                  \
-        if (pk)                                                                                              \
-            hipLaunchKernelGGL((dev::k_sample_part<NT_, true>), grid, dim3(NT_), lds, st, g, states, threads, \
-                               bs, neg, bern, filter, parts, w);                                              \
-        else                                                                                                 \
-            hipLaunchKernelGGL((dev::k_sample_part<NT_, false>), grid, dim3(NT_), lds, st, g, states, threads, \
-                               bs, neg, bern, filter, parts, w);                                              \
+    const int sl = part_sl(bs, neg, parts);
+#define PT_PART(NT_, PK_, SL_)                                                                                 \
+    if (part_nt() == NT_ && pk == PK_ && sl == SL_) {                                                        \
+        hipLaunchKernelGGL((dev::k_sample_part<NT_, PK_, SL_>), grid, dim3(NT_), lds, st, g, states, threads, \
+                           bs, neg, bern, filter, parts, w);                                                  \
         return hipGetLastError();                                                                            \
     }
-    PT_PART(256) PT_PART(512) PT_PART(1024)
+    PT_PART(256, true, 2) PT_PART(256, true, 4) PT_PART(256, false, 2) PT_PART(256, false, 4)
+    PT_PART(512, true, 2) PT_PART(512, true, 4) PT_PART(512, false, 2) PT_PART(512, false, 4)
+    PT_PART(1024, true, 2) PT_PART(1024, true, 4) PT_PART(1024, false, 2) PT_PART(1024, false, 4)
 #undef PT_PART
     return hipErrorInvalidValue;
-}
-
-hipError_t launch_resolve(const CsrWork &w, int64_t bs, int64_t neg, int64_t calls, uint64_t *states, int64_t threads,
-                          hipStream_t st) {
-    const int64_t slots = bs * neg;
-    const dim3 grid((unsigned)((slots + 255) / 256), (unsigned)calls);
-    hipLaunchKernelGGL(dev::k_resolve, grid, dim3(256), 0, st, w, slots, states, threads, bs, 1 + 2 * neg, calls);
-    return hipGetLastError();
 }
 
 hipError_t launch_scan_counts(const CsrWork &w, int64_t n, int64_t calls, uint64_t *states, int64_t threads,

@@ -22,7 +22,7 @@ PT_SGD, PT_ADAGRAD = 0, 1
 # sampling paths of the counting-sort (large neg) step (include/putranse.h PT_PATH_*)
 PT_PATH_TWO_PASS, PT_PATH_FUSED, PT_PATH_PART, PT_PATH_SAMPLED = 0, 1, 2, 3
 PATH_KERNELS = {PT_PATH_TWO_PASS: ("k_sample_csr", "k_scan_counts"), PT_PATH_FUSED: ("k_sample_sort", "k_advance"),
-                PT_PATH_PART: ("k_sample_part", "k_resolve"), PT_PATH_SAMPLED: (None, None)}
+                PT_PATH_PART: ("k_sample_part", None), PT_PATH_SAMPLED: (None, None)}
 
 
 class NativeError(RuntimeError):
