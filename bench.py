@@ -228,8 +228,10 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True):
            "universes_per_gpu": len(own), "host_universe_build_s": build_s,
            "roofline": {"bound": "latency (per-universe dependent step chain)", "achieved_per_gpu": achieved,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                        "note": "algorithmic bytes per wall second vs HBM peak; a universe's tables, state and "
-                                "contribution slots live in LDS, so frac > 1 (C4) means on-chip service, not HBM"}}
+                        "note": "algorithmic bytes (SURVEY 8(d) per slot) per wall second vs the HBM peak, not an HBM "
+                                "measurement: a universe's working set (tables, Adagrad state, contribution rows, "
+                                "a few hundred KB) is cache-resident and its work lists, relation gradient rows and "
+                                "presampled batches live in LDS, so frac > 1 (C4) means on-chip service"}}
     if do_lp:
         out["link_prediction"] = universe_link_prediction(L, path, unis, mid, p_norm, ws, dev)
     L.pt_graph_free(g)
@@ -464,7 +466,9 @@ def main():
     names = list(_native.PATH_KERNELS.get(path, ("sampling", "bucket scan"))) + step_names
     per_kernel = {n: float(v) for n, v in zip(names, ms4) if n and v > 0}
     bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
-    achieved = bytes_step / (sum(per_kernel.values()) * 1e-3) / 1e9
+    step_kernel_s = sum(per_kernel.values()) * 1e-3
+    achieved = bytes_step / step_kernel_s / 1e9
+    traffic = load_traffic(args.workload)
 
     c3 = None if args.no_c3 else run_universes(args, ws, rank, dev, "c3", cpu=False)
     if rank != 0:
@@ -492,10 +496,16 @@ def main():
                    "global_batch": seq * ws, "slots_per_step_per_gpu": seq,
                    "parallelism": "replicas%d" % ws if ws > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.workload),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "one training step = " + " + ".join(per_kernel),
                      "ms_per_kernel": per_kernel,
-                     "algorithmic_bytes_per_step": bytes_step},
+                     "algorithmic_bytes_per_step": bytes_step,
+                     "hbm_frac": None if traffic is None else traffic / (step_kernel_s * 1e9) / HBM_PEAK_GBS,
+                     "note": "achieved / frac: SURVEY 8(d) algorithmic bytes per step over the summed kernel time "
+                             "(HIP events); traffic: measured HBM bytes per step (rocprofv3 PMC, profiles/"
+                             "pmc_c2.json), lower than the algorithmic count because the %.1f MB entity table is "
+                             "Infinity-Cache resident; hbm_frac = measured traffic over the same time vs the "
+                             "HBM peak" % (4e-6 * dl.get_ent_tot() * dim)},
         "loss_last_step": loss_last,
     }
     if c3 is not None:

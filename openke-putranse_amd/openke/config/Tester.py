@@ -172,6 +172,11 @@ class Tester(object):
             elif total_false == total_true:
                 return 0.5, threshlod
         acc = 0
+        if threshlod is None and len(res):
+            # no threshold with a positive accuracy (e.g. a single negative score): the reference's loop fails
+            # at its first comparison `score > threshlod` (Tester.py:183-184); fail the same way
+            raise TypeError("'>' not supported between instances of 'numpy.float64' and 'NoneType' "
+                            "(get_best_threshlod found no threshold, Tester.py:120-139)")
         above = np.nonzero(res[:, 1] > threshlod)[0] if threshlod is not None else np.zeros(0, dtype=np.int64)
         if len(above):
             index = int(above[0])

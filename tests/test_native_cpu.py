@@ -162,3 +162,48 @@ def test_ranking_and_metrics_match_reference(path):
                                   ranks[3].ctypes.data, n, met.ctypes.data))
     np.testing.assert_array_equal(met[:5], z["metrics"].astype(np.float32))
     L.pt_known_free(known)
+
+
+def _reference_best_threshold(score, ans):
+    """Literal restatement of the reference's get_best_threshlod loop (Tester.py:120-139)."""
+    res = np.concatenate([ans.reshape(-1, 1), score.reshape(-1, 1)], axis=-1)[np.argsort(score)]
+    total_all = float(len(score))
+    total_false = total_all - np.sum(ans)
+    cur, mx, thr = 0.0, 0.0, None
+    for index, (a, s) in enumerate(res):
+        if a == 1:
+            cur += 1.0
+        v = (2 * cur + total_false - index - 1) / total_all
+        if v > mx:
+            mx, thr = v, s
+    return thr, mx
+
+
+def test_best_threshold_matches_reference_loop():
+    """Tester.get_best_threshlod (vectorized) equals the reference loop on random and tied scores."""
+    from openke.config import Tester
+    t = Tester()
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 7, 100, 1000):
+        for ties in (False, True):
+            score = rng.integers(0, 5, n).astype(np.float32) if ties else rng.standard_normal(n).astype(np.float32)
+            ans = rng.integers(0, 2, n)
+            assert t.get_best_threshlod(score, ans) == _reference_best_threshold(score, ans)
+
+
+def test_classification_without_threshold_raises_like_reference():
+    """No threshold with a positive accuracy (a lone negative score): the reference's loop raises TypeError
+    at `score > None` (Tester.py:183-184); the drop-in raises the same error instead of returning 0."""
+    from openke.config import Tester
+
+    class _Scores(Tester):
+        def test_one_step(self, data):
+            return np.asarray(data, dtype=np.float32)
+
+    t = _Scores()
+    assert t.get_best_threshlod(np.array([0.5], np.float32), np.array([0]))[0] is None
+    with pytest.raises(TypeError):
+        t.run_triple_classification(data_iterator=[([], [0.5])])
+    # a usable threshold: the reference's accuracy formula (Tester.py:182-190)
+    acc, thr = t.run_triple_classification(data_iterator=[([0.1, 0.2], [0.9, 0.3])])
+    assert thr == np.float32(0.2) and acc == 1.0
