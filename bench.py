@@ -117,7 +117,7 @@ def _xavier(rng, rows, dim):
     return rng.uniform(-b, b, (rows, dim)).astype(np.float32)
 
 
-def run_universes(args, ws, rank, dev, name="c3", cpu=True):
+def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
     """PuTransE / PuTransH universes: universe k on rank k % N (no collective in training), Adagrad,
     neg 1, bern 0, filter 0, nbatches 20, 8 sampler threads. One step = every universe's full training
     run (all its epochs) in one persistent launch. C4 adds link prediction over the test split: each
@@ -126,6 +126,9 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True):
     from openke import _native
     L = _native.lib()
     shape, n_univ, model, dim_spec, p_norm, tc_range, margin_range, do_lp = PU_WORKLOADS[name]
+    if per_gpu:   # weak scaling: the workload's universe count on EVERY GPU (universes 4+k continue the seeds)
+        n_univ *= ws
+        do_lp = False
     path = synth_kg.ensure_dataset(os.path.join(args.data_dir, "rank%d" % rank), shape)
     g = ctypes.c_void_p()
     _native.check(L.pt_graph_load(path.encode(), ctypes.byref(g)))
@@ -223,7 +226,7 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True):
                        "nbatches 20" % (name.upper(), model, shape, n_univ,
                                         "U{%d..%d}" % dim_spec if isinstance(dim_spec, tuple) else dim_spec, p_norm,
                                         tc_range[0], tc_range[1]),
-           "value": slots_all * args.c3_steps / el, "unit": "triples/s", "scaling": "strong",
+           "value": slots_all * args.c3_steps / el, "unit": "triples/s", "scaling": "weak" if per_gpu else "strong",
            "steps": args.c3_steps, "warmup": args.c3_warmup, "s_per_step": el / args.c3_steps,
            "universes_per_gpu": len(own), "host_universe_build_s": build_s,
            "roofline": {"bound": "latency (per-universe dependent step chain)", "achieved_per_gpu": achieved,
@@ -461,9 +464,9 @@ def main():
     _native.check(L.pt_trainer_run_timed(tr._native, sampler, bs, neg, bern, filt, n_t, _native.ptr(tl), ms4,
                                          _native.stream()))
     # the sampling kernels of the path the library took for this chunking (pt_trainer_last_path)
-    path = L.pt_trainer_last_path(tr._native)
-    step_names = ["k_step_csr", "k_apply_buf"] if path != _native.PT_PATH_SAMPLED else ["k_step_sampled", "k_apply"]
-    names = list(_native.PATH_KERNELS.get(path, ("sampling", "bucket scan"))) + step_names
+    spath = L.pt_trainer_last_path(tr._native)
+    step_names = ["k_step_csr", "k_apply_buf"] if spath != _native.PT_PATH_SAMPLED else ["k_step_sampled", "k_apply"]
+    names = list(_native.PATH_KERNELS.get(spath, ("sampling", "bucket scan"))) + step_names
     per_kernel = {n: float(v) for n, v in zip(names, ms4) if n and v > 0}
     bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
     step_kernel_s = sum(per_kernel.values()) * 1e-3
@@ -471,6 +474,8 @@ def main():
     traffic = load_traffic(args.workload)
 
     c3 = None if args.no_c3 else run_universes(args, ws, rank, dev, "c3", cpu=False)
+    # universe weak scaling (512 universes per GPU, no collective): at N = 1 it is the strong line
+    c3w = None if args.no_c3 or ws == 1 else run_universes(args, ws, rank, dev, "c3", cpu=False, per_gpu=True)
     if rank != 0:
         if ws > 1:
             import torch.distributed as dist
@@ -510,6 +515,8 @@ def main():
     }
     if c3 is not None:
         rec["pu_c3"] = c3
+    if c3w is not None:
+        rec["pu_c3_weak"] = c3w
     if ws == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(path, wl, args.cpu_seconds)
     print(json.dumps(rec), flush=True)

@@ -32,26 +32,35 @@ print(json.dumps(out, indent=1))
 
 # HBM traffic of one C2 training step for bench.py's roofline.traffic (MI355X_MICROARCH.md §HBM:
 # FETCH_SIZE / WRITE_SIZE are kilobytes; on gfx950 FETCH_SIZE counts half the bytes of wide coalesced
-# reads, so it is doubled; WRITE_SIZE is exact for streaming stores and float atomics)
+# reads, so it is doubled; WRITE_SIZE is exact for streaming stores and float atomics).
+# Per step = mean per dispatch of the step kernel + mean per dispatch of the apply kernel + the sampling
+# kernels' total over the steps they sampled (argv[3]; bench.py --steps K --warmup W samples W + 3K steps:
+# warmup, graph capture run, timed run, measurement run; the isolation re-timing loops sample nothing).
 if len(sys.argv) > 2:
-    step_kernels = ("k_sample_csr", "k_scan_counts", "k_sample_sort", "k_advance", "k_step_csr", "k_step_sampled", "k_apply")
-    fetch = write = 0.0
+    sampled = float(sys.argv[3]) if len(sys.argv) > 3 else None
+    samplers = ("k_sample_csr", "k_scan_counts", "k_sample_sort", "k_advance", "k_sample_part")
+    per_step = ("k_step_csr", "k_step_sampled", "k_apply")
+    def kb(d):
+        return 2.0 * sum(d.get("FETCH_SIZE", [])) + sum(d.get("WRITE_SIZE", []))
+    total = 0.0
     steps = 0
+    parts = {}
     for k, d in vals.items():
-        if not any(s in k for s in step_kernels):
-            continue
-        fetch += sum(d.get("FETCH_SIZE", []))
-        write += sum(d.get("WRITE_SIZE", []))
-        if "k_step_csr" in k or "k_step_sampled" in k:
-            steps = max(steps, len(d.get("FETCH_SIZE", [])))
-    if steps:
-        rec = {"bytes_per_step": (2.0 * fetch + write) * 1024.0 / steps,
-               "fetch_kb_per_step_raw": fetch / steps, "write_kb_per_step": write / steps,
-               "steps_counted": steps,
+        short = k.split("(")[0][-60:]
+        n = len(d.get("FETCH_SIZE", []))
+        if any(s in k for s in per_step) and n:
+            parts[short] = kb(d) / n * 1024.0
+            if "k_step" in k:
+                steps = max(steps, n)
+        elif any(s in k for s in samplers) and n and sampled:
+            parts[short] = kb(d) / sampled * 1024.0
+    if parts:
+        rec = {"bytes_per_step": sum(parts.values()), "bytes_per_step_by_kernel": parts,
+               "step_dispatches_counted": steps, "sampled_steps": sampled,
                "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py; "
-                         "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B summed over k_sample_sort, k_advance, k_sample_csr, k_scan_counts, "
-                         "k_step_csr, k_apply_buf dispatches / k_step_csr dispatches",
+                         "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B: mean per dispatch of the step and apply "
+                         "kernels + the sampling kernels' total / sampled steps",
                "per_kernel": {k.split("(")[0][-60:]: {cn: sum(v) / len(v) for cn, v in d.items()}
-                              for k, d in vals.items() if any(s in k for s in step_kernels)}}
+                              for k, d in vals.items() if any(s in k for s in samplers + per_step)}}
         json.dump(rec, open(sys.argv[2], "w"), indent=1)
         print("wrote", sys.argv[2], rec["bytes_per_step"])

@@ -10,7 +10,7 @@ EXTRA=${2:-}
 i=0
 for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
     i=$((i+1))
-    timeout -k 10 240 rocprofv3 --kernel-trace --pmc $set -d gpurun_out/pmc/p$i -o run --output-format csv -- python3 bench.py --steps 200 --warmup 3 --no-cpu-baseline $EXTRA > gpurun_out/pmc/p$i.log 2>&1
+    timeout -k 10 240 rocprofv3 --kernel-trace --pmc $set -d gpurun_out/pmc/p$i -o run --output-format csv -- python3 bench.py --steps ${STEPS:-20} --warmup ${WARMUP:-5} --no-cpu-baseline $EXTRA > gpurun_out/pmc/p$i.log 2>&1
     rc=$?
     echo "pmc $i ($set) rc=$rc" >> gpurun_out/steps.log
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
