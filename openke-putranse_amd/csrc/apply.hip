@@ -36,7 +36,6 @@ struct ApplyTable {
     int jacobian;
     const int *start;       // CSR of extra contribution rows (NULL: none): rows start[r] .. start[r+1]-1
     const float *contrib;   // [n][dim]
-    const int2 *info;       // base-row form (k_apply_base): per contribution (positive << 1 | tail side, scale)
 };
 struct ApplyParams {
     ApplyTable t[3];
@@ -51,8 +50,6 @@ struct ApplyParams {
     const float *lpart;   // [bs] per-positive loss partials of the step
     float margin, inv_count;
     int dbg;   // timing experiments only (PT_STEP_DBG bit 3: contribution rows read from a 4096-row hot window)
-    const float *bases;   // base-row form: [bs][3][dim] per positive (h-hat + r-hat, r-hat, t-hat)
-    int norm_flag;
     int loss_assign;
 };
 
@@ -255,97 +252,6 @@ __global__ __launch_bounds__(256) void k_apply_buf(ApplyParams A) {
     }
 }
 
-// Apply pass of the base-row form (TransE, float4 rows, raw buffers; one lane group per table row). An
-// entity row's contributions are not stored rows: contribution j names its slot's positive, side and scale
-// (info[j], written by k_step_csr<BASE>), and the slot's gradient row is re-formed here exactly as the step
-// formed it - v = (h-hat + r-hat) - e-hat for a corrupted tail, (e-hat + r-hat) - t-hat for a corrupted head,
-// from the positive's stored normalized rows and this row's pre-step normalization - then scaled: p = 2
-// v * scale, p = 1 sgn(v) * scale. Contributions are summed in bucket order after the row's own gradient
-// row, as k_apply_buf sums stored rows. The bases (3 rows per positive, a few MB) stay cache-resident, so
-// the contribution rows' HBM write + read of k_step_csr / k_apply_buf is gone.
-template <int G, int VEC, int KCH, int NC, int PN>
-__global__ __launch_bounds__(256) void k_apply_base(ApplyParams A) {
-    using Vec = V<G, VEC, KCH>;
-    constexpr int GPB = 256 / G;
-    const int lane = threadIdx.x % G;
-    int64_t r = uni<G>((int32_t)(blockIdx.x * GPB + threadIdx.x / G));   // scalar at G = 64
-    if (blockIdx.x == 0 && threadIdx.x < 64) apply_block0(A);
-    const int D = (int)A.dim;
-    const uint32_t rowb = (uint32_t)D * 4u;
-    int ti = 0;
-    while (ti < A.ntab && r >= A.t[ti].rows) {
-        r -= A.t[ti].rows;
-        ++ti;
-    }
-    if (ti >= A.ntab) return;
-    const ApplyTable &T = A.t[ti];
-    const uint32_t tb = (uint32_t)T.rows * rowb;
-    Vec x, a, g;
-    bload(x, make_rsrc(T.w, tb), (uint32_t)r * rowb, D, lane);
-    if (A.opt != 0) bload(a, make_rsrc(T.acc, tb), (uint32_t)r * rowb, D, lane);
-    const int flag = T.flag[r];
-    int c0 = 0, c1 = 0;
-    if (T.start) {
-        c0 = T.start[r];
-        c1 = T.start[r + 1];
-    }
-    bload(g, make_rsrc(T.grad, tb), flag ? (uint32_t)r * rowb : kOob, D, lane);
-    if (!flag && c0 == c1) return;   // untouched row: unchanged
-    if (c1 > c0) {
-        Vec eh;
-        if (A.norm_flag) vnormalize<true>(x, eh); else eh = x;
-        const auto b_rs = make_rsrc(A.bases, 0x7fffffffu);
-        for (int j = c0; j < c1; j += NC) {
-            int2 inf[NC];
-#pragma unroll
-            for (int q = 0; q < NC; ++q) inf[q] = j + q < c1 ? T.info[j + q] : make_int2(0, 0);
-            Vec B0[NC], B1[NC];
-#pragma unroll
-            for (int q = 0; q < NC; ++q) {
-                const bool tail = inf[q].x & 1, live = inf[q].y != 0;   // scale 0: inactive pair or past the end
-                const uint32_t b3 = (uint32_t)(inf[q].x >> 1) * 3u;
-                bload(B0[q], b_rs, live ? (b3 + (tail ? 0u : 1u)) * rowb : kOob, D, lane);
-                bload(B1[q], b_rs, live && !tail ? (b3 + 2u) * rowb : kOob, D, lane);
-            }
-#pragma unroll
-            for (int q = 0; q < NC; ++q) {
-                const float sc = __int_as_float(inf[q].y);
-                const bool tail = inf[q].x & 1;
-#pragma unroll
-                for (int i = 0; i < Vec::N; ++i) {
-                    const float v = tail ? B0[q].x[i] - eh.x[i] : (eh.x[i] + B0[q].x[i]) - B1[q].x[i];
-                    g.x[i] += PN == 2 ? v * sc : (v > 0.f ? sc : (v < 0.f ? -sc : 0.f));
-                }
-            }
-        }
-    }
-    Vec gg;
-    if (T.jacobian) {
-        const float n = sqrtf(vdot(x, x));
-        vnormalize_bwd(x, n, g, gg);
-    } else {
-        gg = g;
-    }
-    if (A.opt == 0) {
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) x.x[i] = x.x[i] + (-A.lr) * gg.x[i];
-    } else {
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            a.x[i] = a.x[i] + gg.x[i] * gg.x[i];
-            x.x[i] = x.x[i] + (-A.lr) * gg.x[i] / (sqrtf(a.x[i]) + 1e-10f);
-        }
-        bstore(a, make_rsrc(T.acc, tb), (uint32_t)r * rowb, D, lane);
-    }
-    bstore(x, make_rsrc(T.w, tb), (uint32_t)r * rowb, D, lane);
-    if (flag) {
-        Vec z;
-        vzero(z);
-        bstore(z, make_rsrc(T.grad, tb), (uint32_t)r * rowb, D, lane);
-        if (lane == 0) T.flag[r] = 0;
-    }
-}
-
 // Apply pass, RPW consecutive rows per lane group with all their loads in flight together (the
 // one-row-per-group form is a chain of two dependent memory round trips per row). Consecutive entity
 // rows own consecutive counting-sort contribution ranges, so a group streams ONE contiguous range
@@ -464,13 +370,10 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
     A.ntab = 0;
     const int ent_j = P.model == 0 && P.norm_flag;
     A.t[A.ntab++] = dev::ApplyTable{P.ent, P.ent_acc, W.gent, W.fent, P.ent_total, ent_j,
-                                    csr ? csr->start : nullptr, csr ? csr->contrib : nullptr,
-                                    csr ? csr->info : nullptr};
-    A.t[A.ntab++] = dev::ApplyTable{P.rel, P.rel_acc, W.grel, W.frel, P.rel_total, P.norm_flag, nullptr, nullptr,
-                                    nullptr};
+                                    csr ? csr->start : nullptr, csr ? csr->contrib : nullptr};
+    A.t[A.ntab++] = dev::ApplyTable{P.rel, P.rel_acc, W.grel, W.frel, P.rel_total, P.norm_flag, nullptr, nullptr};
     if (P.model == 1)
-        A.t[A.ntab++] = dev::ApplyTable{P.normv, P.norm_acc, W.gnorm, W.fnorm, P.rel_total, 1, nullptr, nullptr,
-                                        nullptr};
+        A.t[A.ntab++] = dev::ApplyTable{P.normv, P.norm_acc, W.gnorm, W.fnorm, P.rel_total, 1, nullptr, nullptr};
     A.dim = P.dim;
     A.opt = P.opt;
     A.lr = P.lr;
@@ -483,32 +386,9 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
     A.margin = P.margin;
     A.inv_count = P.inv_count;
     A.dbg = P.dbg;
-    A.bases = csr ? csr->bases : nullptr;
-    A.norm_flag = P.norm_flag;
     A.loss_assign = P.loss_assign;
     int64_t rows = 0;
     for (int i = 0; i < A.ntab; ++i) rows += A.t[i].rows;
-    // base-row form (set only when k_step_csr<BASE> runs: TransE, float4 rows)
-    if (csr && csr->bases) {
-        const int64_t chunks = P.dim / 4;
-        int G = 2;
-        while (G < chunks && G < 64) G <<= 1;
-        const int KCH = (int)((chunks + G - 1) / G);
-        const int64_t gpb4 = 256 / G;
-        const dim3 grid((unsigned)((rows + gpb4 - 1) / gpb4)), block(256);
-#define PT_APPLYBASE(G_, K_)                                                                     \
-        if (G == G_ && KCH == K_) {                                                             \
-            if (P.p_norm == 1)                                                                  \
-                hipLaunchKernelGGL((dev::k_apply_base<G_, 4, K_, 4, 1>), grid, block, 0, st, A);   \
-            else                                                                                \
-                hipLaunchKernelGGL((dev::k_apply_base<G_, 4, K_, 4, 2>), grid, block, 0, st, A);   \
-            return hipGetLastError();                                                           \
-        }
-        PT_APPLYBASE(2, 1) PT_APPLYBASE(4, 1) PT_APPLYBASE(8, 1) PT_APPLYBASE(16, 1) PT_APPLYBASE(32, 1)
-        PT_APPLYBASE(64, 1) PT_APPLYBASE(64, 2) PT_APPLYBASE(64, 3) PT_APPLYBASE(64, 4)
-#undef PT_APPLYBASE
-        return hipErrorInvalidValue;
-    }
     // float4 rows through raw buffers (PT_APPLY_OLD=1 keeps the kernels below)
     static const bool old_apply = [] {
         const char *v = getenv("PT_APPLY_OLD");

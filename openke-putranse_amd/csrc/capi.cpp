@@ -314,15 +314,9 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     const size_t per_call = 16 * bs + 8 * bs * neg + 4 * cs + 4 * ss + 4 + 1024;
     int64_t chunk = (int64_t)std::max<size_t>(1, ((size_t)512 << 20) / per_call);
     chunk = std::min(chunk, kCsrChunk);
-    // the step's gradient rows of the corrupted entities: per-positive base rows + per-slot (positive,
-    // scale) when k_step_csr takes the base-row form, else one contribution row per slot
-    pt::StepParams Q = t->P;
-    Q.batch_size = bs;
-    Q.neg = neg;
-    const bool base = pt::step_base_ok(Q);
     const size_t a_pos = al(16 * bs * chunk), a_neg = al(4 * bs * neg * chunk), a_off = a_neg,
                  a_cnt = al(4 * cs * chunk), a_start = al(4 * ss * chunk), a_tick = al(4 * chunk + 4),
-                 a_con = base ? al(4 * bs * 3 * D) + al(8 * bs * neg) : al(4 * bs * neg * D);
+                 a_con = al(4 * bs * neg * D);
     const size_t need = a_pos + a_neg + a_off + a_cnt + a_start + a_tick + a_con;
     PT_HIP(hipDeviceSynchronize());   // queued work may still use the old carving
     t->drop_graphs();
@@ -341,15 +335,7 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     t->csr.cnt = (int32_t *)b; b += a_cnt;
     t->csr.start = (int32_t *)b; b += a_start;
     t->csr.tick = (int32_t *)b; b += a_tick;
-    if (base) {
-        t->csr.contrib = nullptr;
-        t->csr.bases = (float *)b; b += al(4 * bs * 3 * D);
-        t->csr.info = (int2 *)b;
-    } else {
-        t->csr.contrib = (float *)b;
-        t->csr.bases = nullptr;
-        t->csr.info = nullptr;
-    }
+    t->csr.contrib = (float *)b;
     t->csr.cnt_stride = cs;
     t->csr.start_stride = ss;
     t->csr_bs = bs;

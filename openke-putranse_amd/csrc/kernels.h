@@ -41,11 +41,6 @@ struct CsrWork {
     int32_t *cnt = nullptr;     // [calls][cnt_stride] bucket sizes (zero between uses)
     int32_t *start = nullptr;   // [calls][start_stride] exclusive prefix of cnt (E+1 used)
     float *contrib = nullptr;   // [bs*neg][dim] gradient rows of the corrupted entities (one step)
-    // base-row form (TransE, float4 rows): instead of contribution rows the step stores, per positive,
-    // its normalized rows [bs][3][dim] = (h-hat + r-hat, r-hat, t-hat) and, per slot at its destination,
-    // (positive << 1 | tail side, slot scale); the apply pass re-forms each slot's gradient row from them
-    float *bases = nullptr;
-    int2 *info = nullptr;       // [bs*neg]
     int32_t *tick = nullptr;    // [calls + 1] parts of a call done, then calls done (k_sample_part; zero
                                 // between uses)
     int rank_only = 0;          // off[] holds bucket ranks (k_sample_part) instead of destinations
@@ -127,9 +122,6 @@ hipError_t launch_sample_part(const DeviceGraph &g, uint64_t *states, int64_t th
 hipError_t launch_scan_counts(const CsrWork &w, int64_t n, int64_t calls, uint64_t *states, int64_t threads,
                               int64_t bs, int64_t dpp, hipStream_t st);
 bool step_fits(const StepParams &P, int64_t neg, bool csr);
-// whether the counting-sort step for (P with its batch_size / neg) runs k_step_csr and can take the base-row
-// form (CsrWork::bases / info instead of contribution rows); opt-in with PT_STEP_BASE=1
-bool step_base_ok(const StepParams &P);
 hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t *states, int64_t threads, int bern,
                        int filter, const int64_t *bh, const int64_t *bt, const int64_t *br, const StepWorkspace &W,
                        float *loss, hipStream_t st, const CsrWork *csr = nullptr);

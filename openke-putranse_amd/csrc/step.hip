@@ -349,7 +349,7 @@ __device__ __forceinline__ int32_t gbcast(int32_t v, int j) {
     if constexpr (G == 64) return __builtin_amdgcn_readlane(v, j); else return __shfl(v, j, G);
 }
 
-template <int G, int VEC, int KCH, int NCH, int S, int PN, int NT = 256, bool BASE = false>
+template <int G, int VEC, int KCH, int NCH, int S, int PN, int NT = 256>
 __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, CsrWork cw) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = NT / G;      // lane groups per block
@@ -422,14 +422,6 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
             vpos.x[i] = bt.x[i] - th.x[i];
         }
         ps = vpnorm<true>(vpos, p);
-        if constexpr (BASE) {   // the positive's normalized rows, for the apply pass (one lane group stores)
-            if (sub == 0) {
-                const auto base_rs = make_rsrc(cw.bases, (uint32_t)(P.batch_size * 3) * rowb);
-                bstore(bt, base_rs, (uint32_t)(b * 3) * rowb, D, lane);
-                bstore(rh, base_rs, (uint32_t)(b * 3 + 1) * rowb, D, lane);
-                bstore(th, base_rs, (uint32_t)(b * 3 + 2) * rowb, D, lane);
-            }
-        }
         auto process = [&](Vec(&E)[NCH], int k0) {
 #pragma unroll
             for (int u = 0; u < NCH; ++u) {
@@ -455,16 +447,7 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
                 // slot gradient d loss / d e-hat: -g for a corrupted tail, +g for a corrupted head
                 // (g = dL/dv); an inactive pair stores zeros (the reserved slot must be defined)
                 vpnorm_bwd<true>(vk, ns, p, tail_side ? c : -c, gs);
-                if constexpr (BASE) {
-                    // the slot's scale (vpnorm_bwd's: p = 2 ds / ||v||, p = 1 ds) at its destination; the
-                    // apply pass re-forms v from the bases and the pre-step row and gets the same gs
-                    const float ds = tail_side ? c : -c;
-                    const float sc = p == 1 ? ds : (ns == 0.f ? 0.f : ds * frcp<true>(ns));
-                    if (lane == 0) cw.info[di] = make_int2((int32_t)(b << 1) | (tail_side ? 1 : 0),
-                                                                    __float_as_int(sc));
-                } else {
-                    bstore(gs, con_rs, (P.dbg & 1) ? kOob : slot, D, lane);
-                }
+                bstore(gs, con_rs, (P.dbg & 1) ? kOob : slot, D, lane);
                 if (tail_side) {
 #pragma unroll
                     for (int i = 0; i < Vec::N; ++i) At.x[i] -= gs.x[i];
@@ -620,14 +603,6 @@ static bool csr_fast_path(const StepParams &P) {
     return P.model == 0 && P.dim % 4 == 0 && fits31 && !old_step;
 }
 
-bool step_base_ok(const StepParams &P) {
-    // opt-in (PT_STEP_BASE=1): measured slower on C2 (k_step_csr -1.5 us, k_apply_base +2.9 us per step:
-    // the apply pass is latency-bound and the form adds a dependent load level, start -> info -> bases)
-    const char *v = getenv("PT_STEP_BASE");
-    if (!(v && atoi(v) != 0)) return false;
-    return csr_fast_path(P) && P.dbg == 0 && !getenv("PT_STEP_G") && !getenv("PT_STEP_S") && !getenv("PT_STEP_NCH");
-}
-
 // whether launch_step can take this (P, neg) on the in-kernel-sampled path: k_step_csr has no LDS
 // limit on neg; the sub-group kernel keeps a block's negative records in LDS (64 KB)
 bool step_fits(const StepParams &P0, int64_t neg, bool csr) {
@@ -682,13 +657,8 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
         if (G == G_ && KCH == K_ && nch == N_ && S == S_) {                                          \
             constexpr int NT_ = S_ * G_ >= 256 || 256 % (S_ * G_) != 0 ? S_ * G_ : 256;             \
             const dim3 grid((unsigned)((P.batch_size * S_ * G_ + NT_ - 1) / NT_)), block(NT_);        \
-            const bool base_ = csr->bases != nullptr;                                                \
-            if (P.p_norm == 1 && base_)                                                              \
-                hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 1, NT_, true>), grid, block, 0, st, P, sink, *csr); \
-            else if (P.p_norm == 1)                                                                  \
+            if (P.p_norm == 1)                                                                       \
                 hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 1, NT_>), grid, block, 0, st, P, sink, *csr); \
-            else if (base_)                                                                          \
-                hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 2, NT_, true>), grid, block, 0, st, P, sink, *csr); \
             else                                                                                     \
                 hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 2, NT_>), grid, block, 0, st, P, sink, *csr); \
             return hipGetLastError();                                                                \

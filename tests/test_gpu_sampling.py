@@ -148,43 +148,3 @@ def test_split_sampler_any_part_count(parts, monkeypatch):
         _check_batches(ctx.sample(bs, neg, bern, filt, calls, PATHS["part"]), want, E, bs, neg)
     finally:
         ctx.close()
-
-
-@pytest.mark.parametrize("p_norm,opt", [(1, "sgd"), (2, "sgd"), (2, "adagrad")])
-def test_base_row_form_matches_contribution_rows(p_norm, opt, monkeypatch):
-    """The opt-in base-row form of the large-neg TransE step (PT_STEP_BASE=1: k_step_csr<BASE> stores per-
-    positive normalized rows and per-slot scales, k_apply_base re-forms every slot's gradient row) against
-    the default contribution-row form and the oracle, 30 steps. The re-formed rows are the step's own
-    (same operations), so losses agree to 1e-6 relative and tables to 1e-5 absolute."""
-    from openke.config import Trainer
-    from openke.data import TrainDataLoader
-    from openke.module.loss import MarginLoss
-    from openke.module.model import TransE
-    from openke.module.strategy import NegativeSampling
-    bs, neg, dim, steps, lr, margin, seed = 64, 6, 20, 30, 0.05 if opt == "sgd" else 0.02, 3.0, 21
-    runs = {}
-    for base in ("1", "0"):
-        monkeypatch.setenv("PT_STEP_BASE", base)
-        dl = TrainDataLoader(in_path=KG_SMALL, batch_size=bs, threads=THREADS, sampling_mode="normal", bern_flag=1,
-                             filter_flag=1, neg_ent=neg, neg_rel=0, random_seed=seed)
-        dl.nbatches = steps
-        torch.manual_seed(5)
-        kge = TransE(dl.get_ent_tot(), dl.get_rel_tot(), dim=dim, p_norm=p_norm, norm_flag=True)
-        e0 = kge.ent_embeddings.weight.detach().numpy().copy()
-        r0 = kge.rel_embeddings.weight.detach().numpy().copy()
-        ns = NegativeSampling(model=kge, loss=MarginLoss(margin=margin), batch_size=bs)
-        tr = Trainer(model=ns, data_loader=dl, train_times=1, alpha=lr, use_gpu=True, opt_method=opt)
-        tr.run()
-        runs[base] = (tr.last_epoch_loss, kge.ent_embeddings.weight.detach().cpu().numpy(),
-                      kge.rel_embeddings.weight.detach().cpu().numpy())
-    np.testing.assert_allclose(runs["1"][0], runs["0"][0], rtol=1e-6)
-    for i in (1, 2):
-        np.testing.assert_allclose(runs["1"][i], runs["0"][i], atol=1e-5, rtol=0)
-    kg = oracle.KG.load(KG_SMALL)
-    st = oracle.GlibcRand(seed).rand_reset(THREADS)
-    accs = (np.zeros_like(e0), np.zeros_like(r0), None) if opt == "adagrad" else (None, None, None)
-    loss = 0.0
-    for _ in range(steps):
-        h, t, r, _ = kg.sample(st, THREADS, bs, neg, 1, 1)
-        loss += oracle.train_step("TransE", p_norm, True, opt, lr, margin, e0, r0, None, accs, h, t, r, bs, neg)
-    np.testing.assert_allclose(runs["1"][0], loss, rtol=1e-5)
