@@ -415,7 +415,7 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
         }
         PT_APPLYB(2, 1, 4, 1) PT_APPLYB(4, 1, 4, 1) PT_APPLYB(8, 1, 4, 1) PT_APPLYB(16, 1, 4, 1)
         PT_APPLYB(32, 1, 4, 1) PT_APPLYB(64, 1, 4, 1) PT_APPLYB(64, 2, 4, 1) PT_APPLYB(64, 3, 4, 1)
-        PT_APPLYB(64, 4, 4, 1) PT_APPLYB(64, 1, 2, 1) PT_APPLYB(64, 1, 4, 2) PT_APPLYB(64, 1, 2, 2)
+        PT_APPLYB(64, 4, 4, 1) PT_APPLYB(64, 1, 2, 1) PT_APPLYB(64, 1, 4, 2) PT_APPLYB(64, 1, 2, 2) PT_APPLYB(64, 1, 8, 1)
         PT_APPLYB(64, 1, 2, 4) PT_APPLYB(64, 1, 1, 4)
 #undef PT_APPLYB
     }
