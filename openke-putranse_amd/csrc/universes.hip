@@ -130,6 +130,17 @@ __device__ __forceinline__ float transe_step(const StepParams &P, int64_t hp, in
     vload(hh, P.ent + hp * D, D, lane);
     vload(th, P.ent + tp * D, D, lane);
     vload(rh, P.rel + rp * D, D, lane);
+    // long wide rows (16 floats per lane over >= 16 lanes, D > 128): the first negative's row loads
+    // with the positive's, the rest one at a time in the loop (measured: C4, D = 200, 129 -> 108 ms; for
+    // the short rows of C3 the extra live row costs more than the round trip it hides, 66 -> 74 ms)
+    constexpr bool kPrefetch = VEC * KCH >= 16 && G >= 16;
+    int64_t e = 0;
+    bool tail_side = false;
+    Vec x;
+    if (kPrefetch && neg > 0) {
+        get_neg(0, e, tail_side);
+        vload(x, P.ent + e * D, D, lane);
+    }
     if (nf) {
         vnormalize(hh, hh);
         vnormalize(rh, rh);
@@ -143,11 +154,10 @@ __device__ __forceinline__ float transe_step(const StepParams &P, int64_t hp, in
     float csum = 0.f, lsum = 0.f;
     const float m = P.margin, inv = P.inv_count;
     for (int64_t k = 0; k < neg; ++k) {
-        int64_t e;
-        bool tail_side;
-        get_neg(k, e, tail_side);
-        Vec x;
-        vload(x, P.ent + e * D, D, lane);
+        if (!kPrefetch || k > 0) {
+            get_neg(k, e, tail_side);
+            vload(x, P.ent + e * D, D, lane);
+        }
         if (nf) vnormalize(x, x);
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) x.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - x.x[i] : (x.x[i] + rh.x[i]) - th.x[i];
@@ -201,6 +211,13 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
     vload(T, P.ent + tp * D, D, lane);
     vload(rh, P.rel + rp * D, D, lane);
     vload(nW, P.normv + rp * D, D, lane);
+    int64_t e = 0;   // the first negative's row loads with the positive's
+    bool tail_side = false;
+    Vec X;
+    if (neg > 0) {
+        get_neg(0, e, tail_side);
+        vload(X, P.ent + e * D, D, lane);
+    }
     vnormalize(nW, nW);
     const float hdot = vdot(H, nW), tdot = vdot(T, nW);
 #pragma unroll
@@ -222,11 +239,11 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
     float csum = 0.f, lsum = 0.f;
     const float m = P.margin, inv = P.inv_count;
     for (int64_t k = 0; k < neg; ++k) {
-        int64_t e;
-        bool tail_side;
-        get_neg(k, e, tail_side);
-        Vec X, xs, xh, vk;
-        vload(X, P.ent + e * D, D, lane);
+        if (k > 0) {
+            get_neg(k, e, tail_side);
+            vload(X, P.ent + e * D, D, lane);
+        }
+        Vec xs, xh, vk;
         const float ed = vdot(X, nW);
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) xs.x[i] = X.x[i] - ed * nW.x[i];
@@ -476,7 +493,8 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // ---- phase B: row updates of the touched rows, RB rows per lane group at a time (all their
             // loads in flight together: the pass is a chain of dependent memory round trips otherwise)
             const int n = s_count;
-            constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? 2 : 4);
+            // (TransH: 2 rows of 8 floats per lane in flight spill its step's registers; TransE keeps 2)
+            constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? (MODEL == 1 ? 1 : 2) : 4);
             // (guards, not breaks, inside the unrolled loops: the row arrays must stay in registers)
             for (int i0 = grp * RB; i0 < n; i0 += GPB * RB) {
                 Vec x[RB], gs[RB], a[RB], y[RB];

@@ -6,7 +6,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "release", "libputranse_hip.so")
+# PT_LIB_PATH: an alternative build of the same library (A/B measurements of two builds on one box)
+LIB_PATH = os.environ.get("PT_LIB_PATH") or os.path.join(_HERE, "release", "libputranse_hip.so")
 _LIB = None
 
 c_i64 = ctypes.c_int64
