@@ -44,13 +44,21 @@ def algorithmic_bytes_per_slot(model, opt, dim):
 
 
 def dist_setup():
+    """One process per GPU over RCCL (backend "nccl"). PT_BENCH_BACKEND=gloo runs the same multi-rank logic
+    over gloo with ranks sharing the visible GPUs (rank -> GPU local_rank % device_count): a rehearsal of the
+    N > 1 path on a one-GPU box, not a measurement."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if ws > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
+        dev = local % torch.cuda.device_count()
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return ws, rank, local
@@ -60,6 +68,17 @@ def barrier(ws):
     if ws > 1:
         import torch.distributed as dist
         dist.barrier()
+
+
+def all_reduce(t, op):
+    """In-place all_reduce of a device tensor (through host memory when the backend is gloo)."""
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(t, op=op)
+    else:
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
 
 
 def cpu_baseline(path, wl, seconds=15.0):
@@ -202,8 +221,8 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
     if ws > 1:
         import torch.distributed as dist
         mx = tot[:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        all_reduce(mx, dist.ReduceOp.MAX)
+        all_reduce(tot, dist.ReduceOp.SUM)
         el = float(mx.item())
     slots_all, bytes_all = float(tot[1].item()), float(tot[2].item())
     assert torch.isfinite(losses).all(), "non-finite universe loss"
@@ -322,8 +341,8 @@ def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
     t_score = time.perf_counter() - t0
     if ws > 1:
         import torch.distributed as dist
-        dist.all_reduce(rows, op=dist.ReduceOp.MIN)
-        dist.all_reduce(tup, op=dist.ReduceOp.MIN)
+        all_reduce(rows, dist.ReduceOp.MIN)
+        all_reduce(tup, dist.ReduceOp.MIN)
     torch.cuda.synchronize()
     t_comb = time.perf_counter() - t0 - t_score
     ranks = []
@@ -450,7 +469,7 @@ def main():
     if ws > 1:
         import torch.distributed as dist
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        all_reduce(tt, dist.ReduceOp.MAX)
         el = float(tt.item())
     loss_last = float(losses[-1].item())
     assert np.isfinite(loss_last), "non-finite loss"
@@ -520,6 +539,9 @@ def main():
     if ws == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(path, wl, args.cpu_seconds)
     print(json.dumps(rec), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
