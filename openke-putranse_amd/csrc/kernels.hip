@@ -337,6 +337,12 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
     // relative to b0 walked incrementally
     const int32_t neg32 = (int32_t)neg, db = NT / neg32, dk = NT - db * neg32;
     int32_t b = tid / neg32, k = tid - b * neg32;
+    // a part of at most SL * NT slots (the usual case) keeps its slots' entities and LDS ranks in registers
+    // until the bucket bases are known: one store per slot, no reload
+    const bool one = o1 - o0 <= (int64_t)SL * NT;
+    int32_t keep_e[SL], keep_r[SL];
+#pragma unroll
+    for (int i = 0; i < SL; ++i) keep_e[i] = keep_r[i] = 0;
     for (int64_t o = o0 + tid; o < o1; o += SL * NT) {
         // SL slots o + i*NT per iteration, their run searches in lock step; a slot past the end draws nothing
         SlotDraw d[SL];
@@ -352,9 +358,16 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
         slot_searchN<SL>(d);
 #pragma unroll
         for (int i = 0; i < SL; ++i) {
-            if (o + i * NT >= o1) break;
-            nrec[o + i * NT] = (int32_t)((d[i].e << 1) | d[i].side);
-            noff[o + i * NT] = lds_rank<PACK>(cnt, d[i].e);
+            if (o + i * NT < o1) {
+                nrec[o + i * NT] = (int32_t)((d[i].e << 1) | d[i].side);
+                const int32_t r = lds_rank<PACK>(cnt, d[i].e);
+                if (one) {
+                    keep_e[i] = (int32_t)d[i].e;
+                    keep_r[i] = r;
+                } else {
+                    noff[o + i * NT] = r;
+                }
+            }
         }
         b = bi; k = ki;
     }
@@ -380,8 +393,14 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
     }
     __syncthreads();
     PT_PHASE(3);
-    // the slots this thread wrote above (same thread, same addresses): rank inside the call-wide bucket
-    for (int64_t o = o0 + tid; o < o1; o += NT) noff[o] += lds_bucket<PACK>(cnt, nrec[o] >> 1);
+    // rank inside the call-wide bucket: from registers, or re-read (same thread, same addresses)
+    if (one) {
+#pragma unroll
+        for (int i = 0; i < SL; ++i)
+            if (o0 + tid + i * NT < o1) noff[o0 + tid + i * NT] = keep_r[i] + lds_bucket<PACK>(cnt, keep_e[i]);
+    } else {
+        for (int64_t o = o0 + tid; o < o1; o += NT) noff[o] += lds_bucket<PACK>(cnt, nrec[o] >> 1);
+    }
     // every wave's count atomics have returned (their values were used): count this part done
     __syncthreads();
     if (tid == 0) is_last = atomicAdd(&w.tick[call], 1) == (int32_t)(parts - 1);
