@@ -237,6 +237,10 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
                   (steps, prof[i, 0] / steps, prof[i, 1] / steps, prof[i, 2] / steps), file=sys.stderr)
         tot_p = prof[:, :3].sum(axis=0) / max(prof[:, 3].sum(), 1)
         print("universe-prof all: cycles/step presample %.0f A %.0f B %.0f" % tuple(tot_p), file=sys.stderr)
+        span = prof[:, :3].sum(axis=1)
+        print("universe-prof longest universe: %.1f Mcycles (%.1f ms at 2.4 GHz), %d steps; run %.1f ms" %
+              (span.max() / 1e6, span.max() / 2.4e6, prof[int(np.argmax(span)), 3], el * 1e3 / args.c3_steps),
+              file=sys.stderr)
     _native.check(L.pt_universe_set_free(uset))
     for i in range(len(own)):
         L.pt_universe_free(handles[i])
