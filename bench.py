@@ -227,20 +227,19 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
     slots_all, bytes_all = float(tot[1].item()), float(tot[2].item())
     assert torch.isfinite(losses).all(), "non-finite universe loss"
     if os.environ.get("PT_UNI_PROF") == "1":
-        prof = np.zeros(4 * max(len(jobs), 1), dtype=np.uint64)
+        prof = np.zeros(8 * max(len(jobs), 1), dtype=np.uint64)
         _native.check(L.pt_universe_set_profile(uset, prof.ctypes.data))
-        prof = prof.reshape(-1, 4).astype(np.float64)
-        order = np.argsort(-prof[:, 3])
-        for i in order[:5]:
+        prof = prof.reshape(-1, 8).astype(np.float64)
+        span = prof[:, :3].sum(axis=1)
+        for i in np.argsort(-span)[:6]:   # the longest universes (cycles of the last run)
             steps = max(prof[i, 3], 1)
-            print("universe-prof steps %d  cycles/step: presample %.0f  A %.0f  B %.0f" %
-                  (steps, prof[i, 0] / steps, prof[i, 1] / steps, prof[i, 2] / steps), file=sys.stderr)
+            print("universe-prof span %.1f Mcyc steps %d bs %d D %d E %d  cycles/step: presample %.0f"
+                  "  A %.0f  B %.0f" % (span[i] / 1e6, steps, prof[i, 4], prof[i, 5], prof[i, 6],
+                                       prof[i, 0] / steps, prof[i, 1] / steps, prof[i, 2] / steps), file=sys.stderr)
         tot_p = prof[:, :3].sum(axis=0) / max(prof[:, 3].sum(), 1)
         print("universe-prof all: cycles/step presample %.0f A %.0f B %.0f" % tuple(tot_p), file=sys.stderr)
-        span = prof[:, :3].sum(axis=1)
-        print("universe-prof longest universe: %.1f Mcycles (%.1f ms at 2.4 GHz), %d steps; run %.1f ms" %
-              (span.max() / 1e6, span.max() / 2.4e6, prof[int(np.argmax(span)), 3], el * 1e3 / args.c3_steps),
-              file=sys.stderr)
+        print("universe-prof longest universe: %.1f Mcycles (%.1f ms at 2.4 GHz); run %.1f ms" %
+              (span.max() / 1e6, span.max() / 2.4e6, el * 1e3 / args.c3_steps), file=sys.stderr)
     _native.check(L.pt_universe_set_free(uset))
     for i in range(len(own)):
         L.pt_universe_free(handles[i])

@@ -177,8 +177,9 @@ int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, int32_t model
  * [sum of epochs] floats, job-order concatenation of Trainer.run's per-epoch loss sums */
 int pt_universe_set_train(pt_universe_set *s, float *d_losses, void *stream);
 int pt_universe_set_free(pt_universe_set *s);
-/* diagnostics of a set created with PT_UNI_PROF=1 in the environment: per universe (in the set's
- * launch order) shader-clock cycles spent in epoch presampling, phase A, phase B, and the step count */
+/* diagnostics of a set created with PT_UNI_PROF=1 in the environment: out[n][8], per universe (in the
+ * set's launch order) shader-clock cycles spent in epoch presampling, phase A, phase B, the step count,
+ * batch size, dim and entity count (last train call; out[.][7] unused) */
 int pt_universe_set_profile(pt_universe_set *s, uint64_t *out);
 /* create + train + free (synchronizes `stream`) */
 int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm, int32_t norm_flag,

@@ -849,7 +849,7 @@ struct pt_universe_set {
     pt::UniverseLaunch cfg;
     std::vector<pt::UniverseDev> host;    // same order; loss pointers patched per train call
     std::vector<int64_t> host_loss_off;
-    uint64_t *prof = nullptr;             // PT_UNI_PROF=1: [n][4] cycle counters (device)
+    uint64_t *prof = nullptr;             // PT_UNI_PROF=1: [n][8] cycle counters + shape (device)
     ~pt_universe_set() {
         for (auto e : events) (void)hipEventDestroy(e);
         for (auto q : streams) (void)hipStreamDestroy(q);
@@ -871,8 +871,8 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     PT_HIP(hipGetDevice(&set->device));
     if (const char *v = getenv("PT_UNI_PROF")) {
         if (atoi(v) && n > 0) {
-            PT_HIP(hipMalloc((void **)&set->prof, 32 * (size_t)n));
-            PT_HIP(hipMemset(set->prof, 0, 32 * (size_t)n));
+            PT_HIP(hipMalloc((void **)&set->prof, 64 * (size_t)n));
+            PT_HIP(hipMemset(set->prof, 0, 64 * (size_t)n));
         }
     }
     int64_t neg = -1;
@@ -1009,7 +1009,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         U.fnorm = U.frel + g.rel_total;
         U.contrib = (float *)(base + slots[i].contrib);
         U.losses = nullptr;
-        U.prof = set->prof ? set->prof + 4 * (int64_t)set->host.size() : nullptr;
+        U.prof = set->prof ? set->prof + 8 * (int64_t)set->host.size() : nullptr;
         U.threads = J.threads; U.bs = J.batch_size; U.nbatches = J.nbatches; U.epochs = J.epochs; U.dim = J.dim;
         U.lr = J.lr; U.margin = J.margin;
         U.shape = pt::universe_shape_id(J.dim, model);
@@ -1107,12 +1107,13 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
     return PT_OK;
 }
 
-// PT_UNI_PROF diagnostics: per universe (set order) cycles in presampling / phase A / phase B and steps
+// PT_UNI_PROF diagnostics: per universe (set order) cycles in presampling / phase A / phase B, steps,
+// batch size, dim and entities
 extern "C" int pt_universe_set_profile(pt_universe_set *set, uint64_t *out) {
     PT_CHECK(set && out, PT_EINVAL, "null argument");
     PT_CHECK(set->prof, PT_ESTATE, "set created without PT_UNI_PROF=1");
     PT_HIP(hipDeviceSynchronize());
-    PT_HIP(hipMemcpy(out, set->prof, 32 * set->host.size(), hipMemcpyDeviceToHost));
+    PT_HIP(hipMemcpy(out, set->prof, 64 * set->host.size(), hipMemcpyDeviceToHost));
     return PT_OK;
 }
 

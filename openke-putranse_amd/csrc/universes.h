@@ -19,7 +19,7 @@ struct UniverseDev {
     int32_t *fent, *frel, *fnorm;                   // touched-row flags, zero between steps
     float *contrib;                                 // [bs*(4+neg)][dim] gradient-row contributions
     float *losses;                                  // [epochs] Trainer.run's per-epoch loss sum (or null)
-    uint64_t *prof;                                 // null, or [4] cycle counters (presample, A, B, steps)
+    uint64_t *prof;                                 // null, or [8]: cycles (presample, A, B), steps, bs, dim, E, 0
     int64_t threads, bs, nbatches, epochs, dim;
     float lr, margin;
     int32_t shape;                                  // universe_shape_id(dim)

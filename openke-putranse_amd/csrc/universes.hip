@@ -594,6 +594,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
         U.prof[1] = t_a;
         U.prof[2] = t_b;
         U.prof[3] = (uint64_t)U.epochs * U.nbatches;
+        U.prof[4] = (uint64_t)bs;
+        U.prof[5] = (uint64_t)D;
+        U.prof[6] = (uint64_t)E;
     }
     if (tid < threads) U.states[tid] = s_states[tid];
 }
