@@ -60,6 +60,14 @@ int pt_sampler_get_seeds(pt_sampler *s, uint64_t *seeds);       /* current state
 /* one sampling() call into DEVICE arrays of length bs*(1+neg); advances the streams */
 int pt_sampler_sample(pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter, int64_t *d_h,
                       int64_t *d_t, int64_t *d_r, float *d_y, void *stream);
+/* sampling() with its mode and relation corruptions (Base.cpp:185-264; replaces the mode / negRelRate
+ * arguments of Base.cpp:266-279 bound at TrainDataLoader.py:33-45 and used by sampling_head /
+ * sampling_tail / cross_sampling, TrainDataLoader.py:198-246): mode 0 normal, -1 head_batch (heads
+ * replaced by corrupt_tail), 1 tail_batch (tails replaced by corrupt_head); neg_rel relation corruptions
+ * per positive (corrupt_rel, p = false). DEVICE arrays of length bs*(1+neg+neg_rel). PT_EINVAL when
+ * neg_rel > 0 and some (h,t) pair holds every relation (the reference divides by zero there). */
+int pt_sampler_sample_ex(pt_sampler *s, int64_t bs, int64_t neg, int64_t neg_rel, int64_t mode, int64_t bern,
+                         int64_t filter, int64_t *d_h, int64_t *d_t, int64_t *d_r, float *d_y, void *stream);
 
 /* ------------------------------------------------------------------ training ---------------- */
 enum { PT_TRANSE = 0, PT_TRANSH = 1 };

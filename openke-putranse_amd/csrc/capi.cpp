@@ -209,18 +209,27 @@ extern "C" int pt_sampler_get_seeds(pt_sampler *s, uint64_t *seeds) {
     PT_HIP(hipMemcpy(seeds, s->d_states, sizeof(uint64_t) * (size_t)s->threads, hipMemcpyDeviceToHost));
     return PT_OK;
 }
-extern "C" int pt_sampler_sample(pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter, int64_t *d_h,
-                                 int64_t *d_t, int64_t *d_r, float *d_y, void *stream) {
+extern "C" int pt_sampler_sample_ex(pt_sampler *s, int64_t bs, int64_t neg, int64_t neg_rel, int64_t mode,
+                                    int64_t bern, int64_t filter, int64_t *d_h, int64_t *d_t, int64_t *d_r, float *d_y,
+                                    void *stream) {
     PT_CHECK(s && s->g && d_h && d_t && d_r, PT_EINVAL, "pt_sampler_sample: null argument");
-    PT_CHECK(bs >= 0 && neg >= 0, PT_EINVAL, "negative batch size");
+    PT_CHECK(bs >= 0 && neg >= 0 && neg_rel >= 0, PT_EINVAL, "negative batch size or negative rate");
+    PT_CHECK(mode >= -1 && mode <= 1, PT_EINVAL, "sampling mode must be 0, -1 (head_batch) or 1 (tail_batch)");
     PT_CHECK(s->g->ent_total > 1, PT_EINVAL, "graph needs at least two entities");
     int rc = s->g->upload();
     if (rc) return rc;
+    PT_CHECK(neg_rel == 0 || !s->g->ht_full, PT_EINVAL,
+             "corrupt_rel: an (h,t) pair is linked by every relation (the reference divides by zero, Corrupt.h:135)");
     hipStream_t st = (hipStream_t)stream;
-    PT_HIP(pt::launch_sample(s->g->dev, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, d_h, d_t, d_r, d_y,
-                             st));
-    PT_HIP(pt::launch_advance(s->d_states, s->threads, bs, 1 + 2 * neg, st));
+    PT_HIP(pt::launch_sample(s->g->dev, s->d_states, s->threads, bs, neg, neg_rel, (int)mode, (int)bern, (int)filter,
+                             d_h, d_t, d_r, d_y, st));
+    PT_HIP(pt::launch_advance(s->d_states, s->threads, bs, 1 + (mode == 0 ? 2 : 1) * neg + neg_rel, st));
     return PT_OK;
+}
+
+extern "C" int pt_sampler_sample(pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter, int64_t *d_h,
+                                 int64_t *d_t, int64_t *d_r, float *d_y, void *stream) {
+    return pt_sampler_sample_ex(s, bs, neg, 0, 0, bern, filter, d_h, d_t, d_r, d_y, stream);
 }
 
 // ======================================================================== training ===============
@@ -1386,7 +1395,6 @@ extern "C" int64_t getTripleTotal(void) { return L().triple_total; }
 
 extern "C" void sampling(int64_t *bh, int64_t *bt, int64_t *br, float *by, int64_t bs, int64_t neg, int64_t neg_rel,
                          int64_t mode, int64_t filter, int64_t p, int64_t val_loss) {
-    (void)p;
     Legacy &l = L();
     std::lock_guard<std::mutex> lk(l.mu);
     if (val_loss) {   // positives of the validation list (Base.cpp:255-262)
@@ -1395,8 +1403,8 @@ extern "C" void sampling(int64_t *bh, int64_t *bt, int64_t *br, float *by, int64
         }
         return;
     }
-    if (neg_rel != 0 || mode != 0) {
-        legacy_err(pt::fail(PT_ENOTSUP, "sampling: only mode 0 with neg_rel 0 runs on the GPU path"));
+    if (neg_rel > 0 && p) {   // corrupt_rel's p branch reads a relation-probability table never loaded
+        legacy_err(pt::fail(PT_ENOTSUP, "sampling: p = 1 (probability-weighted corrupt_rel) is not supported"));
         return;
     }
     if (!l.active()) {
@@ -1405,7 +1413,7 @@ extern "C" void sampling(int64_t *bh, int64_t *bt, int64_t *br, float *by, int64
     }
     int rc = legacy_sync_sampler(l);
     if (rc) return legacy_err(rc);
-    const int64_t seq = bs * (1 + neg);
+    const int64_t seq = bs * (1 + neg + neg_rel);
     const size_t need = (size_t)seq * 3 * sizeof(int64_t) + (size_t)seq * sizeof(float);
     if (need > l.dbuf_cap) {
         if (l.dbuf) (void)hipFree(l.dbuf);
@@ -1415,7 +1423,7 @@ extern "C" void sampling(int64_t *bh, int64_t *bt, int64_t *br, float *by, int64
     }
     int64_t *dh = l.dbuf, *dt = dh + seq, *dr = dt + seq;
     float *dy = (float *)(dr + seq);
-    rc = pt_sampler_sample(&l.sampler, bs, neg, l.bern, filter, dh, dt, dr, dy, nullptr);
+    rc = pt_sampler_sample_ex(&l.sampler, bs, neg, neg_rel, mode, l.bern, filter, dh, dt, dr, dy, nullptr);
     if (rc) return legacy_err(rc);
     (void)hipMemcpy(bh, dh, sizeof(int64_t) * seq, hipMemcpyDeviceToHost);
     (void)hipMemcpy(bt, dt, sizeof(int64_t) * seq, hipMemcpyDeviceToHost);

@@ -305,6 +305,7 @@ struct PosDraw {
     int64_t h, r, t;
     int32_t hr_lo, hr_hi, tr_lo, tr_hi;
     uint64_t s1;   // stream state after the positive's index draw
+    int64_t idx;   // trainList index of the positive
 };
 
 // positive b: i = rand_max(trainTotal), trainList[i] (Base.cpp:210-215)
@@ -314,7 +315,7 @@ __device__ __forceinline__ PosDraw draw_positive(const DeviceGraph &g, const uin
     const int64_t i = rand_max(s, g.train_total);
     const int4 *p = reinterpret_cast<const int4 *>(g.rec + i);
     const int4 a = p[0], c = p[1];
-    return PosDraw{a.x, a.y, a.z, a.w, c.x, c.y, c.z, s};
+    return PosDraw{a.x, a.y, a.z, a.w, c.x, c.y, c.z, s, i};
 }
 
 // negative k of a positive (stream offsets 1+2k coin, 2+2k corruption; Base.cpp:217-232): returns the

@@ -188,13 +188,32 @@ int Graph::upload() {
     }
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
     const size_t off_rec = 0, off_ht = off_rec + al(sizeof(TripleRec) * n), off_th = off_ht + al(4 * n),
-                 off_bp = off_th + al(4 * n), total = off_bp + al(4 * (R ? R : 1));
+                 off_bp = off_th + al(4 * n), off_rr = off_bp + al(4 * (R ? R : 1)), off_hr = off_rr + al(4 * n),
+                 total = off_hr + al(8 * n);
     std::vector<char> host(total, 0);
     memcpy(host.data() + off_rec, rec.data(), sizeof(TripleRec) * n);
     int32_t *ht = (int32_t *)(host.data() + off_ht), *th = (int32_t *)(host.data() + off_th);
     for (int64_t i = 0; i < n; ++i) {
         ht[i] = (int32_t)head[i].t;
         th[i] = (int32_t)tail[i].h;
+    }
+    // corrupt_rel (Corrupt.h:108-189): the relations of the cmp_rel list and, per triple in head order,
+    // the (h,t) run [ll, rr] its two binary searches find
+    int32_t *rr_col = (int32_t *)(host.data() + off_rr), *hr_run = (int32_t *)(host.data() + off_hr);
+    std::vector<int64_t> rorder((size_t)n);
+    for (int64_t i = 0; i < n; ++i) rorder[i] = i;
+    std::sort(rorder.begin(), rorder.end(), [&](int64_t a, int64_t b) { return cmp_rel(list[a], list[b]); });
+    ht_full = false;
+    for (int64_t i = 0; i < n;) {
+        int64_t j = i;
+        while (j + 1 < n && rel[j + 1].h == rel[i].h && rel[j + 1].t == rel[i].t) ++j;
+        for (int64_t k = i; k <= j; ++k) {
+            rr_col[k] = (int32_t)rel[k].r;
+            hr_run[2 * rorder[k]] = (int32_t)i;
+            hr_run[2 * rorder[k] + 1] = (int32_t)j;
+        }
+        if (j - i + 1 >= R) ht_full = true;
+        i = j + 1;
     }
     float *bp = (float *)(host.data() + off_bp);
     for (int64_t r = 0; r < R; ++r) bp[r] = 1000 * right_mean[r] / (right_mean[r] + left_mean[r]);
@@ -208,6 +227,8 @@ int Graph::upload() {
     dev.head_t = (const int32_t *)(b + off_ht);
     dev.tail_h = (const int32_t *)(b + off_th);
     dev.bern_prob = (const float *)(b + off_bp);
+    dev.rel_r = (const int32_t *)(b + off_rr);
+    dev.ht_run = (const int2 *)(b + off_hr);
     device = cur;
     return PT_OK;
 }

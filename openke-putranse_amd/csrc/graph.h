@@ -27,6 +27,8 @@ struct DeviceGraph {
     const int32_t *head_t = nullptr;    // trainHead[k].t: values corrupt_head searches
     const int32_t *tail_h = nullptr;    // trainTail[k].h: values corrupt_tail searches
     const float *bern_prob = nullptr;   // per relation: 1000*right_mean/(right_mean+left_mean) (Base.cpp:219-221)
+    const int32_t *rel_r = nullptr;     // trainRel[k].r (cmp_rel order): values corrupt_rel searches
+    const int2 *ht_run = nullptr;       // per triple (head order): its (h,t) run [ll, rr] in the cmp_rel list
 };
 
 struct Graph {
@@ -37,6 +39,7 @@ struct Graph {
     std::vector<float> left_mean, right_mean;
 
     // device copy (lazily uploaded to the current device)
+    bool ht_full = false;                 // some (h,t) pair holds every relation: corrupt_rel would divide by 0
     int device = -1;
     void *dev_block = nullptr;
     DeviceGraph dev;

@@ -98,7 +98,8 @@ inline Shape pick_shape(int64_t D, bool vec4 = true) {
 
 bool shape_supported(int64_t dim);
 hipError_t launch_sample(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
-                         int bern, int filter, int64_t *h, int64_t *t, int64_t *r, float *y, hipStream_t st);
+                         int64_t neg_rel, int mode, int bern, int filter, int64_t *h, int64_t *t, int64_t *r, float *y,
+                         hipStream_t st);
 hipError_t launch_spin(int64_t us, hipStream_t st);
 hipError_t launch_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t dpp, hipStream_t st);
 hipError_t launch_sample_csr(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,

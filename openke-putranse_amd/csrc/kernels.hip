@@ -28,24 +28,49 @@ namespace dev {
 using pt::CsrWork;
 
 
-// sampling() into arrays (one thread per positive); the stream advance is a separate kernel
+// sampling() into arrays (one thread per positive, Base.cpp:185-264); the stream advance is a separate
+// kernel. mode 0: a coin per negative picks the replaced side (draw_negative); mode -1 (sampling_head)
+// replaces the head via corrupt_tail, mode 1 (sampling_tail) the tail via corrupt_head - no coin, and
+// corrupt_*'s default filter_flag = true (Base.cpp:233-245). Then neg_rel relation corruptions
+// (corrupt_rel, p = false, filter_flag = true: Corrupt.h:108-135, :179-189) drawn among the relations
+// not yet linking (h, t) - the same run search as the entity corruptions, over the cmp_rel list.
 __global__ void k_sample(DeviceGraph g, const uint64_t *__restrict__ states, int64_t threads, int64_t bs, int64_t neg,
-                         int bern, int filter, int64_t *__restrict__ oh, int64_t *__restrict__ ot,
-                         int64_t *__restrict__ orr, float *__restrict__ oy) {
+                         int64_t neg_rel, int mode, int bern, int filter, int64_t *__restrict__ oh,
+                         int64_t *__restrict__ ot, int64_t *__restrict__ orr, float *__restrict__ oy) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= bs) return;
-    const PosDraw pd = draw_positive(g, states, threads, bs, b, 1 + 2 * neg);
+    const int64_t per_neg = mode == 0 ? 2 : 1;
+    const PosDraw pd = draw_positive(g, states, threads, bs, b, 1 + per_neg * neg + neg_rel);
     const int64_t hp = pd.h, rp = pd.r, tp = pd.t;
     oh[b] = hp; ot[b] = tp; orr[b] = rp;
     if (oy) oy[b] = 1.f;
     for (int64_t k = 0; k < neg; ++k) {
-        int tail_side;
-        const int64_t e = draw_negative(g, pd, k, bern, filter, &tail_side);
+        int64_t hh = hp, tt = tp;
+        if (mode == 0) {
+            int tail_side;
+            const int64_t e = draw_negative(g, pd, k, bern, filter, &tail_side);
+            if (tail_side) tt = e; else hh = e;
+        } else {
+            uint64_t s = lcg_jump(pd.s1, (uint64_t)k);
+            if (mode < 0) hh = corrupt_in_run(g.tail_h, pd.tr_lo, pd.tr_hi, g.ent_total, s);
+            else tt = corrupt_in_run(g.head_t, pd.hr_lo, pd.hr_hi, g.ent_total, s);
+        }
         const int64_t o = (k + 1) * bs + b;
-        oh[o] = tail_side ? hp : e;
-        ot[o] = tail_side ? e : tp;
+        oh[o] = hh;
+        ot[o] = tt;
         orr[o] = rp;
         if (oy) oy[o] = -1.f;
+    }
+    if (neg_rel > 0) {
+        const int2 run = g.ht_run[pd.idx];
+        for (int64_t k = 0; k < neg_rel; ++k) {
+            uint64_t s = lcg_jump(pd.s1, (uint64_t)(per_neg * neg + k));
+            const int64_t o = (neg + k + 1) * bs + b;
+            oh[o] = hp;
+            ot[o] = tp;
+            orr[o] = corrupt_in_run(g.rel_r, run.x, run.y, g.rel_total, s);
+            if (oy) oy[o] = -1.f;
+        }
     }
 }
 
@@ -773,11 +798,12 @@ bool shape_supported(int64_t dim) {
 }
 
 hipError_t launch_sample(const DeviceGraph &g, const uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
-                         int bern, int filter, int64_t *h, int64_t *t, int64_t *r, float *y, hipStream_t st) {
+                         int64_t neg_rel, int mode, int bern, int filter, int64_t *h, int64_t *t, int64_t *r, float *y,
+                         hipStream_t st) {
     if (bs <= 0) return hipSuccess;
     const int bl = 256;
     hipLaunchKernelGGL(dev::k_sample, dim3((unsigned)((bs + bl - 1) / bl)), dim3(bl), 0, st, g, states, threads, bs,
-                       neg, bern, filter, h, t, r, y);
+                       neg, neg_rel, mode, bern, filter, h, t, r, y);
     return hipGetLastError();
 }
 

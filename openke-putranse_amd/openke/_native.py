@@ -66,6 +66,8 @@ SIGNATURES = {
     "pt_sampler_set_seeds": (ctypes.c_int, [c_vp, c_vp]),
     "pt_sampler_get_seeds": (ctypes.c_int, [c_vp, c_vp]),
     "pt_sampler_sample": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "pt_sampler_sample_ex": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                            c_vp]),
     "pt_trainer_create": (ctypes.c_int, [ctypes.POINTER(ModelDesc), ctypes.POINTER(c_vp)]),
     "pt_trainer_free": (ctypes.c_int, [c_vp]),
     "pt_trainer_update_desc": (ctypes.c_int, [c_vp, ctypes.POINTER(ModelDesc)]),

@@ -6,7 +6,8 @@ each epoch is ONE replayed hipGraph of `nbatches` fused steps: every step sample
 kernel from the data loader's stream (bit-identical to TrainDataLoader.sampling()), computes
 NegativeSampling + MarginLoss forward and the analytic backward, and applies SGD or Adagrad to the
 touched rows only (identical to the reference's dense update). Losses stay on the device until the
-end of the epoch (one host sync per epoch instead of one per step)."""
+end of the epoch (one host sync per epoch instead of one per step). Cross sampling and relation
+corruption (neg_rel > 0) train batch by batch: GPU-sampled batch, then the external-batch step."""
 import ctypes
 import os
 
@@ -114,8 +115,21 @@ class Trainer(object):
         h = torch.as_tensor(np.asarray(data['batch_h']), dtype=torch.int64).to(dev).contiguous()
         t = torch.as_tensor(np.asarray(data['batch_t']), dtype=torch.int64).to(dev).contiguous()
         r = torch.as_tensor(np.asarray(data['batch_r']), dtype=torch.int64).to(dev).contiguous()
-        if data.get('mode', 'normal') != 'normal':
-            raise NotImplementedError("cross-sampled batches are outside the accelerated path")
+        mode = data.get('mode', 'normal')
+        if mode != 'normal':
+            # head_batch / tail_batch (TransE.py:51-58, TransH.py:66-73): the uncorrupted side and the
+            # relation are given once per positive and broadcast over the negatives - the same slots as
+            # the expanded normal-mode batch (the score adds h + (r - t) instead of (h + r) - t there:
+            # fp32 association only)
+            if mode not in ('head_batch', 'tail_batch'):
+                raise ValueError("unknown batch mode %r" % (mode,))
+            full = h if mode == 'head_batch' else t
+            rep = full.numel() // max(bs, 1)
+            if mode == 'head_batch':
+                t = t[:bs].repeat(rep)
+            else:
+                h = h[:bs].repeat(rep)
+            r = r[:bs].repeat(rep)
         n = h.numel()
         if n % bs != 0 or n // bs < 2:
             raise ValueError("batch of %d triples does not match batch_size %d with negatives" % (n, bs))
@@ -125,6 +139,26 @@ class Trainer(object):
                                                     _native.ptr(t), _native.ptr(r), _native.ptr(out),
                                                     _native.stream()))
         return out.item()
+
+    def _run_batches(self, L, sampler, bern, bs, nb, losses, buf):
+        """One epoch of device-sampled batches outside the fused form - cross sampling (the loader's
+        __iter__ alternates tail_batch / head_batch, TrainDataLoader.py:240-246, 320-324) or relation
+        corruption (neg_rel > 0): every batch is drawn by the GPU sampler into device arrays (k_sample,
+        bit-identical to the loader's sampling call) and trained by the external-batch step."""
+        dl = self.data_loader
+        neg, neg_rel = dl.negative_ent, dl.negative_rel
+        h, t, r, y = buf
+        st = _native.stream()
+        for i in range(nb):
+            if dl.sampling_mode == "normal":
+                mode = 0
+            else:
+                dl.cross_sampling_flag = 1 - dl.cross_sampling_flag
+                mode = -1 if dl.cross_sampling_flag == 0 else 1
+            _native.check(L.pt_sampler_sample_ex(sampler, bs, neg, neg_rel, mode, bern, dl.filter, _native.ptr(h),
+                                                 _native.ptr(t), _native.ptr(r), _native.ptr(y), st))
+            _native.check(L.pt_trainer_step(self._native, None, bs, neg + neg_rel, 0, 0, _native.ptr(h),
+                                            _native.ptr(t), _native.ptr(r), _native.ptr(losses[i:i + 1]), st))
 
     def run(self):
         ns, kge, loss = self._setup()
@@ -137,12 +171,21 @@ class Trainer(object):
         bern = L.pt_legacy_bern()
         dev = kge.ent_embeddings.weight.device
         losses = torch.zeros(max(nb, 1), dtype=torch.float32, device=dev)
+        fused = dl.sampling_mode == "normal" and dl.negative_rel == 0
+        buf = None
+        if not fused:
+            seq = bs * (1 + neg + dl.negative_rel)
+            buf = tuple(torch.zeros(seq, dtype=torch.int64, device=dev) for _ in range(3)) + \
+                (torch.zeros(seq, dtype=torch.float32, device=dev),)
         print("Finish initializing...")
         training_range = tqdm(range(self.train_times))
         for epoch in training_range:
-            if nb > 0:
+            if nb > 0 and fused:
                 _native.check(L.pt_trainer_run(self._native, sampler, bs, neg, bern, dl.filter, nb,
                                                _native.ptr(losses), _native.stream()))
+            elif nb > 0:
+                losses.zero_()
+                self._run_batches(L, sampler, bern, bs, nb, losses, buf)
             host = losses.cpu().numpy()
             res = float(host[:nb].sum())
             loss_v = float(host[nb - 1]) if nb > 0 else 0.0

@@ -39,8 +39,6 @@ class TrainDataLoader(object):
         self.lib = _native.lib()
         if incremental_setting:
             raise NotImplementedError("incremental_setting is outside the accelerated path")
-        if neg_rel != 0:
-            raise NotImplementedError("neg_rel > 0 (relation corruption) is outside the accelerated path")
         self.in_path = in_path
         self.work_threads = threads
         self.nbatches = nbatches
@@ -114,13 +112,35 @@ class TrainDataLoader(object):
         }
 
     def sampling_head(self):
-        raise NotImplementedError("cross sampling (head_batch) is outside the accelerated path")
+        """head_batch: every negative replaces the head (corrupt_tail), TrainDataLoader.py:198-217."""
+        self.lib.sampling(self.batch_h_addr, self.batch_t_addr, self.batch_r_addr, self.batch_y_addr,
+                          self.batch_size, self.negative_ent, self.negative_rel, -1, self.filter, 0, 0)
+        return {
+            "batch_h": self.batch_h,
+            "batch_t": self.batch_t[:self.batch_size],
+            "batch_r": self.batch_r[:self.batch_size],
+            "batch_y": self.batch_y,
+            "mode": "head_batch"
+        }
 
     def sampling_tail(self):
-        raise NotImplementedError("cross sampling (tail_batch) is outside the accelerated path")
+        """tail_batch: every negative replaces the tail (corrupt_head), TrainDataLoader.py:219-238."""
+        self.lib.sampling(self.batch_h_addr, self.batch_t_addr, self.batch_r_addr, self.batch_y_addr,
+                          self.batch_size, self.negative_ent, self.negative_rel, 1, self.filter, 0, 0)
+        return {
+            "batch_h": self.batch_h[:self.batch_size],
+            "batch_t": self.batch_t,
+            "batch_r": self.batch_r[:self.batch_size],
+            "batch_y": self.batch_y,
+            "mode": "tail_batch"
+        }
 
     def cross_sampling(self):
-        raise NotImplementedError("cross sampling is outside the accelerated path")
+        """Alternates tail_batch / head_batch (TrainDataLoader.py:240-246)."""
+        self.cross_sampling_flag = 1 - self.cross_sampling_flag
+        if self.cross_sampling_flag == 0:
+            return self.sampling_head()
+        return self.sampling_tail()
 
     def device_sampler(self):
         """Handle of the GPU sampler that produces exactly the batches sampling() would return next."""
@@ -151,8 +171,6 @@ class TrainDataLoader(object):
         self.negative_ent = rate
 
     def set_rel_neg_rate(self, rate):
-        if rate != 0:
-            raise NotImplementedError("neg_rel > 0 is outside the accelerated path")
         self.negative_rel = rate
 
     def set_bern_flag(self, bern):

@@ -311,6 +311,86 @@ void oracle_sampling(const okg *g, uint64_t *states, int64_t threads, int64_t bs
     oracle_sampling_sides(g, states, threads, bs, neg, bern, filter, h, t, r, y, NULL);
 }
 
+/* corrupt_rel, p == false, filter_flag == true (Corrupt.h:108-135, :179-189): the (h,t) run [ll,rr] of the
+ * cmp_rel-sorted list holds the relations already known between h and t; draw among the others.
+ * Returns -1 where the reference divides by zero (every relation is known for (h,t)). */
+static int64_t corrupt_rel_filtered(const okg *g, int64_t h, int64_t t, uint64_t *s) {
+    const otriple *L = g->train_rel;
+    int64_t lo = g->lef_rel[h] - 1, hi = g->rig_rel[h], mid;
+    while (lo + 1 < hi) {
+        mid = (lo + hi) >> 1;
+        if (L[mid].t >= t) hi = mid; else lo = mid;
+    }
+    const int64_t ll = hi;
+    lo = g->lef_rel[h];
+    hi = g->rig_rel[h] + 1;
+    while (lo + 1 < hi) {
+        mid = (lo + hi) >> 1;
+        if (L[mid].t <= t) lo = mid; else hi = mid;
+    }
+    const int64_t rr = lo;
+    if (g->rel_total - (rr - ll + 1) <= 0) return -1;
+    const int64_t tmp = lcg_max(s, g->rel_total - (rr - ll + 1));
+    if (tmp < L[ll].r) return tmp;
+    if (tmp > L[rr].r - rr + ll - 1) return tmp + rr - ll + 1;
+    lo = ll;
+    hi = rr + 1;
+    while (lo + 1 < hi) {
+        mid = (lo + hi) >> 1;
+        if (L[mid].r - mid + ll - 1 < tmp) lo = mid; else hi = mid;
+    }
+    return tmp + lo - ll + 1;
+}
+
+/* getBatch with every argument of sampling() (Base.cpp:185-264), val_loss aside: mode 0 is the coin form
+ * above; mode -1 (sampling_head) replaces the head by corrupt_tail, mode 1 (sampling_tail) the tail by
+ * corrupt_head - both with corrupt_*'s default filter_flag = true (Base.cpp:233-245, Corrupt.h:9, :59) and
+ * no coin draw; then neg_rel relation corruptions per positive (Base.cpp:247-253, p = false). */
+void oracle_sampling_ex(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t neg_rel,
+                        int64_t mode, int64_t bern, int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y) {
+    for (int64_t id = 0; id < threads; ++id) {
+        int64_t lef, rig;
+        if (bs % threads == 0) {
+            lef = id * (bs / threads);
+            rig = (id + 1) * (bs / threads);
+        } else {
+            lef = id * (bs / threads + 1);
+            rig = (id + 1) * (bs / threads + 1);
+            if (rig > bs) rig = bs;
+        }
+        uint64_t *s = &states[id];
+        float prob = 500;
+        for (int64_t b = lef; b < rig; ++b) {
+            int64_t i = lcg_max(s, g->train_total);
+            otriple p = g->train_list[i];
+            h[b] = p.h; t[b] = p.t; r[b] = p.r; y[b] = 1;
+            int64_t last = bs;
+            for (int64_t k = 0; k < neg; ++k) {
+                h[b + last] = p.h; t[b + last] = p.t; r[b + last] = p.r;
+                if (mode == 0) {
+                    if (bern) prob = 1000 * g->right_mean[p.r] / (g->right_mean[p.r] + g->left_mean[p.r]);
+                    if ((float)(lcg_next(s) % 1000) < prob)
+                        t[b + last] = filter ? corrupt_filtered(g, 1, p.h, p.r, s) : corrupt_plain(g, p.h, s);
+                    else
+                        h[b + last] = filter ? corrupt_filtered(g, 0, p.t, p.r, s) : corrupt_plain(g, p.t, s);
+                } else if (mode == -1) {
+                    h[b + last] = corrupt_filtered(g, 0, p.t, p.r, s);
+                } else {
+                    t[b + last] = corrupt_filtered(g, 1, p.h, p.r, s);
+                }
+                y[b + last] = -1;
+                last += bs;
+            }
+            for (int64_t k = 0; k < neg_rel; ++k) {
+                h[b + last] = p.h; t[b + last] = p.t;
+                r[b + last] = corrupt_rel_filtered(g, p.h, p.t, s);
+                y[b + last] = -1;
+                last += bs;
+            }
+        }
+    }
+}
+
 /* ---------------------------------------------------------------- universe construction ------- */
 typedef struct { int64_t *a; int64_t n, cap; } iset;   /* sorted set, std::set<INT> iteration order */
 static void iset_init(iset *s) { s->n = 0; s->cap = 16; s->a = malloc(sizeof(int64_t) * 16); }

@@ -48,6 +48,10 @@ void oracle_sampling(const okg *g, uint64_t *states, int64_t threads, int64_t bs
                      int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y);
 void oracle_sampling_sides(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
                            int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y, int8_t *side);
+/* sampling with mode (0 / -1 sampling_head / 1 sampling_tail) and neg_rel relation corruptions
+ * (Base.cpp:185-264, Corrupt.h:108-189); seq = bs * (1 + neg + neg_rel) */
+void oracle_sampling_ex(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t neg_rel,
+                        int64_t mode, int64_t bern, int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y);
 
 /* getParallelUniverse (UniverseConstructor.h:327-397): returns the universe graph (local ids, helpers
  * built as loadUniverseHelpers does) and writes local->global maps (sized >= E and >= R). */

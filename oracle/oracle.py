@@ -46,6 +46,7 @@ def lib():
         L.oracle_sampling.argtypes = [ctypes.c_void_p, u64p] + [ctypes.c_int64] * 5 + [i64p, i64p, i64p, f32p]
         L.oracle_sampling_sides.argtypes = [ctypes.c_void_p, u64p] + [ctypes.c_int64] * 5 + \
             [i64p, i64p, i64p, f32p, ctypes.c_void_p]
+        L.oracle_sampling_ex.argtypes = [ctypes.c_void_p, u64p] + [ctypes.c_int64] * 7 + [i64p, i64p, i64p, f32p]
         L.oracle_universe.restype = ctypes.c_void_p
         L.oracle_universe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_float, i64p, i64p]
         L.oracle_train_step.restype = ctypes.c_float
@@ -135,6 +136,16 @@ class KG:
         lib().oracle_sampling_sides(self.h, _p(states, u64p), threads, bs, neg, bern, filt, _p(h, i64p),
                                     _p(t, i64p), _p(r, i64p), _p(y, f32p), side.ctypes.data if sides else None)
         return (h, t, r, y, side) if sides else (h, t, r, y)
+
+    def sample_ex(self, states, threads, bs, neg, neg_rel, mode, bern, filt):
+        """sampling() with its mode (0 normal, -1 sampling_head, 1 sampling_tail) and neg_rel relation
+        corruptions (Base.cpp:185-264); seq = bs * (1 + neg + neg_rel)."""
+        seq = bs * (1 + neg + neg_rel)
+        h, t, r = (np.zeros(seq, dtype=np.int64) for _ in range(3))
+        y = np.zeros(seq, dtype=np.float32)
+        lib().oracle_sampling_ex(self.h, _p(states, u64p), threads, bs, neg, neg_rel, mode, bern, filt,
+                                 _p(h, i64p), _p(t, i64p), _p(r, i64p), _p(y, f32p))
+        return h, t, r, y
 
     def universe(self, rng, tc, balance):
         em = np.full(max(self.ent_total, 1), -1, dtype=np.int64)

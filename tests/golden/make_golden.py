@@ -57,6 +57,16 @@ TRAIN_CASES = [
     ("t7", "TransE", 64, 2, True, "adagrad", 0.1, 1.0, 4, 90, 3, 1, 0, 10, 7, 4),
 ]
 
+SAMPLER_MODE_CASES = [
+    # name, dataset, threads, batch_size, neg_ent, neg_rel, bern, filter, seed, calls
+    # calls: n = sampling(), h = sampling_head(), t = sampling_tail(), c = cross_sampling()
+    ("m1", "small", 8, 123, 3, 0, 1, 0, 13, "hth"),
+    ("m2", "small", 8, 64, 2, 2, 1, 1, 14, "nnh"),
+    ("m3", "tiny", 3, 37, 1, 3, 0, 1, 15, "tccc"),
+    ("m4", "small", 8, 200, 0, 1, 0, 0, 16, "nn"),
+    ("m5", "small", 5, 101, 4, 1, 1, 1, 17, "cnt"),
+]
+
 UNIVERSE_CASES = [
     # name, model, dim, p_norm, n_universes, min_tc, max_tc, const_epochs, seed
     ("u1", "TransE", 8, 1, 6, 200, 400, 2, 123),
@@ -115,6 +125,24 @@ def case_sampler(out, name, ds, threads, bs, neg, bern, filt, seed):
     np.savez_compressed(out, threads=threads, batch_size=bs, neg_ent=neg, bern=bern, filter=filt, seed=seed,
                         dataset=ds, batch_h=np.stack(hs), batch_t=np.stack(ts), batch_r=np.stack(rs),
                         batch_y=np.stack(ys))
+
+
+def case_sampler_mode(out, name, ds, threads, bs, neg, neg_rel, bern, filt, seed, calls):
+    """sampling() with mode -1 / 1 (sampling_head / sampling_tail / cross_sampling, TrainDataLoader.py:198-246)
+    and neg_rel relation corruptions (Base.cpp:233-253); the loader's full buffers are recorded."""
+    from openke.data import TrainDataLoader
+    dl = TrainDataLoader(in_path=DATASETS[ds], batch_size=bs, threads=threads, sampling_mode="cross",
+                         bern_flag=bern, filter_flag=filt, neg_ent=neg, neg_rel=neg_rel, random_seed=seed)
+    fn = {"n": dl.sampling, "h": dl.sampling_head, "t": dl.sampling_tail, "c": dl.cross_sampling}
+    hs, ts, rs, ys, modes = [], [], [], [], []
+    for c in calls:
+        d = fn[c]()
+        modes.append(d["mode"])
+        hs.append(dl.batch_h.copy()); ts.append(dl.batch_t.copy())
+        rs.append(dl.batch_r.copy()); ys.append(dl.batch_y.copy())
+    np.savez_compressed(out, threads=threads, batch_size=bs, neg_ent=neg, neg_rel=neg_rel, bern=bern, filter=filt,
+                        seed=seed, dataset=ds, calls=calls, modes=np.array(modes), batch_h=np.stack(hs),
+                        batch_t=np.stack(ts), batch_r=np.stack(rs), batch_y=np.stack(ys))
 
 
 def case_train(out, name, model, dim, p, norm_flag, opt, lr, margin, threads, bs, neg, bern, filt, seed, tseed,
@@ -275,7 +303,7 @@ def run_case(kind, args_json, out, tmp):
     args = json.loads(args_json)
     _import_reference(tmp)
     _silence()
-    {"glibc": case_glibc, "sampler": case_sampler, "train": case_train, "universes": case_universes,
+    {"glibc": case_glibc, "sampler": case_sampler, "sampler_mode": case_sampler_mode, "train": case_train, "universes": case_universes,
      "lp": case_lp, "tc": case_tc}[kind](out, *args)
 
 
@@ -287,6 +315,7 @@ def main():
     tmp = tempfile.mkdtemp(prefix="refpy_")
     jobs = [("glibc", [], "glibc_rand.npz")]
     jobs += [("sampler", list(c), "sampler_%s.npz" % c[0]) for c in SAMPLER_CASES]
+    jobs += [("sampler_mode", list(c), "samplermode_%s.npz" % c[0]) for c in SAMPLER_MODE_CASES]
     jobs += [("train", list(c), "train_%s.npz" % c[0]) for c in TRAIN_CASES]
     jobs += [("universes", list(c), "universes_%s.npz" % c[0]) for c in UNIVERSE_CASES]
     jobs += [("lp", list(c), "lp_%s.npz" % c[0]) for c in LP_CASES]

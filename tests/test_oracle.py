@@ -30,6 +30,39 @@ def test_sampler_bit_exact(path):
         np.testing.assert_array_equal(y, z["batch_y"][c])
 
 
+MODE_OF_CALL = {"n": 0, "h": -1, "t": 1}
+
+
+def call_modes(calls):
+    """sampling() mode of each loader call; cross_sampling flips its flag first (TrainDataLoader.py:240-246)."""
+    flag, out = 0, []
+    for c in calls:
+        if c == "c":
+            flag = 1 - flag
+            out.append(1 if flag else -1)
+        else:
+            out.append(MODE_OF_CALL[c])
+    return out
+
+
+@pytest.mark.parametrize("path", golden("samplermode_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_sampler_modes_bit_exact(path):
+    """sampling_head / sampling_tail / cross_sampling and neg_rel relation corruption vs the reference."""
+    z = load(path)
+    kg = oracle.KG.load(DATASETS[str(z["dataset"])])
+    threads, bs = int(z["threads"]), int(z["batch_size"])
+    neg, neg_rel = int(z["neg_ent"]), int(z["neg_rel"])
+    st = oracle.GlibcRand(int(z["seed"])).rand_reset(threads)
+    modes = call_modes(str(z["calls"]))
+    assert [{0: "normal", -1: "head_batch", 1: "tail_batch"}[m] for m in modes] == list(z["modes"])
+    for c, mode in enumerate(modes):
+        h, t, r, y = kg.sample_ex(st, threads, bs, neg, neg_rel, mode, int(z["bern"]), int(z["filter"]))
+        np.testing.assert_array_equal(h, z["batch_h"][c])
+        np.testing.assert_array_equal(t, z["batch_t"][c])
+        np.testing.assert_array_equal(r, z["batch_r"][c])
+        np.testing.assert_array_equal(y, z["batch_y"][c])
+
+
 @pytest.mark.parametrize("path", golden("train_*.npz"), ids=lambda p: p.split("/")[-1])
 def test_train_steps_match_reference(path):
     z = load(path)
