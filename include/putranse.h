@@ -224,6 +224,16 @@ int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, int32_t mode
 int pt_rank_rows(const float *d_rows, int64_t ent_total, const int64_t *d_row_of, const int64_t *d_truth,
                  const float *d_repl, const int64_t *d_part_off, const int64_t *d_part, int64_t n, int64_t *d_raw,
                  int64_t *d_filt, void *stream);
+/* Type-constrained raw / filtered counts of the same queries (testHead/testTail with type_constrain,
+ * Test.h:127-130, :168-178, :288-298; replaces that branch of the symbols bound at Tester.py:80-82):
+ * d_rel[q] selects the relation's type list [d_type_lef[r], d_type_rig[r]) of d_types (ascending, as
+ * importTypeFiles sorts it, Reader.h:352-396); d_part must be ascending per query (pt_known_partners
+ * returns it so). The reference's position/entity quirk is kept: type entity j is compared with the
+ * score at candidate position j. */
+int pt_rank_types(const float *d_rows, int64_t ent_total, const int64_t *d_row_of, const int64_t *d_truth,
+                  const float *d_repl, const int64_t *d_rel, const int64_t *d_type_lef, const int64_t *d_type_rig,
+                  const int64_t *d_types, const int64_t *d_part_off, const int64_t *d_part, int64_t n,
+                  int64_t *d_raw, int64_t *d_filt, void *stream);
 
 /* Filtered / raw ranks (testHead/testTail, Test.h:118-359) for many queries at once on host threads:
  * con rows [n][ent_total] in candidate order, anchors per query. Known-triple set from
@@ -247,6 +257,9 @@ int64_t pt_legacy_bern(void);
  * count, fills the arrays when non-NULL. The known-triple set used by the filtered rank. */
 int64_t pt_legacy_eval_triples(int32_t valid, int64_t *h, int64_t *t, int64_t *r);
 const pt_known *pt_legacy_known(void);
+/* the type lists importTypeFiles loaded (side 0 heads, 1 tails): lef/rig per relation (relTotal entries)
+ * and the lists, ascending per relation; returns the list length, -1 before importTypeFiles */
+int64_t pt_legacy_types(int32_t side, int64_t *lef, int64_t *rig, int64_t *list);
 /* the global context's full training graph (importTrainFiles), e.g. for pt_universe_build_many */
 pt_graph *pt_legacy_graph(void);
 
@@ -280,6 +293,7 @@ void swapHelpers(void);                              /* UniverseSetting.h:123-15
 void resetUniverse(void);                            /* UniverseSetting.h:160-190 */
 void activateLoadOfAllTriples(int64_t flag);         /* Reader.h:241-244 */
 void importTestFiles(void);                          /* Reader.h:246-342 */
+void importTypeFiles(void);                          /* Reader.h:344-396 */
 void initTest(void);                                 /* Test.h:23-35 */
 void getHeadBatch(int64_t *ph, int64_t *pt, int64_t *pr);    /* Test.h:37-71 */
 void getTailBatch(int64_t *ph, int64_t *pt, int64_t *pr);    /* Test.h:73-107 */

@@ -1263,6 +1263,19 @@ extern "C" int pt_rank_rows(const float *d_rows, int64_t ent_total, const int64_
     return PT_OK;
 }
 
+extern "C" int pt_rank_types(const float *d_rows, int64_t ent_total, const int64_t *d_row_of, const int64_t *d_truth,
+                             const float *d_repl, const int64_t *d_rel, const int64_t *d_type_lef,
+                             const int64_t *d_type_rig, const int64_t *d_types, const int64_t *d_part_off,
+                             const int64_t *d_part, int64_t n, int64_t *d_raw, int64_t *d_filt, void *stream) {
+    if (n == 0) return PT_OK;
+    PT_CHECK(d_rows && d_row_of && d_truth && d_rel && d_type_lef && d_type_rig && d_types && d_part_off && d_raw &&
+                 d_filt && ent_total > 0,
+             PT_EINVAL, "pt_rank_types: null argument");
+    PT_HIP(pt::launch_rank_types(d_rows, ent_total, d_row_of, d_truth, d_repl, d_rel, d_type_lef, d_type_rig, d_types,
+                                 d_part_off, d_part, n, d_raw, d_filt, (hipStream_t)stream));
+    return PT_OK;
+}
+
 // ======================================================================== Base.so surface ========
 // One process-global context with the reference's semantics (Setting.h / Random.h / Reader.h /
 // UniverseSetting.h / Test.h / Valid.h globals). Sampling, training and scoring run on the GPU.
@@ -1296,9 +1309,13 @@ struct Legacy {
     std::vector<pt::Triple> test, valid;
     pt_known *known = nullptr;
     int64_t last_head = 0, last_tail = 0, last_vhead = 0, last_vtail = 0;
-    TestAcc acc;
+    TestAcc acc, acc_tc;                     // unconstrained / type-constrained accumulators
     float mrr = 0, mr = 0, hit10 = 0, hit3 = 0, hit1 = 0;
+    float mrr_tc = 0, mr_tc = 0, hit10_tc = 0, hit3_tc = 0, hit1_tc = 0;
     float l_valid = 0, r_valid = 0, valid_hit10 = 0;
+    // importTypeFiles (Reader.h:344-396): per relation [lef, rig) into the sorted head / tail type lists
+    bool types_loaded = false;
+    std::vector<int64_t> type_lef[2], type_rig[2], type_list[2];
 
     pt::Graph *active() { return swapped && uni ? &uni->g : train.get(); }
     int64_t E() { pt::Graph *g = active(); return g ? g->ent_total : ent_total; }
@@ -1550,6 +1567,7 @@ extern "C" void importTestFiles(void) {
 namespace pt {
 void rank_one(const pt_known &k, int64_t E, int64_t h, int64_t t, int64_t r, int side, const float *con,
               int64_t *raw, int64_t *filt);
+bool known_has(const pt_known &k, int64_t h, int64_t t, int64_t r);
 }
 
 // ------------------------------------------------------------------ triple classification -------
@@ -1631,6 +1649,7 @@ extern "C" void initTest(void) {
     Legacy &l = L();
     l.last_head = l.last_tail = 0;
     l.acc = TestAcc{};
+    l.acc_tc = TestAcc{};
 }
 
 static void fill_batch(const pt::Triple &q, int64_t E, int side, int64_t *ph, int64_t *pt_, int64_t *pr) {
@@ -1672,47 +1691,137 @@ static void accumulate(TestAcc &a, int side, int64_t raw, int64_t filt) {
     ri = (float)((double)ri + 1.0 / (double)(raw + 1));
 }
 
-extern "C" void testHead(float *con, int64_t idx, int64_t type_constrain) {
+// importTypeFiles (Reader.h:352-396): `type_constrain.txt` in the input folder - a count, then for each of
+// relationTotal relations a line of head types and a line of tail types, `r n e_1 .. e_n`; every list is
+// sorted in place. (The reference's Python never calls it; testHead/testTail with type_constrain read
+// these arrays.)
+extern "C" void importTypeFiles(void) {
     Legacy &l = L();
-    if (type_constrain) legacy_err(pt::fail(PT_ENOTSUP, "type_constrain is not part of this path; ignored"));
+    std::lock_guard<std::mutex> lk(l.mu);
+    const std::string path = l.in_path + "type_constrain.txt";
+    FILE *f = fopen(path.c_str(), "r");
+    if (!f) return legacy_err(pt::fail(PT_EIO, "importTypeFiles: cannot open " + path));
+    const int64_t R = l.rel_total;
+    for (int s = 0; s < 2; ++s) {
+        l.type_lef[s].assign((size_t)R, 0);
+        l.type_rig[s].assign((size_t)R, 0);
+        l.type_list[s].clear();
+    }
+    long tmp = 0;
+    bool ok = fscanf(f, "%ld", &tmp) == 1;
+    for (int64_t i = 0; ok && i < R; ++i) {
+        for (int s = 0; s < 2 && ok; ++s) {
+            long rel = 0, tot = 0;
+            ok = fscanf(f, "%ld %ld", &rel, &tot) == 2 && rel >= 0 && rel < R && tot >= 0;
+            if (!ok) break;
+            std::vector<int64_t> &v = l.type_list[s];
+            l.type_lef[s][(size_t)rel] = (int64_t)v.size();
+            for (long j = 0; j < tot && ok; ++j) {
+                long e = 0;
+                ok = fscanf(f, "%ld", &e) == 1;
+                v.push_back(e);
+            }
+            l.type_rig[s][(size_t)rel] = (int64_t)v.size();
+            std::sort(v.begin() + l.type_lef[s][(size_t)rel], v.end());
+        }
+    }
+    fclose(f);
+    l.types_loaded = ok;
+    if (!ok) legacy_err(pt::fail(PT_EIO, "importTypeFiles: malformed " + path));
+}
+
+// Type-constrained counts of one query (Test.h:168-178 / :288-298). The reference walks candidate
+// POSITIONS j = 1..E-1 and matches j against the relation's sorted type list as an ENTITY id, so the
+// score it compares for type entity j is con[j] (the candidate at position j) and the filter asks
+// _find about entity j; nothing is counted when con[0] == inf. Restated as is.
+static void rank_constrained(const Legacy &l, const pt::Triple &q, int side, const float *con, int64_t *raw,
+                             int64_t *filt) {
+    int64_t s = 0, fs = 0;
+    const float minimal = con[0];
+    if (minimal != INFINITY) {
+        const std::vector<int64_t> &v = l.type_list[side];
+        const int64_t lo = l.type_lef[side][(size_t)q.r], hi = l.type_rig[side][(size_t)q.r];
+        for (int64_t k = lo; k < hi; ++k) {
+            const int64_t j = v[(size_t)k];
+            if (j < 1 || j >= l.ent_total || (k > lo && v[(size_t)k - 1] == j)) continue;
+            if (con[j] < minimal) {
+                ++s;
+                if (!(side == 0 ? pt::known_has(*l.known, j, q.t, q.r) : pt::known_has(*l.known, q.h, j, q.r))) ++fs;
+            }
+        }
+    }
+    *raw = s;
+    *filt = fs;
+}
+
+static void test_one(float *con, int64_t idx, int64_t type_constrain, int side) {
+    Legacy &l = L();
     const pt::Triple &q = l.test[(size_t)idx];
     int64_t raw, filt;
-    pt::rank_one(*l.known, l.ent_total, q.h, q.t, q.r, 0, con, &raw, &filt);
-    accumulate(l.acc, 0, raw, filt);
+    pt::rank_one(*l.known, l.ent_total, q.h, q.t, q.r, side, con, &raw, &filt);
+    accumulate(l.acc, side, raw, filt);
+    if (type_constrain) {
+        if (!l.types_loaded) {
+            legacy_err(pt::fail(PT_ESTATE, "type_constrain needs importTypeFiles() first (the reference reads "
+                                           "unallocated type arrays, Test.h:127-130)"));
+            return;
+        }
+        rank_constrained(l, q, side, con, &raw, &filt);
+        accumulate(l.acc_tc, side, raw, filt);
+    }
 }
-extern "C" void testTail(float *con, int64_t idx, int64_t type_constrain) {
-    Legacy &l = L();
-    if (type_constrain) legacy_err(pt::fail(PT_ENOTSUP, "type_constrain is not part of this path; ignored"));
-    const pt::Triple &q = l.test[(size_t)idx];
-    int64_t raw, filt;
-    pt::rank_one(*l.known, l.ent_total, q.h, q.t, q.r, 1, con, &raw, &filt);
-    accumulate(l.acc, 1, raw, filt);
-}
-extern "C" void test_link_prediction(int64_t type_constrain) {
-    (void)type_constrain;
-    Legacy &l = L();
-    TestAcc &a = l.acc;
-    const float n = (float)l.test_total;
+extern "C" void testHead(float *con, int64_t idx, int64_t type_constrain) { test_one(con, idx, type_constrain, 0); }
+extern "C" void testTail(float *con, int64_t idx, int64_t type_constrain) { test_one(con, idx, type_constrain, 1); }
+
+// test_link_prediction's averaging (Test.h:408-454, constrained block :456-502)
+static void finish_acc(TestAcc &a, float n, float out[5]) {
     a.l_rank /= n; a.r_rank /= n; a.l_reci /= n; a.r_reci /= n;
     a.l_tot /= n; a.l3_tot /= n; a.l1_tot /= n; a.r_tot /= n; a.r3_tot /= n; a.r1_tot /= n;
     a.l_filter_rank /= n; a.r_filter_rank /= n; a.l_filter_reci /= n; a.r_filter_reci /= n;
     a.l_filter_tot /= n; a.l3_filter_tot /= n; a.l1_filter_tot /= n;
     a.r_filter_tot /= n; a.r3_filter_tot /= n; a.r1_filter_tot /= n;
+    out[0] = (a.l_filter_reci + a.r_filter_reci) / 2;
+    out[1] = (a.l_filter_rank + a.r_filter_rank) / 2;
+    out[2] = (a.l_filter_tot + a.r_filter_tot) / 2;
+    out[3] = (a.l3_filter_tot + a.r3_filter_tot) / 2;
+    out[4] = (a.l1_filter_tot + a.r1_filter_tot) / 2;
+}
+
+extern "C" void test_link_prediction(int64_t type_constrain) {
+    Legacy &l = L();
+    if (type_constrain) {
+        float m[5];
+        finish_acc(l.acc_tc, (float)l.test_total, m);
+        l.mrr_tc = m[0]; l.mr_tc = m[1]; l.hit10_tc = m[2]; l.hit3_tc = m[3]; l.hit1_tc = m[4];
+        printf("type constraint results:\n");
+        printf("averaged(filter):\t %f \t %f \t %f \t %f \t %f \n", m[0], m[1], m[2], m[3], m[4]);
+    }
+    TestAcc &a = l.acc;
+    float m[5];
+    finish_acc(a, (float)l.test_total, m);
     printf("metric:\t\t\t MRR \t\t MR \t\t hit@10 \t hit@3  \t hit@1 \n");
     printf("averaged(raw):\t\t %f \t %f \t %f \t %f \t %f \n", (a.l_reci + a.r_reci) / 2, (a.l_rank + a.r_rank) / 2,
            (a.l_tot + a.r_tot) / 2, (a.l3_tot + a.r3_tot) / 2, (a.l1_tot + a.r1_tot) / 2);
-    l.mrr = (a.l_filter_reci + a.r_filter_reci) / 2;
-    l.mr = (a.l_filter_rank + a.r_filter_rank) / 2;
-    l.hit10 = (a.l_filter_tot + a.r_filter_tot) / 2;
-    l.hit3 = (a.l3_filter_tot + a.r3_filter_tot) / 2;
-    l.hit1 = (a.l1_filter_tot + a.r1_filter_tot) / 2;
+    l.mrr = m[0]; l.mr = m[1]; l.hit10 = m[2]; l.hit3 = m[3]; l.hit1 = m[4];
     printf("averaged(filter):\t %f \t %f \t %f \t %f \t %f \n", l.mrr, l.mr, l.hit10, l.hit3, l.hit1);
 }
-extern "C" float getTestLinkMRR(int64_t) { return L().mrr; }
-extern "C" float getTestLinkMR(int64_t) { return L().mr; }
-extern "C" float getTestLinkHit10(int64_t) { return L().hit10; }
-extern "C" float getTestLinkHit3(int64_t) { return L().hit3; }
-extern "C" float getTestLinkHit1(int64_t) { return L().hit1; }
+extern "C" float getTestLinkMRR(int64_t tc) { return tc ? L().mrr_tc : L().mrr; }
+extern "C" float getTestLinkMR(int64_t tc) { return tc ? L().mr_tc : L().mr; }
+extern "C" float getTestLinkHit10(int64_t tc) { return tc ? L().hit10_tc : L().hit10; }
+extern "C" float getTestLinkHit3(int64_t tc) { return tc ? L().hit3_tc : L().hit3; }
+extern "C" float getTestLinkHit1(int64_t tc) { return tc ? L().hit1_tc : L().hit1; }
+
+// the loaded type lists for the GPU ranking: side 0 heads, 1 tails; lef/rig per relation (relTotal
+// entries each) and the lists; returns the list length (-1 before importTypeFiles). NULL outputs skip.
+extern "C" int64_t pt_legacy_types(int32_t side, int64_t *lef, int64_t *rig, int64_t *list) {
+    Legacy &l = L();
+    if (!l.types_loaded || (side != 0 && side != 1)) return -1;
+    const auto &lv = l.type_lef[side], &rv = l.type_rig[side], &tv = l.type_list[side];
+    if (lef) std::copy(lv.begin(), lv.end(), lef);
+    if (rig) std::copy(rv.begin(), rv.end(), rig);
+    if (list) std::copy(tv.begin(), tv.end(), list);
+    return (int64_t)tv.size();
+}
 
 extern "C" void validInit(void) {
     Legacy &l = L();

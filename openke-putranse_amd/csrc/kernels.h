@@ -142,5 +142,9 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
 hipError_t launch_rank_rows(const float *rows, int64_t E, const int64_t *row_of, const int64_t *truth,
                             const float *repl, const int64_t *part_off, const int64_t *part, int64_t nq, int64_t *raw,
                             int64_t *filt, hipStream_t st);
+hipError_t launch_rank_types(const float *rows, int64_t E, const int64_t *row_of, const int64_t *truth,
+                             const float *repl, const int64_t *rel, const int64_t *type_lef, const int64_t *type_rig,
+                             const int64_t *types, const int64_t *part_off, const int64_t *part, int64_t nq,
+                             int64_t *raw, int64_t *filt, hipStream_t st);
 
 }  // namespace pt

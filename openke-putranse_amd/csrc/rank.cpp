@@ -77,6 +77,7 @@ void rank_one(const pt_known &k, int64_t E, int64_t h, int64_t t, int64_t r, int
     *raw = rs;
     *filt = fs;
 }
+bool known_has(const pt_known &k, int64_t h, int64_t t, int64_t r) { return k.has(h, t, r); }
 }  // namespace pt
 
 extern "C" int pt_known_create(const int64_t *h, const int64_t *t, const int64_t *r, int64_t n, pt_known **out) {
@@ -114,7 +115,7 @@ extern "C" int pt_rank_queries(const pt_known *k, int64_t E, const int64_t *h, c
 
 // CSR of the known partners of many (anchor, r) queries: side 0 (head prediction, anchor = t) lists the
 // h with (h, t, r) known; side 1 (tail prediction, anchor = h) lists the t with (h, t, r) known.
-// off[n + 1]; when list is NULL only off is filled (off[n] = total).
+// off[n + 1]; when list is NULL only off is filled (off[n] = total). Each query's list is ascending.
 extern "C" int pt_known_partners(const pt_known *k, int32_t side, int64_t n, const int64_t *anchor, const int64_t *rel,
                                  int64_t *off, int64_t *list) {
     if (!k || (n > 0 && (!anchor || !rel)) || !off || (side != 0 && side != 1))
@@ -131,6 +132,7 @@ extern "C" int pt_known_partners(const pt_known *k, int32_t side, int64_t n, con
                 ++c;
             }
         }
+        if (list) std::sort(list + off[q], list + off[q] + c);   // ascending: pt_rank_types bisects it
         off[q + 1] = off[q] + c;
     }
     return PT_OK;

@@ -82,7 +82,81 @@ __global__ __launch_bounds__(256) void k_rank_rows(const float *__restrict__ row
     }
 }
 
+// Type-constrained counts (testHead/testTail with type_constrain, Test.h:127-130, :168-178, :288-298).
+// The reference walks candidate POSITIONS j = 1..E-1 and matches j against the relation's sorted type
+// list as an ENTITY id: for type entity j it compares con[j], the score of the candidate at position j
+// - entity j-1 when j-1 < truth, else entity j - and its filter asks _find about entity j itself.
+// Restated on the global-order row: one workgroup per query walks the relation's type list (duplicates
+// and ids outside [1, E) skipped, as the reference's merge skips them), gathers val(c(j)) and bisects
+// the query's ascending partner list for j. Nothing is counted when the truth's score is +inf.
+__global__ __launch_bounds__(256) void k_rank_types(const float *__restrict__ rows, int64_t E,
+                                                    const int64_t *__restrict__ row_of, const int64_t *__restrict__ truth,
+                                                    const float *__restrict__ repl, const int64_t *__restrict__ rel,
+                                                    const int64_t *__restrict__ type_lef,
+                                                    const int64_t *__restrict__ type_rig,
+                                                    const int64_t *__restrict__ types, const int64_t *__restrict__ part_off,
+                                                    const int64_t *__restrict__ part, int64_t *__restrict__ raw,
+                                                    int64_t *__restrict__ filt) {
+    __shared__ int64_t red[2][4];
+    const int64_t q = blockIdx.x;
+    const float *row = rows + row_of[q] * E;
+    const float rp = repl ? repl[q] : INFINITY;
+    const int64_t tr = truth[q];
+    const float s0 = repl_val(row[tr], rp);
+    int64_t below = 0, unknown_below = 0;
+    if (s0 != INFINITY) {
+        const int64_t r = rel[q], lo = type_lef[r], hi = type_rig[r];
+        const int64_t plo = part_off[q], phi = part_off[q + 1];
+        for (int64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
+            const int64_t j = types[k];
+            if (j < 1 || j >= E || (k > lo && types[k - 1] == j)) continue;
+            const int64_t c = j - 1 < tr ? j - 1 : j;
+            if (!(repl_val(row[c], rp) < s0)) continue;
+            ++below;
+            int64_t a = plo, b = phi;   // first partner >= j
+            while (a < b) {
+                const int64_t m = (a + b) >> 1;
+                if (part[m] < j) a = m + 1; else b = m;
+            }
+            unknown_below += !(a < phi && part[a] == j);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        below += __shfl_down(below, o, 64);
+        unknown_below += __shfl_down(unknown_below, o, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][w] = below;
+        red[1][w] = unknown_below;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t b = 0, u = 0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+            b += red[0][i];
+            u += red[1][i];
+        }
+        raw[q] = b;
+        filt[q] = u;
+    }
+}
+
 }  // namespace dev
+
+hipError_t launch_rank_types(const float *rows, int64_t E, const int64_t *row_of, const int64_t *truth,
+                             const float *repl, const int64_t *rel, const int64_t *type_lef, const int64_t *type_rig,
+                             const int64_t *types, const int64_t *part_off, const int64_t *part, int64_t nq,
+                             int64_t *raw, int64_t *filt, hipStream_t st) {
+    if (nq <= 0) return hipSuccess;
+    for (int64_t off = 0; off < nq; off += 1 << 30) {
+        const int64_t n = nq - off < (1 << 30) ? nq - off : (1 << 30);
+        hipLaunchKernelGGL(dev::k_rank_types, dim3((unsigned)n), dim3(256), 0, st, rows, E, row_of + off, truth + off,
+                           repl ? repl + off : nullptr, rel + off, type_lef, type_rig, types, part_off + off, part,
+                           raw + off, filt + off);
+    }
+    return hipGetLastError();
+}
 
 hipError_t launch_rank_rows(const float *rows, int64_t E, const int64_t *row_of, const int64_t *truth,
                             const float *repl, const int64_t *part_off, const int64_t *part, int64_t nq, int64_t *raw,

@@ -100,6 +100,8 @@ SIGNATURES = {
     "pt_lp_min_scores": (ctypes.c_int, [ctypes.POINTER(LpUniverse), c_i64, c_i32, c_i32, c_i32,
                                         ctypes.POINTER(LpPair), c_i64, c_i64, c_vp, c_vp, c_vp]),
     "pt_rank_rows": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "pt_rank_types": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
+                                     c_vp, c_vp]),
     "pt_known_partners": (ctypes.c_int, [c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "pt_known_create": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(c_vp)]),
     "pt_known_free": (ctypes.c_int, [c_vp]),
@@ -109,6 +111,7 @@ SIGNATURES = {
     "pt_legacy_graph": (c_vp, []),
     "pt_legacy_eval_triples": (c_i64, [c_i32, c_vp, c_vp, c_vp]),
     "pt_legacy_known": (c_vp, []),
+    "pt_legacy_types": (c_i64, [c_i32, c_vp, c_vp, c_vp]),
     # Base.so surface (argument types as the reference's loaders declare them)
     "setInPath": (None, [ctypes.c_char_p]),
     "setOutPath": (None, [ctypes.c_char_p]),
@@ -136,6 +139,7 @@ SIGNATURES = {
     "resetUniverse": (None, []),
     "activateLoadOfAllTriples": (None, [c_i64]),
     "importTestFiles": (None, []),
+    "importTypeFiles": (None, []),
     "initTest": (None, []),
     "getHeadBatch": (None, [c_vp, c_vp, c_vp]),
     "getTailBatch": (None, [c_vp, c_vp, c_vp]),

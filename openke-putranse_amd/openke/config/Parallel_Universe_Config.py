@@ -39,7 +39,7 @@ from ..data import TestDataLoader
 from ..module.loss import MarginLoss
 from ..module.model.Model import Model
 from ..module.strategy import NegativeSampling
-from .Tester import Tester
+from .Tester import Tester, device_type_lists, rank_types
 
 
 def get_string_key(entity, relation):
@@ -591,8 +591,9 @@ class Parallel_Universe_Config(Tester):
         else:
             print("- No universes to be evaluated.")
 
-    def _ranks(self, eval_mode):
-        """raw / filtered ranks of every query of the split (head side, tail side) on the GPU."""
+    def _ranks(self, eval_mode, types=None):
+        """raw / filtered ranks of every query of the split (head side, tail side) on the GPU; with `types`
+        (Tester.device_type_lists) the type-constrained pair of each side follows."""
         L = _native.lib()
         st = self._store(eval_mode)
         known = L.pt_legacy_known()
@@ -620,6 +621,12 @@ class Parallel_Universe_Config(Tester):
                                          _native.ptr(d_repl), _native.ptr(d_off), _native.ptr(d_part), n,
                                          _native.ptr(raw), _native.ptr(filt), _native.stream()))
             out.append((raw.cpu().numpy(), filt.cpu().numpy()))
+            if types:
+                d_rel = torch.from_numpy(r).to(dev)
+                out.append(rank_types(L, st.rows, self.ent_tot, d_row, d_truth, d_repl, d_rel, types[side], d_off,
+                                      d_part, n))
+        if types:
+            return [out[0], out[2], out[1], out[3]]   # head, tail, then the constrained head, tail
         return out   # [(raw_head, filt_head), (raw_tail, filt_tail)]
 
     def valid(self):
@@ -707,16 +714,21 @@ class Parallel_Universe_Config(Tester):
         return best
 
     def run_link_prediction(self, type_constrain=False):
-        if type_constrain:
-            raise NotImplementedError("type-constrained ranking is outside the accelerated path")
         self.data_loader.set_sampling_mode('link')
         self.eval_universes(eval_mode='test')
-        (rh, fh), (rt, ft) = self._ranks('test')
         L = _native.lib()
+        types = device_type_lists(L, self._store('test').rows.device) if type_constrain else None
+        ranks = self._ranks('test', types)
+        (rh, fh), (rt, ft) = ranks[:2]
         met = np.zeros(10, dtype=np.float32)
         _native.check(L.pt_lp_metrics(rh.ctypes.data, fh.ctypes.data, rt.ctypes.data, ft.ctypes.data, len(rh),
                                       met.ctypes.data))
         self.last_ranks = (rh, fh, rt, ft)
+        if type_constrain:   # the constrained metrics, as the reference's getters return them (Test.h:533-567)
+            (crh, cfh), (crt, cft) = ranks[2:]
+            self.last_tc_ranks = (crh, cfh, crt, cft)
+            _native.check(L.pt_lp_metrics(crh.ctypes.data, cfh.ctypes.data, crt.ctypes.data, cft.ctypes.data,
+                                          len(rh), met.ctypes.data))
         mrr, mr, hit10, hit3, hit1 = (float(x) for x in met[:5])
         print('Mean Reciprocal Rank: {}'.format(mrr))
         print('Mean Rank: {}'.format(mr))

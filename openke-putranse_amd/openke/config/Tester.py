@@ -14,6 +14,38 @@ import torch
 from .. import _native
 
 
+def device_type_lists(lib, dev):
+    """The head / tail type lists of importTypeFiles (Reader.h:344-396) as device tensors
+    [(lef, rig, list)] per side. The reference dereferences them unloaded when its Python asks for
+    type_constrain without calling importTypeFiles (Test.h:127-130); here they are loaded on first use."""
+    if lib.pt_legacy_types(0, None, None, None) < 0:
+        lib.importTypeFiles()
+    out = []
+    for side in (0, 1):
+        n = lib.pt_legacy_types(side, None, None, None)
+        if n < 0:
+            raise RuntimeError("type_constrain: no readable type_constrain.txt in the input folder")
+        R = lib.getRelationTotal()
+        lef, rig = np.zeros(R, dtype=np.int64), np.zeros(R, dtype=np.int64)
+        lst = np.zeros(max(n, 1), dtype=np.int64)
+        lib.pt_legacy_types(side, lef.ctypes.data, rig.ctypes.data, lst.ctypes.data)
+        out.append(tuple(torch.from_numpy(x).to(dev) for x in (lef, rig, lst)))
+    return out
+
+
+def rank_types(lib, rows, E, d_row, d_truth, d_repl, d_rel, types, d_off, d_part, n):
+    """Type-constrained raw / filtered counts on the GPU (pt_rank_types)."""
+    dev = rows.device
+    raw = torch.zeros(n, dtype=torch.int64, device=dev)
+    filt = torch.zeros(n, dtype=torch.int64, device=dev)
+    lef, rig, lst = types
+    _native.check(lib.pt_rank_types(_native.ptr(rows), E, _native.ptr(d_row), _native.ptr(d_truth), _native.ptr(d_repl),
+                                    _native.ptr(d_rel), _native.ptr(lef), _native.ptr(rig), _native.ptr(lst),
+                                    _native.ptr(d_off), _native.ptr(d_part), n, _native.ptr(raw), _native.ptr(filt),
+                                    _native.stream()))
+    return raw.cpu().numpy(), filt.cpu().numpy()
+
+
 class Tester(object):
 
     def __init__(self, model=None, data_loader=None, use_gpu=True):
@@ -55,8 +87,9 @@ class Tester(object):
                                                 _native.ptr(qr), len(h), _native.ptr(out), _native.stream()))
         return out
 
-    def _rank_all(self, h, t, r, E):
-        """raw/filtered head and tail ranks for every test query (chunked to bound memory)."""
+    def _rank_all(self, h, t, r, E, types=None):
+        """raw/filtered head and tail ranks for every test query (chunked to bound memory); with `types`
+        (device_type_lists) also the type-constrained ones (ranks[4:8])."""
         n = len(h)
         known = self.lib.pt_legacy_known()
         if not known:
@@ -64,7 +97,7 @@ class Tester(object):
         kge = self.model
         dev = kge.ent_embeddings.weight.device
         desc = kge.native_desc()
-        ranks = [np.zeros(n, dtype=np.int64) for _ in range(4)]
+        ranks = [np.zeros(n, dtype=np.int64) for _ in range(8 if types else 4)]
         chunk = max(1, min(65535, (1 << 30) // (4 * max(E, 1))))
         for s in range(0, n, chunk):
             e = min(n, s + chunk)
@@ -90,20 +123,30 @@ class Tester(object):
                                                     _native.ptr(filt), _native.stream()))
                 ranks[2 * side][s:e] = raw.cpu().numpy()
                 ranks[2 * side + 1][s:e] = filt.cpu().numpy()
+                if types:
+                    rc, fc = rank_types(self.lib, rows, E, row_of, truth, None, qr, types[side], d_off, d_part, m)
+                    ranks[4 + 2 * side][s:e] = rc
+                    ranks[5 + 2 * side][s:e] = fc
         return ranks
 
     def run_link_prediction(self, type_constrain=False):
-        if type_constrain:
-            raise NotImplementedError("type-constrained ranking is outside the accelerated path")
+        """Tester.py:70-93: filtered (mrr, mr, hit10, hit3, hit1); with type_constrain the constrained
+        ones, as the reference's getters return them (Test.h:533-567)."""
         self.data_loader.set_sampling_mode('link')
         h, t, r = self.data_loader.eval_triples()
         E = self.data_loader.get_ent_tot()
-        rh, fh, rt, ft = self._rank_all(h, t, r, E)
+        types = device_type_lists(self.lib, self.model.ent_embeddings.weight.device) if type_constrain else None
+        ranks = self._rank_all(h, t, r, E, types)
+        rh, fh, rt, ft = ranks[:4]
         met = np.zeros(10, dtype=np.float32)
         _native.check(self.lib.pt_lp_metrics(rh.ctypes.data, fh.ctypes.data, rt.ctypes.data, ft.ctypes.data, len(h),
                                              met.ctypes.data))
         self.last_ranks = (rh, fh, rt, ft)
         self.last_raw_metrics = tuple(float(x) for x in met[5:])
+        self.last_metrics = tuple(float(x) for x in met[:5])
+        if type_constrain:
+            self.last_tc_ranks = tuple(ranks[4:])
+            _native.check(self.lib.pt_lp_metrics(*(x.ctypes.data for x in ranks[4:]), len(h), met.ctypes.data))
         mrr, mr, hit10, hit3, hit1 = (float(x) for x in met[:5])
         print(hit10)
         return mrr, mr, hit10, hit3, hit1

@@ -767,3 +767,65 @@ void oracle_link_prediction(int64_t E, const int64_t *ah, const int64_t *at, con
     metrics[4] = (l1_filter_tot + r1_filter_tot) / 2;
     free(all);
 }
+
+/* Type-constrained counts of testHead / testTail (Test.h:127-130, :168-178, :225-237 and the tail mirror
+ * :248-251, :288-298, :346-358), restated literally: j walks the candidate POSITIONS 1..E-1 while the
+ * sorted type list of r is scanned for j as an ENTITY id, so con[j] (the score of the candidate at
+ * position j) is compared for entity j, and the filter asks _find for entity j. Nothing is counted when
+ * con[0] == inf. Metrics as the constrained block of test_link_prediction (Test.h:456-502). */
+void oracle_rank_constrained(int64_t E, const int64_t *ah, const int64_t *at, const int64_t *ar, int64_t n_all,
+                             const int64_t *th, const int64_t *tt, const int64_t *tr, int64_t n_test,
+                             const float *con_head, const float *con_tail, const int64_t *head_lef,
+                             const int64_t *head_rig, const int64_t *head_type, const int64_t *tail_lef,
+                             const int64_t *tail_rig, const int64_t *tail_type, int64_t *rank_head,
+                             int64_t *frank_head, int64_t *rank_tail, int64_t *frank_tail, float *metrics) {
+    otriple *all = malloc(sizeof(otriple) * (size_t)(n_all ? n_all : 1));
+    for (int64_t i = 0; i < n_all; ++i) { all[i].h = ah[i]; all[i].t = at[i]; all[i].r = ar[i]; }
+    qsort(all, (size_t)n_all, sizeof(otriple), cmp_head);
+    float lt = 0, l3 = 0, l1 = 0, lr = 0, li = 0, rt = 0, r3 = 0, r1 = 0, rr_ = 0, ri = 0;
+    for (int64_t q = 0; q < n_test; ++q) {
+        int64_t h = th[q], t = tt[q], r = tr[q];
+        for (int side = 0; side < 2; ++side) {
+            const float *con = (side == 0 ? con_head : con_tail) + q * E;
+            const int64_t *type = side == 0 ? head_type : tail_type;
+            int64_t lef = side == 0 ? head_lef[r] : tail_lef[r], rig = side == 0 ? head_rig[r] : tail_rig[r];
+            int64_t s = 0, fs = 0;
+            const float minimal = con[0];
+            if (minimal != INFINITY) {
+                for (int64_t j = 1; j < E; ++j) {
+                    while (lef < rig && type[lef] < j) lef++;
+                    if (lef < rig && j == type[lef] && con[j] < minimal) {
+                        s++;
+                        int known = side == 0 ? find_triple(all, n_all, j, t, r) : find_triple(all, n_all, h, j, r);
+                        if (!known) fs++;
+                    }
+                }
+            }
+            if (side == 0) {
+                rank_head[q] = s; frank_head[q] = fs;
+                if (fs < 10) lt += 1;
+                if (fs < 3) l3 += 1;
+                if (fs < 1) l1 += 1;
+                lr += (float)(fs + 1);
+                li = (float)((double)li + 1.0 / (double)(fs + 1));
+            } else {
+                rank_tail[q] = s; frank_tail[q] = fs;
+                if (fs < 10) rt += 1;
+                if (fs < 3) r3 += 1;
+                if (fs < 1) r1 += 1;
+                rr_ += (float)(1 + fs);
+                ri = (float)((double)ri + 1.0 / (double)(1 + fs));
+            }
+        }
+    }
+    float nt = (float)n_test;
+    lr /= nt; rr_ /= nt; li /= nt; ri /= nt;
+    lt /= nt; l3 /= nt; l1 /= nt;
+    rt /= nt; r3 /= nt; r1 /= nt;
+    metrics[0] = (li + ri) / 2;                             /* Test.h:498-502 */
+    metrics[1] = (lr + rr_) / 2;
+    metrics[2] = (lt + rt) / 2;
+    metrics[3] = (l3 + r3) / 2;
+    metrics[4] = (l1 + r1) / 2;
+    free(all);
+}

@@ -86,4 +86,13 @@ int64_t oracle_train_loop(const okg *g, uint64_t *states, int64_t threads, int64
                           int64_t filter, int model, int p_norm, int norm_flag, int opt, float lr, float margin,
                           int64_t dim, float *ent, float *rel, float *normv, float *ent_acc, float *rel_acc,
                           float *norm_acc, int64_t steps);
+/* type-constrained counts and metrics of testHead/testTail/test_link_prediction (Test.h:127-502); type
+ * lists per relation [lef, rig) as importTypeFiles builds them (Reader.h:352-396) */
+void oracle_rank_constrained(int64_t E, const int64_t *ah, const int64_t *at, const int64_t *ar, int64_t n_all,
+                             const int64_t *th, const int64_t *tt, const int64_t *tr, int64_t n_test,
+                             const float *con_head, const float *con_tail, const int64_t *head_lef,
+                             const int64_t *head_rig, const int64_t *head_type, const int64_t *tail_lef,
+                             const int64_t *tail_rig, const int64_t *tail_type, int64_t *rank_head,
+                             int64_t *frank_head, int64_t *rank_tail, int64_t *frank_tail, float *metrics);
+
 #endif

@@ -57,6 +57,8 @@ def lib():
         L.oracle_sort_test.argtypes = [ctypes.c_int64, i64p, i64p, i64p]
         L.oracle_link_prediction.argtypes = ([ctypes.c_int64] + [i64p] * 3 + [ctypes.c_int64] + [i64p] * 3 +
                                              [ctypes.c_int64] + [f32p] * 2 + [i64p] * 4 + [f32p])
+        L.oracle_rank_constrained.argtypes = ([ctypes.c_int64] + [i64p] * 3 + [ctypes.c_int64] + [i64p] * 3 +
+                                              [ctypes.c_int64] + [f32p] * 2 + [i64p] * 6 + [i64p] * 4 + [f32p])
         L.oracle_train_loop.restype = ctypes.c_int64
         L.oracle_train_loop.argtypes = ([ctypes.c_void_p, u64p] + [ctypes.c_int64] * 5 + [ctypes.c_int] * 4 +
                                         [ctypes.c_float] * 2 + [ctypes.c_int64] + [f32p] * 6 + [ctypes.c_int64])
@@ -221,6 +223,46 @@ def link_prediction(E, all_triples, test, con_head, con_tail):
     lib().oracle_link_prediction(E, _p(ah, i64p), _p(at, i64p), _p(ar, i64p), len(ah), _p(th, i64p),
                                  _p(tt, i64p), _p(tr, i64p), n, _p(ch, f32p), _p(ct, f32p), _p(rh, i64p),
                                  _p(fh, i64p), _p(rt, i64p), _p(ft, i64p), _p(met, f32p))
+    return met, (rh, fh, rt, ft)
+
+
+def read_types(path, rel_total):
+    """importTypeFiles (Reader.h:352-396): `type_constrain.txt` = a count, then per relation two lines
+    `r n e_1 .. e_n` (heads, then tails); relationTotal records read, each list sorted in place.
+    Returns (head_lef, head_rig, head_type, tail_lef, tail_rig, tail_type) with lef/rig per relation."""
+    with open(path) as f:
+        tok = f.read().split()
+    pos = 1
+    lef = [np.zeros(rel_total, dtype=np.int64) for _ in range(2)]
+    rig = [np.zeros(rel_total, dtype=np.int64) for _ in range(2)]
+    types = [[], []]
+    for _ in range(rel_total):
+        for side in range(2):
+            r, n = int(tok[pos]), int(tok[pos + 1])
+            pos += 2
+            vals = sorted(int(x) for x in tok[pos:pos + n])
+            pos += n
+            lef[side][r] = len(types[side])
+            types[side].extend(vals)
+            rig[side][r] = len(types[side])
+    ht, tt = (np.array(x if x else [0], dtype=np.int64) for x in types)
+    return lef[0], rig[0], ht, lef[1], rig[1], tt
+
+
+def rank_constrained(E, all_triples, test, con_head, con_tail, types):
+    """Type-constrained ranks and metrics (Test.h:127-502), restated literally (see oracle.c)."""
+    ah, at, ar = (np.ascontiguousarray(x, dtype=np.int64) for x in all_triples)
+    th, tt, tr = (np.ascontiguousarray(x, dtype=np.int64) for x in test)
+    n = len(th)
+    rh, fh, rt, ft = (np.zeros(n, dtype=np.int64) for _ in range(4))
+    met = np.zeros(5, dtype=np.float32)
+    ch = np.ascontiguousarray(con_head, dtype=np.float32)
+    ct = np.ascontiguousarray(con_tail, dtype=np.float32)
+    hl, hr, hty, tl, trr, tty = (np.ascontiguousarray(x, dtype=np.int64) for x in types)
+    lib().oracle_rank_constrained(E, _p(ah, i64p), _p(at, i64p), _p(ar, i64p), len(ah), _p(th, i64p),
+                                  _p(tt, i64p), _p(tr, i64p), n, _p(ch, f32p), _p(ct, f32p), _p(hl, i64p),
+                                  _p(hr, i64p), _p(hty, i64p), _p(tl, i64p), _p(trr, i64p), _p(tty, i64p),
+                                  _p(rh, i64p), _p(fh, i64p), _p(rt, i64p), _p(ft, i64p), _p(met, f32p))
     return met, (rh, fh, rt, ft)
 
 

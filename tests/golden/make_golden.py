@@ -81,6 +81,14 @@ LP_CASES = [
 ]
 
 
+LPT_CASES = [
+    # type-constrained link prediction (Tester.run_link_prediction(type_constrain=True)); the reference
+    # only reads type_constrain.txt when importTypeFiles() is called (Reader.h:352-396), so the case calls it
+    # name, model, dim, p_norm, torch_seed
+    ("t1", "TransE", 16, 1, 23),
+    ("t2", "TransH", 10, 2, 24),
+]
+
 TC_CASES = [
     # name, model, dim, p_norm, torch_seed
     ("c1", "TransE", 16, 1, 31),
@@ -277,6 +285,52 @@ def case_lp(out, name, model, dim, p, tseed):
                         metrics=np.array(res, dtype=np.float64), **tables)
 
 
+def write_type_file(ds_path, seed=0):
+    """type_constrain.txt for a synthetic dataset (the format importTypeFiles reads, Reader.h:352-396): per
+    relation the heads and tails seen with it in train/valid/test, thinned at random (so the constraint
+    drops candidates that do score well) plus a few random unseen entities, and unsorted per line."""
+    rng = np.random.default_rng(seed)
+    trip = np.concatenate([np.loadtxt(ds_path + f, dtype=np.int64, ndmin=2)
+                           for f in ("train2id.txt", "valid2id.txt", "test2id.txt")])
+    with open(ds_path + "entity2id.txt") as f:
+        E = sum(1 for _ in f)
+    with open(ds_path + "relation2id.txt") as f:
+        R = sum(1 for _ in f)
+    lines = [str(R)]
+    for r in range(R):
+        sel = trip[trip[:, 2] == r]
+        for col in (0, 1):
+            ents = np.unique(sel[:, col])
+            keep = ents[rng.random(len(ents)) < 0.7]
+            extra = rng.integers(0, E, size=int(rng.integers(0, 6)))
+            vals = np.unique(np.concatenate([keep, extra]))
+            rng.shuffle(vals)
+            lines.append(" ".join([str(r), str(len(vals))] + [str(int(v)) for v in vals]))
+    with open(ds_path + "type_constrain.txt", "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def case_lpt(out, name, model, dim, p, tseed):
+    import torch
+    from openke.config import Tester
+    from openke.data import TestDataLoader
+    from openke.module.model import TransE, TransH
+    test_dl = TestDataLoader(DATASETS["small"], "link")
+    test_dl.lib.importTypeFiles()
+    torch.manual_seed(tseed)
+    cls = TransE if model == "TransE" else TransH
+    kge = cls(ent_tot=test_dl.get_ent_tot(), rel_tot=test_dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=True)
+    tables = {k.split(".")[0]: v.detach().numpy().copy() for k, v in kge.state_dict().items()
+              if "embeddings" in k or "norm_vector" in k}
+    tester = Tester(model=kge, data_loader=test_dl, use_gpu=False)
+    res = tester.run_link_prediction(type_constrain=True)
+    plain = [tester.lib.getTestLinkMRR(0), tester.lib.getTestLinkMR(0), tester.lib.getTestLinkHit10(0),
+             tester.lib.getTestLinkHit3(0), tester.lib.getTestLinkHit1(0)]
+    np.savez_compressed(out, model=model, dim=dim, p_norm=p, torch_seed=tseed,
+                        metrics_tc=np.array(res, dtype=np.float64), metrics=np.array(plain, dtype=np.float64),
+                        **tables)
+
+
 def case_tc(out, name, model, dim, p, tseed):
     """Tester.run_triple_classification on a random-init model (Tester.py:142-191), then one more
     getTestBatch call of the same loader (the negatives continue the thread-0 stream)."""
@@ -304,7 +358,7 @@ def run_case(kind, args_json, out, tmp):
     _import_reference(tmp)
     _silence()
     {"glibc": case_glibc, "sampler": case_sampler, "sampler_mode": case_sampler_mode, "train": case_train, "universes": case_universes,
-     "lp": case_lp, "tc": case_tc}[kind](out, *args)
+     "lp": case_lp, "lpt": case_lpt, "tc": case_tc}[kind](out, *args)
 
 
 def main():
@@ -312,6 +366,8 @@ def main():
     for ds, path in DATASETS.items():
         if not os.path.exists(os.path.join(path, "test2id.txt")):
             synth_kg.write_dataset(path, *synth_kg.SHAPES[ds], seed=0, ent_skew=synth_kg.ENT_SKEW[ds])
+    if not os.path.exists(DATASETS["small"] + "type_constrain.txt"):
+        write_type_file(DATASETS["small"])
     tmp = tempfile.mkdtemp(prefix="refpy_")
     jobs = [("glibc", [], "glibc_rand.npz")]
     jobs += [("sampler", list(c), "sampler_%s.npz" % c[0]) for c in SAMPLER_CASES]
@@ -319,6 +375,7 @@ def main():
     jobs += [("train", list(c), "train_%s.npz" % c[0]) for c in TRAIN_CASES]
     jobs += [("universes", list(c), "universes_%s.npz" % c[0]) for c in UNIVERSE_CASES]
     jobs += [("lp", list(c), "lp_%s.npz" % c[0]) for c in LP_CASES]
+    jobs += [("lpt", list(c), "lpt_%s.npz" % c[0]) for c in LPT_CASES]
     jobs += [("tc", list(c), "tc_%s.npz" % c[0]) for c in TC_CASES]
     only = sys.argv[1:]
     for kind, args, fname in jobs:

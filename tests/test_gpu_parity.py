@@ -158,6 +158,46 @@ def test_link_prediction_matches_reference(path):
     np.testing.assert_allclose(np.array(res, dtype=np.float32), z["metrics"].astype(np.float32), rtol=1e-6)
 
 
+@pytest.mark.parametrize("path", golden("lpt_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_type_constrained_link_prediction_matches_reference(path):
+    """Tester.run_link_prediction(type_constrain=True) (k_rank_types on the GPU rows) == the reference's
+    constrained metrics; the legacy testHead/testTail symbols with type_constrain on candidate-order
+    vectors give the same (host ranking, Test.h:118-504)."""
+    from openke.config import Tester
+    from openke.data import TestDataLoader
+    from openke.module.model import TransE, TransH
+    z = load(path)
+    test_dl = TestDataLoader(KG_SMALL, "link")
+    cls = TransE if str(z["model"]) == "TransE" else TransH
+    kge = cls(ent_tot=test_dl.get_ent_tot(), rel_tot=test_dl.get_rel_tot(), dim=int(z["dim"]),
+              p_norm=int(z["p_norm"]), norm_flag=True)
+    with torch.no_grad():
+        kge.ent_embeddings.weight.copy_(torch.from_numpy(z["ent_embeddings"]))
+        kge.rel_embeddings.weight.copy_(torch.from_numpy(z["rel_embeddings"]))
+        if str(z["model"]) == "TransH":
+            kge.norm_vector.weight.copy_(torch.from_numpy(z["norm_vector"]))
+    tester = Tester(model=kge, data_loader=test_dl, use_gpu=True)
+    res = tester.run_link_prediction(type_constrain=True)
+    np.testing.assert_allclose(np.array(res, dtype=np.float32), z["metrics_tc"].astype(np.float32), rtol=1e-6)
+    np.testing.assert_allclose(np.array(tester.last_metrics, dtype=np.float32), z["metrics"].astype(np.float32),
+                               rtol=1e-6)
+    # the reference's own loop over the Base.so-compatible symbols (Tester.py:70-93)
+    L = tester.lib
+    L.initTest()
+    E = test_dl.get_ent_tot()
+    for index, (dh, dt) in enumerate(test_dl):
+        con = np.ascontiguousarray(tester.test_one_step(dh), dtype=np.float32)
+        L.testHead(con.ctypes.data, index, 1)
+        con = np.ascontiguousarray(tester.test_one_step(dt), dtype=np.float32)
+        L.testTail(con.ctypes.data, index, 1)
+        assert len(con) == E
+    L.test_link_prediction(1)
+    got = [L.getTestLinkMRR(1), L.getTestLinkMR(1), L.getTestLinkHit10(1), L.getTestLinkHit3(1), L.getTestLinkHit1(1)]
+    np.testing.assert_allclose(np.array(got, dtype=np.float32), z["metrics_tc"].astype(np.float32), rtol=1e-6)
+    got = [L.getTestLinkMRR(0), L.getTestLinkMR(0), L.getTestLinkHit10(0), L.getTestLinkHit3(0), L.getTestLinkHit1(0)]
+    np.testing.assert_allclose(np.array(got, dtype=np.float32), z["metrics"].astype(np.float32), rtol=1e-6)
+
+
 @pytest.mark.parametrize("model,p,norm_flag", [("TransE", 1, True), ("TransE", 2, True), ("TransE", 2, False),
                                                ("TransH", 1, True), ("TransH", 2, True)])
 @pytest.mark.parametrize("dim", [8, 20, 50, 200, 300])

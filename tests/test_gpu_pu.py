@@ -353,3 +353,25 @@ def test_pu_triple_classification_matches_reference(path, tmp_path):
         assert (thr is None and np.isnan(want)) or float(thr) == want, (thr, want)
     else:
         np.testing.assert_allclose(float(thr), want, rtol=1e-5)
+
+
+@pytest.mark.parametrize("path", golden("universes_u*.npz")[:2], ids=lambda p: p.split("/")[-1])
+def test_pu_type_constrained_ranks_match_oracle(path, tmp_path):
+    """run_link_prediction(type_constrain=True): constrained ranks on the GPU (k_rank_types) == the
+    oracle's literal restatement of testHead/testTail's constrained branch (Test.h:127-502, pinned to the
+    reference by test_oracle's lpt goldens) on the same universes; the unconstrained ranks unchanged."""
+    z = load(path)
+    pu = _pu(z, tmp_path)
+    universes = _inject_reference_universes(pu, z)
+    res = pu.run_link_prediction(type_constrain=True)
+    met, ranks, (con_h, con_t) = _oracle_metrics(z, universes, "test2id.txt", with_con=True)
+    mism = _assert_ranks_match(pu.last_ranks, ranks, con_h, con_t)
+    kg = oracle.KG.load(KG_SMALL)
+    all_tr = [np.concatenate(x) for x in zip(*(oracle.read_triples(KG_SMALL + f)
+                                              for f in ("test2id.txt", "train2id.txt", "valid2id.txt")))]
+    ev = oracle.sort_test(*oracle.read_triples(KG_SMALL + "test2id.txt"))
+    types = oracle.read_types(KG_SMALL + "type_constrain.txt", kg.rel_total)
+    met_tc, ranks_tc = oracle.rank_constrained(kg.ent_total, all_tr, ev, con_h, con_t, types)
+    mism += _assert_ranks_match(pu.last_tc_ranks, ranks_tc, con_h, con_t)
+    if mism == 0:
+        np.testing.assert_allclose(np.array(res, dtype=np.float32), met_tc, rtol=1e-6, atol=1e-7)

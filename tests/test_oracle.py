@@ -173,3 +173,30 @@ def test_link_prediction_matches_reference(path):
         con_t[q] = oracle.score(model, p, True, "tail_batch", ent, rel, nv, [h], oracle.candidates(E, t), [r])
     met, _ = oracle.link_prediction(E, all_tr, test, con_h, con_t)
     np.testing.assert_allclose(met, z["metrics"].astype(np.float32), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("path", golden("lpt_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_type_constrained_link_prediction_matches_reference(path):
+    """Tester.run_link_prediction(type_constrain=True) after importTypeFiles (Test.h:127-502): the
+    constrained metrics, and the unconstrained ones of the same run."""
+    z = load(path)
+    model, p = str(z["model"]), int(z["p_norm"])
+    kg = oracle.KG.load(KG_SMALL)
+    E = kg.ent_total
+    ent, rel = z["ent_embeddings"], z["rel_embeddings"]
+    nv = z["norm_vector"] if model == "TransH" else None
+    test = oracle.sort_test(*oracle.read_triples(KG_SMALL + "test2id.txt"))
+    all_tr = [np.concatenate(x) for x in zip(*(oracle.read_triples(KG_SMALL + f)
+                                              for f in ("test2id.txt", "train2id.txt", "valid2id.txt")))]
+    n = len(test[0])
+    con_h = np.zeros((n, E), dtype=np.float32)
+    con_t = np.zeros((n, E), dtype=np.float32)
+    for q in range(n):
+        h, t, r = (int(x[q]) for x in test)
+        con_h[q] = oracle.score(model, p, True, "head_batch", ent, rel, nv, oracle.candidates(E, h), [t], [r])
+        con_t[q] = oracle.score(model, p, True, "tail_batch", ent, rel, nv, [h], oracle.candidates(E, t), [r])
+    types = oracle.read_types(KG_SMALL + "type_constrain.txt", kg.rel_total)
+    met_tc, _ = oracle.rank_constrained(E, all_tr, test, con_h, con_t, types)
+    np.testing.assert_allclose(met_tc, z["metrics_tc"].astype(np.float32), rtol=1e-6, atol=1e-7)
+    met, _ = oracle.link_prediction(E, all_tr, test, con_h, con_t)
+    np.testing.assert_allclose(met, z["metrics"].astype(np.float32), rtol=1e-6, atol=1e-7)
