@@ -89,6 +89,13 @@ LPT_CASES = [
     ("t2", "TransH", 10, 2, 24),
 ]
 
+VAL_CASES = [
+    # Validator.valid() (Validator.py:35-44): filtered hit@10 of the valid split
+    # name, model, dim, p_norm, torch_seed
+    ("v1", "TransE", 12, 1, 25),
+    ("v2", "TransH", 8, 2, 26),
+]
+
 TC_CASES = [
     # name, model, dim, p_norm, torch_seed
     ("c1", "TransE", 16, 1, 31),
@@ -331,6 +338,22 @@ def case_lpt(out, name, model, dim, p, tseed):
                         **tables)
 
 
+def case_val(out, name, model, dim, p, tseed):
+    import torch
+    from openke.config import Validator
+    from openke.data import TestDataLoader
+    from openke.module.model import TransE, TransH
+    valid_dl = TestDataLoader(DATASETS["small"], "link", mode='valid')
+    torch.manual_seed(tseed)
+    cls = TransE if model == "TransE" else TransH
+    kge = cls(ent_tot=valid_dl.get_ent_tot(), rel_tot=valid_dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=True)
+    tables = {k.split(".")[0]: v.detach().numpy().copy() for k, v in kge.state_dict().items()
+              if "embeddings" in k or "norm_vector" in k}
+    validator = Validator(model=kge, data_loader=valid_dl)
+    hit10 = validator.valid()
+    np.savez_compressed(out, model=model, dim=dim, p_norm=p, torch_seed=tseed, hit10=float(hit10), **tables)
+
+
 def case_tc(out, name, model, dim, p, tseed):
     """Tester.run_triple_classification on a random-init model (Tester.py:142-191), then one more
     getTestBatch call of the same loader (the negatives continue the thread-0 stream)."""
@@ -358,7 +381,7 @@ def run_case(kind, args_json, out, tmp):
     _import_reference(tmp)
     _silence()
     {"glibc": case_glibc, "sampler": case_sampler, "sampler_mode": case_sampler_mode, "train": case_train, "universes": case_universes,
-     "lp": case_lp, "lpt": case_lpt, "tc": case_tc}[kind](out, *args)
+     "lp": case_lp, "lpt": case_lpt, "val": case_val, "tc": case_tc}[kind](out, *args)
 
 
 def main():
@@ -376,6 +399,7 @@ def main():
     jobs += [("universes", list(c), "universes_%s.npz" % c[0]) for c in UNIVERSE_CASES]
     jobs += [("lp", list(c), "lp_%s.npz" % c[0]) for c in LP_CASES]
     jobs += [("lpt", list(c), "lpt_%s.npz" % c[0]) for c in LPT_CASES]
+    jobs += [("val", list(c), "val_%s.npz" % c[0]) for c in VAL_CASES]
     jobs += [("tc", list(c), "tc_%s.npz" % c[0]) for c in TC_CASES]
     only = sys.argv[1:]
     for kind, args, fname in jobs:

@@ -198,6 +198,35 @@ def test_type_constrained_link_prediction_matches_reference(path):
     np.testing.assert_allclose(np.array(got, dtype=np.float32), z["metrics"].astype(np.float32), rtol=1e-6)
 
 
+@pytest.mark.parametrize("path", golden("val_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_validator_matches_reference(path):
+    """openke.config.Validator.valid() (the static experiments' early-stopping check, Validator.py:35-44)
+    on the GPU == the reference's hit@10; the legacy validHead/validTail/getValidHit10 symbols agree."""
+    from openke.config import Validator
+    from openke.data import TestDataLoader
+    from openke.module.model import TransE, TransH
+    z = load(path)
+    valid_dl = TestDataLoader(KG_SMALL, "link", mode='valid')
+    cls = TransE if str(z["model"]) == "TransE" else TransH
+    kge = cls(ent_tot=valid_dl.get_ent_tot(), rel_tot=valid_dl.get_rel_tot(), dim=int(z["dim"]),
+              p_norm=int(z["p_norm"]), norm_flag=True)
+    with torch.no_grad():
+        kge.ent_embeddings.weight.copy_(torch.from_numpy(z["ent_embeddings"]))
+        kge.rel_embeddings.weight.copy_(torch.from_numpy(z["rel_embeddings"]))
+        if str(z["model"]) == "TransH":
+            kge.norm_vector.weight.copy_(torch.from_numpy(z["norm_vector"]))
+    validator = Validator(model=kge, data_loader=valid_dl)
+    assert validator.valid() == pytest.approx(float(z["hit10"]), rel=1e-6, abs=1e-7)
+    L = validator.lib
+    L.validInit()
+    for index, (dh, dt) in enumerate(valid_dl):
+        con = np.ascontiguousarray(validator.valid_one_step(dh), dtype=np.float32)
+        L.validHead(con.ctypes.data, index)
+        con = np.ascontiguousarray(validator.valid_one_step(dt), dtype=np.float32)
+        L.validTail(con.ctypes.data, index)
+    assert L.getValidHit10() == pytest.approx(float(z["hit10"]), rel=1e-6, abs=1e-7)
+
+
 @pytest.mark.parametrize("model,p,norm_flag", [("TransE", 1, True), ("TransE", 2, True), ("TransE", 2, False),
                                                ("TransH", 1, True), ("TransH", 2, True)])
 @pytest.mark.parametrize("dim", [8, 20, 50, 200, 300])
@@ -456,3 +485,72 @@ def test_fused_sample_sort_matches_two_pass_and_oracle(model, monkeypatch):
     for k in tf:
         np.testing.assert_allclose(tf[k], tt[k], atol=1e-4, rtol=0)
         np.testing.assert_allclose(tf[k], orc[k], atol=1e-4, rtol=0)
+
+
+def test_static_experiment_flow(tmp_path):
+    """The control flow of the reference's static experiments (experiments/static_experiment_TransE_on_WN18.py
+    :53-162) through the drop-in API: TrainDataLoader(nbatches=100) -> TransE -> NegativeSampling ->
+    Validator on the valid split -> Trainer.run() in rounds of valid_steps epochs with early stopping,
+    save_checkpoint + deepcopy of the best model -> Tester.run_link_prediction. Validation hit@10 and the
+    test metrics must equal the oracle's ranking of the GPU-trained tables."""
+    from copy import deepcopy
+
+    from openke.config import Tester, Trainer, Validator
+    from openke.data import TestDataLoader, TrainDataLoader
+    from openke.module.loss import MarginLoss
+    from openke.module.model import TransE
+    from openke.module.strategy import NegativeSampling
+    sys_test = __import__("test_oracle")
+    dl = TrainDataLoader(in_path=KG_SMALL, nbatches=100, threads=8, sampling_mode="normal", bern_flag=0,
+                         filter_flag=0, neg_ent=1, neg_rel=0, random_seed=12345)
+    torch.manual_seed(5)
+    transe = TransE(ent_tot=dl.get_ent_tot(), rel_tot=dl.get_rel_tot(), dim=16, p_norm=1, norm_flag=True)
+    model = NegativeSampling(model=transe, loss=MarginLoss(margin=4.0), batch_size=dl.get_batch_size())
+    valid_dl = TestDataLoader(dl.in_path, "link", mode='valid')
+    validator = Validator(model=transe, data_loader=valid_dl)
+    trainer = Trainer(model=model, data_loader=dl, alpha=0.01, train_times=2, use_gpu=True)
+    best, best_model, bad, hits, losses = 0, None, 0, [], []
+    for _ in range(3):
+        trainer.run()
+        losses.append(trainer.last_epoch_loss)
+        hit10 = validator.valid()
+        hits.append(hit10)
+        if hit10 > best:
+            best, bad = hit10, 0
+            best_model = deepcopy(transe)
+            transe.save_checkpoint(str(tmp_path / "transe.ckpt"))
+        else:
+            bad += 1
+    assert losses[-1] < losses[0], losses
+    # the last validation == the oracle's ranking of the same (GPU-trained) tables
+    kg = oracle.KG.load(KG_SMALL)
+    E = kg.ent_total
+    ent = transe.ent_embeddings.weight.detach().cpu().numpy()
+    rel = transe.rel_embeddings.weight.detach().cpu().numpy()
+    all_tr = [np.concatenate(x) for x in zip(*(oracle.read_triples(KG_SMALL + f)
+                                              for f in ("test2id.txt", "train2id.txt", "valid2id.txt")))]
+
+    def oracle_ranks(split):
+        ev = oracle.sort_test(*oracle.read_triples(KG_SMALL + split))
+        n = len(ev[0])
+        con_h = np.zeros((n, E), dtype=np.float32)
+        con_t = np.zeros((n, E), dtype=np.float32)
+        for q in range(n):
+            h, t, r = (int(x[q]) for x in ev)
+            con_h[q] = oracle.score("TransE", 1, True, "head_batch", ent, rel, None, oracle.candidates(E, h), [t],
+                                    [r])
+            con_t[q] = oracle.score("TransE", 1, True, "tail_batch", ent, rel, None, [h], oracle.candidates(E, t),
+                                    [r])
+        return oracle.link_prediction(E, all_tr, ev, con_h, con_t)
+
+    _, vr = oracle_ranks("valid2id.txt")
+    assert hits[-1] == pytest.approx(sys_test.valid_hit10(vr), rel=1e-6, abs=1e-7)
+    # checkpoint round trip and the test metrics of the final model
+    again = TransE(ent_tot=dl.get_ent_tot(), rel_tot=dl.get_rel_tot(), dim=16, p_norm=1, norm_flag=True)
+    again.load_checkpoint(str(tmp_path / "transe.ckpt"))
+    np.testing.assert_array_equal(again.ent_embeddings.weight.detach().cpu().numpy(),
+                                  best_model.ent_embeddings.weight.detach().cpu().numpy())
+    tester = Tester(model=transe, data_loader=TestDataLoader(KG_SMALL, "link", mode='test'), use_gpu=True)
+    res = tester.run_link_prediction(type_constrain=False)
+    met, _ = oracle_ranks("test2id.txt")
+    np.testing.assert_allclose(np.array(res, dtype=np.float32), met, rtol=1e-5, atol=1e-6)

@@ -200,3 +200,34 @@ def test_type_constrained_link_prediction_matches_reference(path):
     np.testing.assert_allclose(met_tc, z["metrics_tc"].astype(np.float32), rtol=1e-6, atol=1e-7)
     met, _ = oracle.link_prediction(E, all_tr, test, con_h, con_t)
     np.testing.assert_allclose(met, z["metrics"].astype(np.float32), rtol=1e-6, atol=1e-7)
+
+
+def valid_hit10(ranks):
+    """getValidHit10 (Valid.h:244-256) from filtered ranks: per side #{rank < 10} / validTotal, then mean."""
+    _, fh, _, ft = ranks
+    n = np.float32(len(fh))
+    return float((np.float32(np.count_nonzero(fh < 10)) / n + np.float32(np.count_nonzero(ft < 10)) / n)
+                 / np.float32(2))
+
+
+@pytest.mark.parametrize("path", golden("val_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_validator_hit10_matches_reference(path):
+    """Validator.valid() (validHead/validTail + getValidHit10 over the valid split) == the reference."""
+    z = load(path)
+    model, p = str(z["model"]), int(z["p_norm"])
+    kg = oracle.KG.load(KG_SMALL)
+    E = kg.ent_total
+    ent, rel = z["ent_embeddings"], z["rel_embeddings"]
+    nv = z["norm_vector"] if model == "TransH" else None
+    ev = oracle.sort_test(*oracle.read_triples(KG_SMALL + "valid2id.txt"))
+    all_tr = [np.concatenate(x) for x in zip(*(oracle.read_triples(KG_SMALL + f)
+                                              for f in ("test2id.txt", "train2id.txt", "valid2id.txt")))]
+    n = len(ev[0])
+    con_h = np.zeros((n, E), dtype=np.float32)
+    con_t = np.zeros((n, E), dtype=np.float32)
+    for q in range(n):
+        h, t, r = (int(x[q]) for x in ev)
+        con_h[q] = oracle.score(model, p, True, "head_batch", ent, rel, nv, oracle.candidates(E, h), [t], [r])
+        con_t[q] = oracle.score(model, p, True, "tail_batch", ent, rel, nv, [h], oracle.candidates(E, t), [r])
+    _, ranks = oracle.link_prediction(E, all_tr, ev, con_h, con_t)
+    assert valid_hit10(ranks) == pytest.approx(float(z["hit10"]), rel=1e-6, abs=1e-7)
