@@ -290,6 +290,14 @@ int64_t getTrainTotalUniverse(void);                 /* UniverseSetting.h:74-77 
 void getEntityRemapping(int64_t *ent_remapping);     /* UniverseSetting.h:79-84 */
 void getRelationRemapping(int64_t *rel_remapping);   /* UniverseSetting.h:86-91 */
 void swapHelpers(void);                              /* UniverseSetting.h:123-154 */
+/* neighbourhood getters (Base.cpp:312-466; bound at TrainDataLoader.py:60-101, used by
+ * get_positive_entities / get_negative_entities / get_entity_relations, :248-276) */
+int64_t getNumOfNegatives(int64_t entity, int64_t relation, int64_t entity_is_tail);
+int64_t getNumOfPositives(int64_t entity, int64_t relation, int64_t entity_is_tail);
+void getNegativeEntities(int64_t *out, int64_t entity, int64_t relation, int64_t entity_is_tail);
+void getPositiveEntities(int64_t *out, int64_t entity, int64_t relation, int64_t entity_is_tail);
+int64_t getNumOfEntityRelations(int64_t entity, int64_t entity_is_tail);
+void getEntityRelations(int64_t *out, int64_t entity, int64_t entity_is_tail);
 void resetUniverse(void);                            /* UniverseSetting.h:160-190 */
 void activateLoadOfAllTriples(int64_t flag);         /* Reader.h:241-244 */
 void importTestFiles(void);                          /* Reader.h:246-342 */

@@ -1448,6 +1448,69 @@ extern "C" void sampling(int64_t *bh, int64_t *bt, int64_t *br, float *by, int64
     (void)hipMemcpy(by, dy, sizeof(float) * seq, hipMemcpyDeviceToHost);
 }
 
+// Neighbourhood getters of TrainDataLoader.get_positive_entities / get_negative_entities /
+// get_entity_relations (Base.cpp:312-466) over the active graph (the swapped universe after swapHelpers):
+// `is_tail` != 0 scans the entity's run of the cmp_tail list (partners = heads), else its run of the
+// cmp_head list (partners = tails); positives are the partners under `relation`, negatives those under
+// any other relation, in list order.
+static const pt::Graph *legacy_graph_or_null(const char *who) {
+    const pt::Graph *g = L().active();
+    if (!g) pt::fail(PT_ESTATE, std::string(who) + " before importTrainFiles");
+    return g;
+}
+static int64_t legacy_partners(int64_t entity, int64_t relation, int64_t is_tail, bool positive, int64_t *out) {
+    const pt::Graph *g = legacy_graph_or_null("entity neighbourhood getter");
+    if (!g || entity < 0 || entity >= g->ent_total) return 0;
+    const auto &lst = is_tail ? g->tail : g->head;
+    const int64_t lo = is_tail ? g->lef_tail[(size_t)entity] : g->lef_head[(size_t)entity];
+    const int64_t hi = is_tail ? g->rig_tail[(size_t)entity] : g->rig_head[(size_t)entity];
+    int64_t n = 0;
+    for (int64_t i = lo; i <= hi; ++i) {
+        const pt::Triple &x = lst[(size_t)i];
+        if ((x.r == relation) == positive) {
+            if (out) out[n] = is_tail ? x.h : x.t;
+            ++n;
+        }
+    }
+    return n;
+}
+extern "C" int64_t getNumOfNegatives(int64_t entity, int64_t relation, int64_t is_tail) {
+    return legacy_partners(entity, relation, is_tail, false, nullptr);
+}
+extern "C" int64_t getNumOfPositives(int64_t entity, int64_t relation, int64_t is_tail) {
+    return legacy_partners(entity, relation, is_tail, true, nullptr);
+}
+extern "C" void getNegativeEntities(int64_t *out, int64_t entity, int64_t relation, int64_t is_tail) {
+    legacy_partners(entity, relation, is_tail, false, out);
+}
+extern "C" void getPositiveEntities(int64_t *out, int64_t entity, int64_t relation, int64_t is_tail) {
+    legacy_partners(entity, relation, is_tail, true, out);
+}
+static int64_t legacy_entity_relations(int64_t entity, int64_t is_tail, int64_t *out) {
+    const pt::Graph *g = legacy_graph_or_null("getEntityRelations");
+    if (!g || entity < 0 || entity >= g->ent_total) return 0;
+    const auto &lst = is_tail ? g->tail : g->head;
+    const int64_t lo = is_tail ? g->lef_tail[(size_t)entity] : g->lef_head[(size_t)entity];
+    const int64_t hi = is_tail ? g->rig_tail[(size_t)entity] : g->rig_head[(size_t)entity];
+    int64_t n = 0, cur = -1;
+    for (int64_t i = lo; i <= hi; ++i) {
+        if (lst[(size_t)i].r != cur) {
+            cur = lst[(size_t)i].r;
+            // the reference never advances its output index (Base.cpp:442-466): every distinct relation
+            // lands in out[0], so out[0] ends as the last one and the rest of the buffer is untouched
+            if (out) out[0] = cur;
+            ++n;
+        }
+    }
+    return n;
+}
+extern "C" int64_t getNumOfEntityRelations(int64_t entity, int64_t is_tail) {
+    return legacy_entity_relations(entity, is_tail, nullptr);
+}
+extern "C" void getEntityRelations(int64_t *out, int64_t entity, int64_t is_tail) {
+    legacy_entity_relations(entity, is_tail, out);
+}
+
 extern "C" int64_t pt_legacy_bern(void) { return L().bern; }
 
 // the global context's test / valid lists in the reference's ranking order (cmp_rel2, Reader.h:311-312)

@@ -140,6 +140,12 @@ SIGNATURES = {
     "activateLoadOfAllTriples": (None, [c_i64]),
     "importTestFiles": (None, []),
     "importTypeFiles": (None, []),
+    "getNumOfNegatives": (c_i64, [c_i64, c_i64, c_i64]),
+    "getNumOfPositives": (c_i64, [c_i64, c_i64, c_i64]),
+    "getNegativeEntities": (None, [c_vp, c_i64, c_i64, c_i64]),
+    "getPositiveEntities": (None, [c_vp, c_i64, c_i64, c_i64]),
+    "getNumOfEntityRelations": (c_i64, [c_i64, c_i64]),
+    "getEntityRelations": (None, [c_vp, c_i64, c_i64]),
     "initTest": (None, []),
     "getHeadBatch": (None, [c_vp, c_vp, c_vp]),
     "getTailBatch": (None, [c_vp, c_vp, c_vp]),

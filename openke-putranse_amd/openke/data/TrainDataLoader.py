@@ -142,6 +142,32 @@ class TrainDataLoader(object):
             return self.sampling_head()
         return self.sampling_tail()
 
+    def get_positive_entities(self, entity, relation, entity_is_head):
+        """TrainDataLoader.py:248-255 (Base.cpp:337-403): partners of `entity` under `relation`; the flag
+        is passed to the library's `entity_is_tail` argument unchanged, as the reference does."""
+        num_of_pos = self.lib.getNumOfPositives(entity, relation, entity_is_head)
+        batch_pos_entities = np.zeros(num_of_pos, dtype=np.int64)
+        self.lib.getPositiveEntities(batch_pos_entities.__array_interface__["data"][0], entity, relation,
+                                     entity_is_head)
+        return batch_pos_entities
+
+    def get_negative_entities(self, entity, relation, entity_is_head):
+        """TrainDataLoader.py:257-266 (Base.cpp:312-380): partners of `entity` under other relations."""
+        num_of_neg = self.lib.getNumOfNegatives(entity, relation, entity_is_head)
+        batch_neg_entities = np.zeros(num_of_neg, dtype=np.int64)
+        if num_of_neg != 0:
+            self.lib.getNegativeEntities(batch_neg_entities.__array_interface__["data"][0], entity, relation,
+                                         entity_is_head)
+        return batch_neg_entities
+
+    def get_entity_relations(self, entity, entity_is_tail):
+        """TrainDataLoader.py:268-276 (Base.cpp:405-466); keeps the reference's output (only the first
+        element is written, with the entity's last distinct relation)."""
+        num_of_rel = self.lib.getNumOfEntityRelations(entity, entity_is_tail)
+        batch_entity_relations = np.zeros(num_of_rel, dtype=np.int64)
+        self.lib.getEntityRelations(batch_entity_relations.__array_interface__["data"][0], entity, entity_is_tail)
+        return batch_entity_relations
+
     def device_sampler(self):
         """Handle of the GPU sampler that produces exactly the batches sampling() would return next."""
         s = self.lib.pt_legacy_sampler()

@@ -96,6 +96,14 @@ VAL_CASES = [
     ("v2", "TransH", 8, 2, 26),
 ]
 
+NBR_CASES = [
+    # TrainDataLoader.get_positive_entities / get_negative_entities / get_entity_relations (Base.cpp:312-466),
+    # on the full graph and after swap_helpers onto a universe
+    # name, seed, universe (tc, balance) or None
+    ("n1", 3, None),
+    ("n2", 8, [300, 0.3]),
+]
+
 TC_CASES = [
     # name, model, dim, p_norm, torch_seed
     ("c1", "TransE", 16, 1, 31),
@@ -354,6 +362,24 @@ def case_val(out, name, model, dim, p, tseed):
     np.savez_compressed(out, model=model, dim=dim, p_norm=p, torch_seed=tseed, hit10=float(hit10), **tables)
 
 
+def case_nbr(out, name, seed, uni):
+    from openke.data import TrainDataLoader
+    dl = TrainDataLoader(in_path=DATASETS["small"], batch_size=50, threads=8, sampling_mode="normal", bern_flag=0,
+                         filter_flag=0, neg_ent=1, neg_rel=0, random_seed=seed)
+    if uni is not None:
+        dl.compile_universe_dataset(uni[0], uni[1])
+        dl.swap_helpers()
+    E, R = dl.lib.getEntityTotal(), dl.lib.getRelationTotal()
+    rng = np.random.default_rng(seed)
+    queries = [(int(rng.integers(0, E)), int(rng.integers(0, R)), int(rng.integers(0, 2))) for _ in range(40)]
+    rec = {"queries": np.array(queries, dtype=np.int64), "ent_total": E, "rel_total": R}
+    for i, (e, r, f) in enumerate(queries):
+        rec["pos_%d" % i] = dl.get_positive_entities(e, r, f)
+        rec["neg_%d" % i] = dl.get_negative_entities(e, r, f)
+        rec["rels_%d" % i] = dl.get_entity_relations(e, f)
+    np.savez_compressed(out, seed=seed, universe=np.array(uni if uni is not None else [], dtype=np.float64), **rec)
+
+
 def case_tc(out, name, model, dim, p, tseed):
     """Tester.run_triple_classification on a random-init model (Tester.py:142-191), then one more
     getTestBatch call of the same loader (the negatives continue the thread-0 stream)."""
@@ -381,7 +407,7 @@ def run_case(kind, args_json, out, tmp):
     _import_reference(tmp)
     _silence()
     {"glibc": case_glibc, "sampler": case_sampler, "sampler_mode": case_sampler_mode, "train": case_train, "universes": case_universes,
-     "lp": case_lp, "lpt": case_lpt, "val": case_val, "tc": case_tc}[kind](out, *args)
+     "lp": case_lp, "lpt": case_lpt, "val": case_val, "nbr": case_nbr, "tc": case_tc}[kind](out, *args)
 
 
 def main():
@@ -400,6 +426,7 @@ def main():
     jobs += [("lp", list(c), "lp_%s.npz" % c[0]) for c in LP_CASES]
     jobs += [("lpt", list(c), "lpt_%s.npz" % c[0]) for c in LPT_CASES]
     jobs += [("val", list(c), "val_%s.npz" % c[0]) for c in VAL_CASES]
+    jobs += [("nbr", list(c), "nbr_%s.npz" % c[0]) for c in NBR_CASES]
     jobs += [("tc", list(c), "tc_%s.npz" % c[0]) for c in TC_CASES]
     only = sys.argv[1:]
     for kind, args, fname in jobs:

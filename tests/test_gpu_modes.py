@@ -136,3 +136,22 @@ def test_train_one_step_on_cross_batch(mode):
     got = _tables(kge)
     np.testing.assert_allclose(got[0], ent, rtol=0, atol=2e-6)
     np.testing.assert_allclose(got[1], rel, rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("path", golden("nbr_*.npz"), ids=lambda p: p.split("/")[-1])
+def test_neighbourhood_getters_match_reference(path):
+    """TrainDataLoader.get_positive_entities / get_negative_entities / get_entity_relations (Base.cpp:312-466)
+    on the full graph and on a swapped-in universe == the reference's outputs."""
+    z = load(path)
+    dl = _loader("small", 8, 50, 1, 0, 0, 0, int(z["seed"]), mode="normal")
+    uni = z["universe"]
+    if len(uni):
+        dl.compile_universe_dataset(int(uni[0]), float(uni[1]))
+        dl.swap_helpers()
+    assert dl.lib.getEntityTotal() == int(z["ent_total"]) and dl.lib.getRelationTotal() == int(z["rel_total"])
+    for i, (e, r, f) in enumerate(z["queries"]):
+        np.testing.assert_array_equal(dl.get_positive_entities(int(e), int(r), int(f)), z["pos_%d" % i])
+        np.testing.assert_array_equal(dl.get_negative_entities(int(e), int(r), int(f)), z["neg_%d" % i])
+        np.testing.assert_array_equal(dl.get_entity_relations(int(e), int(f)), z["rels_%d" % i])
+    if len(uni):
+        dl.reset_universe()
