@@ -434,11 +434,7 @@ class Parallel_Universe_Config(Tester):
                     L.pt_universe_free(handles[i])
         return recs
 
-    def add_universe(self, embedding_space, ent_remap, rel_remap):
-        """Register a trained universe as id next_universe_id: add_embedding_space +
-        process_universe_mappings (:179-207) from its local -> global entity / relation maps.
-        embedding_space is None for a universe trained on another rank."""
-        uid = self.next_universe_id
+    def _register_maps(self, uid, ent_remap, rel_remap):
         em = np.ascontiguousarray(ent_remap, dtype=np.int64)
         rm = np.ascontiguousarray(rel_remap, dtype=np.int64)
         emap = self.entity_id_mappings[uid]
@@ -449,11 +445,74 @@ class Parallel_Universe_Config(Tester):
         for local, g in enumerate(rm.tolist()):
             self.relation_universes[g].add(uid)
             rmap[g] = local
+        self._remap_cache[uid] = self._remaps_from_arrays(em, rm)
+
+    def add_universe(self, embedding_space, ent_remap, rel_remap):
+        """Register a trained universe as id next_universe_id: add_embedding_space +
+        process_universe_mappings (:179-207) from its local -> global entity / relation maps.
+        embedding_space is None for a universe trained on another rank."""
+        uid = self.next_universe_id
+        self._register_maps(uid, ent_remap, rel_remap)
         if embedding_space is not None:
             self.add_embedding_space(embedding_space)
-        self._remap_cache[uid] = self._remaps_from_arrays(em, rm)
         self.next_universe_id += 1
         return uid
+
+    # ---------------------------------------------------- the reference's one-universe protocol --
+    # train_parallel_universes builds and trains whole waves of universes in one GPU launch; these are
+    # the reference's per-universe steps (:195-258) for callers that drive one universe at a time:
+    #     set_random_seed(seed0 + k); compile_train_datset(); sp = train_embedding_space();
+    #     add_embedding_space(sp); next_universe_id += 1
+    # They use the Base.so-compatible global context (getParallelUniverse / swapHelpers / resetUniverse
+    # in the library) and the fused single-model trainer on the swapped-in universe graph.
+    def process_universe_mappings(self):
+        """:195-207: the compiled universe's local -> global maps under next_universe_id."""
+        em, rm = self.train_dataloader.get_universe_mappings()
+        print('Entities are %d' % len(em))
+        self._register_maps(self.next_universe_id, em, rm)
+
+    def compile_train_datset(self):
+        """:209-226: draw the triple constraint and balance, build the universe (getParallelUniverse)."""
+        triple_constraint = randrange(self.min_triple_constraint, self.max_triple_constraint)
+        balance_param = round(uniform(self.min_balance, self.max_balance), 2)
+        print('universe information-------------------')
+        print('--- num of training triples: %d' % triple_constraint)
+        self.train_dataloader.compile_universe_dataset(triple_constraint, balance_param)
+        self.process_universe_mappings()
+        lib = self.train_dataloader.lib
+        print('--- num of universe entities: %d' % lib.getEntityTotalUniverse())
+        print('--- num of universe relations: %d' % lib.getRelationTotalUniverse())
+        print('---------------------------------------')
+        print('Train dataset for embedding space compiled.')
+
+    def train_embedding_space(self):
+        """:228-258: margin / epochs / lr draws, the model factory and an Adagrad Trainer run over the
+        swapped-in universe (the fused GPU epoch on the library's sampler, whose graph follows swapHelpers)."""
+        from .Trainer import Trainer
+        self._check_setup()
+        lib = self.train_dataloader.lib
+        entity_total_universe = lib.getEntityTotalUniverse()
+        relation_total_universe = lib.getRelationTotalUniverse()
+        train_total_universe = lib.getTrainTotalUniverse()
+        margin = randrange(self.min_margin, self.max_margin)
+        model = self.embedding_model_factory(ent_tot=entity_total_universe, rel_tot=relation_total_universe,
+                                             margin=margin)
+        train_times = self.const_num_epochs if self.const_num_epochs is not None \
+            else randrange(self.min_num_epochs, self.max_num_epochs)
+        lr = round(uniform(self.min_lr, self.max_lr), len(str(self.min_lr).split('.')[1]))
+        trainer = Trainer(model=model, data_loader=self.train_dataloader, train_times=train_times, alpha=lr,
+                          use_gpu=True, opt_method='Adagrad')
+        print('hyperparams for universe %d------------' % self.next_universe_id)
+        print('--- epochs: %d' % train_times)
+        print('--- learning rate:', lr)
+        print('--- margin: %d' % margin)
+        self.train_dataloader.swap_helpers()
+        trainer.run()
+        self.train_dataloader.reset_universe()
+        self.universe_hparams[self.next_universe_id] = {
+            "tc": None, "balance": None, "margin": margin, "epochs": train_times, "lr": lr,
+            "batch_size": model.batch_size, "train_total": train_total_universe}
+        return model.model
 
     def _commit(self, rec):
         assert rec["id"] == self.next_universe_id

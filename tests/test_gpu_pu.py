@@ -375,3 +375,50 @@ def test_pu_type_constrained_ranks_match_oracle(path, tmp_path):
     mism += _assert_ranks_match(pu.last_tc_ranks, ranks_tc, con_h, con_t)
     if mism == 0:
         np.testing.assert_allclose(np.array(res, dtype=np.float32), met_tc, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("path", golden("universes_u*.npz")[:2], ids=lambda p: p.split("/")[-1])
+def test_pu_one_universe_protocol_matches_reference(path, tmp_path):
+    """The reference's per-universe protocol driven by hand (Parallel_Universe_Config.py:320-327):
+    set_random_seed -> compile_train_datset (getParallelUniverse + process_universe_mappings) ->
+    train_embedding_space (Adagrad Trainer on the swapped-in universe) -> add_embedding_space. Maps,
+    hyperparameters and trained tables == the reference's goldens (as test_pu_training_matches_reference)."""
+    z = load(path)
+    model, dim, p = str(z["model"]), int(z["dim"]), int(z["p_norm"])
+    n_univ = int(z["n_univ"])
+    pu = _pu(z, tmp_path)
+    for _ in range(n_univ):
+        pu.set_random_seed(pu.initial_random_seed + pu.next_universe_id)
+        pu.compile_train_datset()
+        sp = pu.train_embedding_space()
+        pu.add_embedding_space(sp)
+        pu.next_universe_id += 1
+    kg = oracle.KG.load(KG_SMALL)
+    noisy = []
+    for u in range(n_univ):
+        hp = pu.universe_hparams[u]
+        assert hp["margin"] == int(z["u%d_margin" % u])
+        assert abs(hp["lr"] - float(z["u%d_lr" % u])) < 1e-12
+        assert hp["train_total"] == int(z["u%d_train_total" % u])
+        em, rm = pu._remaps(u)[:2]
+        np.testing.assert_array_equal(em, z["u%d_ent_remap" % u])
+        np.testing.assert_array_equal(rm, z["u%d_rel_remap" % u])
+        sp = pu.trained_embedding_spaces[u]
+        ours = {"ent": sp.ent_embeddings.weight.detach().cpu().numpy(),
+                "rel": sp.rel_embeddings.weight.detach().cpu().numpy()}
+        if model == "TransH":
+            ours["norm"] = sp.norm_vector.weight.detach().cpu().numpy()
+        ent, rel, nv, events = _oracle_universe(kg, z, u, model, p, dim)
+        orc = {"ent": ent, "rel": rel, "norm": nv}
+        if events == 0:
+            for name in ours:
+                assert_close_vs_oracle(ours[name], z["u%d_%s" % (u, name)], orc[name], atol=2e-5)
+        else:
+            noisy.append(u)
+            for name in ours:
+                ref = z["u%d_%s" % (u, name)]
+                assert np.abs(ours[name] - ref).mean() <= 3 * np.abs(orc[name] - ref).mean() + 1e-4
+    assert len(noisy) <= n_univ // 2, noisy
+    # the universes feed link prediction like train_parallel_universes' do
+    mrr, mr, hit10, hit3, hit1 = pu.run_link_prediction()
+    assert np.isfinite([mrr, mr, hit10, hit3, hit1]).all()
