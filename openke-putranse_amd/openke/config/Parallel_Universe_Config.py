@@ -716,8 +716,112 @@ class Parallel_Universe_Config(Tester):
                 scores = st.rows[k].index_select(0, torch.from_numpy(ents).to(st.rows.device)).cpu().numpy()
                 repl = float(st.tuple[k].item())
                 break
+        # scores MINed in by hand through obtain_embedding_space_score (the reference's dictionaries)
+        key = get_string_key(anchor, rel)
+        row = (self.evaluation_tail2head_triple_score_dict if side == 0
+               else self.evaluation_head2tail_triple_score_dict).get(key)
+        if row is not None:
+            scores = np.minimum(scores, row[ents])
+        t = (self.evaluation_tail2rel_tuple_score_dict if side == 0
+             else self.evaluation_head2rel_tuple_score_dict).get(key)
+        if t is not None and t < repl:
+            repl = t
         if self.missing_embedding_handling == 'null_vector' and repl != float("inf"):
             scores[scores == np.inf] = repl
+        return scores
+
+    # ------------------------------------------- the reference's per-(key, universe) internals ----
+    # eval_universes scores every (key, universe) pair of a split in two GPU launches into device key rows
+    # (k_lp_bases / k_lp_scan). These are the reference's one-pair steps (:446-543), kept for callers that
+    # drive them directly: the universe's scores come from one GPU predict, and the MIN goes into the
+    # reference's score dictionaries (rows of entTotal floats, +inf default), which
+    # global_energy_estimation reads together with the device rows.
+    def _universe_key_scores(self, data, universe_id):
+        """(global entity ids, scores) of every entity of universe `universe_id` as the missing side of
+        data's key, in the universe's local id order (the reference's mapping order)."""
+        mode = data['mode']
+        mapping = self.entity_id_mappings[universe_id]
+        rmap = self.relation_id_mappings[universe_id]
+        sp = self.trained_embedding_spaces[universe_id]
+        glob = np.fromiter(mapping.keys(), dtype=np.int64, count=len(mapping))
+        loc = np.fromiter(mapping.values(), dtype=np.int64, count=len(mapping))
+        anchor = [mapping[int(g)] for g in (data['batch_t'] if mode == 'head_batch' else data['batch_h'])]
+        rel = [rmap[int(g)] for g in data['batch_r']]
+        batch = {"batch_h": loc if mode == 'head_batch' else np.asarray(anchor, dtype=np.int64),
+                 "batch_t": np.asarray(anchor, dtype=np.int64) if mode == 'head_batch' else loc,
+                 "batch_r": np.asarray(rel, dtype=np.int64), "mode": mode}
+        scores = np.asarray(sp.predict(batch), dtype=np.float32).reshape(-1)
+        return glob, loc, scores
+
+    def transmit_max_scores(self, data, embedding_space_mapping, scores):
+        """:446-469: MIN a universe's scores (indexed by local id) into the key's global score row."""
+        mode = data['mode']
+        eval_rel_id = int(data['batch_r'][0])
+        if mode == 'head_batch':
+            eval_entity_id, score_dict = int(data['batch_t'][0]), self.evaluation_tail2head_triple_score_dict
+        elif mode == 'tail_batch':
+            eval_entity_id, score_dict = int(data['batch_h'][0]), self.evaluation_head2tail_triple_score_dict
+        else:
+            raise ValueError("transmit_max_scores needs head_batch / tail_batch data")
+        row = score_dict.setdefault(get_string_key(eval_entity_id, eval_rel_id),
+                                    np.full(self.ent_tot, np.inf, dtype=np.float32))
+        glob = np.fromiter(embedding_space_mapping.keys(), dtype=np.int64, count=len(embedding_space_mapping))
+        loc = np.fromiter(embedding_space_mapping.values(), dtype=np.int64, count=len(embedding_space_mapping))
+        sc = np.asarray(scores.cpu().numpy() if isinstance(scores, torch.Tensor) else scores,
+                        dtype=np.float32).reshape(-1)
+        row[glob] = np.minimum(row[glob], sc[loc])
+
+    def transmit_tuple_max_score(self, data, universe_id):
+        """:494-512: MIN the universe's null-vector tuple score of the key into the tuple dictionary."""
+        mode = data['mode']
+        eval_rel_id = int(data['batch_r'][0])
+        if mode == 'head_batch':
+            eval_entity_id, score_dict = int(data['batch_t'][0]), self.evaluation_tail2rel_tuple_score_dict
+        elif mode == 'tail_batch':
+            eval_entity_id, score_dict = int(data['batch_h'][0]), self.evaluation_head2rel_tuple_score_dict
+        else:
+            raise ValueError("transmit_tuple_max_score needs head_batch / tail_batch data")
+        key = get_string_key(eval_entity_id, eval_rel_id)
+        sp = self.trained_embedding_spaces[universe_id]
+        s = float(self.calc_tuple_score(self.entity_id_mappings[universe_id][eval_entity_id],
+                                        self.relation_id_mappings[universe_id][eval_rel_id], mode,
+                                        sp).reshape(-1)[0])
+        if s < score_dict.get(key, float("inf")):
+            score_dict[key] = s
+
+    def obtain_embedding_space_score(self, data, universe_id):
+        """:514-540: universe `universe_id`'s scores for data's key, MINed into the score dictionaries."""
+        glob, loc, scores = self._universe_key_scores(data, universe_id)
+        full = np.full(len(loc), np.inf, dtype=np.float32)
+        full[loc] = scores
+        self.transmit_max_scores(data, self.entity_id_mappings[universe_id], full)
+        self.transmit_tuple_max_score(data, universe_id)
+
+    def global_energy_estimation2(self, data):
+        """:644-701: the key's candidate scores computed on the fly over the universes holding the anchor
+        and the relation (no dictionaries), null-vector replacement included; scores in batch order."""
+        mode = data['mode']
+        bh, bt, br = (np.asarray(data[k].cpu().numpy() if isinstance(data[k], torch.Tensor) else data[k])
+                      for k in ('batch_h', 'batch_t', 'batch_r'))
+        anchor = int(bt[0] if mode == 'head_batch' else bh[0])
+        rel = int(br[0])
+        ents = np.asarray(bh if mode == 'head_batch' else bt, dtype=np.int64)
+        row = np.full(self.ent_tot, np.inf, dtype=np.float32)
+        tuple_score = float("inf")
+        for u in self.gather_embedding_spaces(anchor, rel):
+            if u not in self.trained_embedding_spaces:
+                continue
+            glob, loc, scores = self._universe_key_scores(
+                {"batch_h": [anchor] if mode == 'tail_batch' else bh[:1], "batch_t": [anchor] if mode == 'head_batch'
+                 else bt[:1], "batch_r": [rel], "mode": mode}, u)
+            row[glob] = np.minimum(row[glob], scores)
+            if self.missing_embedding_handling == 'null_vector':
+                s = float(self.calc_tuple_score(self.entity_id_mappings[u][anchor], self.relation_id_mappings[u][rel],
+                                                mode, self.trained_embedding_spaces[u]).reshape(-1)[0])
+                tuple_score = s if s < tuple_score else tuple_score
+        scores = row[ents]
+        if self.missing_embedding_handling == 'null_vector' and tuple_score != float("inf"):
+            scores[scores == np.inf] = tuple_score
         return scores
 
     def test_one_step(self, data):

@@ -422,3 +422,36 @@ def test_pu_one_universe_protocol_matches_reference(path, tmp_path):
     # the universes feed link prediction like train_parallel_universes' do
     mrr, mr, hit10, hit3, hit1 = pu.run_link_prediction()
     assert np.isfinite([mrr, mr, hit10, hit3, hit1]).all()
+
+
+@pytest.mark.parametrize("missing", ["last_rank", "null_vector"])
+def test_pu_per_key_internals_match_device_rows(missing, tmp_path):
+    """The reference's per-(key, universe) steps (obtain_embedding_space_score -> transmit_max_scores /
+    transmit_tuple_max_score, :446-540, driven as eval_universes drives them, :556-603) and
+    global_energy_estimation2 (:644-701) give the candidate vectors the batched device path gives
+    (eval_universes -> k_lp_scan key rows -> global_energy_estimation)."""
+    z = load(golden("universes_u1.npz")[0])
+    dev_pu = _pu(z, tmp_path, missing=missing)
+    _inject_reference_universes(dev_pu, z)
+    dev_pu.data_loader.set_sampling_mode('link')
+    dev_pu.eval_universes(eval_mode='test')
+    man_pu = _pu(z, tmp_path, missing=missing)
+    _inject_reference_universes(man_pu, z)
+    man_pu.data_loader.set_sampling_mode('link')
+    datas = []
+    for index, (data_head, data_tail) in enumerate(man_pu.data_loader):
+        if index >= 25:
+            break
+        datas.append((data_head, data_tail))
+        head, rel, tail = int(data_tail['batch_h'][0]), int(data_head['batch_r'][0]), int(data_head['batch_t'][0])
+        for u in range(man_pu.next_universe_id):
+            if u in man_pu.entity_universes[head] and u in man_pu.relation_universes[rel]:
+                man_pu.obtain_embedding_space_score(data_tail, u)
+            if u in man_pu.entity_universes[tail] and u in man_pu.relation_universes[rel]:
+                man_pu.obtain_embedding_space_score(data_head, u)
+    assert man_pu.evaluation_head2tail_triple_score_dict and man_pu.evaluation_tail2head_triple_score_dict
+    for data_head, data_tail in datas:
+        for d in (data_head, data_tail):
+            want = dev_pu.global_energy_estimation(d)
+            np.testing.assert_allclose(man_pu.global_energy_estimation(d), want, rtol=1e-6, atol=1e-6)
+            np.testing.assert_allclose(man_pu.global_energy_estimation2(d), want, rtol=1e-6, atol=1e-6)
