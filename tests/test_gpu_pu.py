@@ -442,6 +442,9 @@ def test_pu_per_key_internals_match_device_rows(missing, tmp_path):
     for index, (data_head, data_tail) in enumerate(man_pu.data_loader):
         if index >= 25:
             break
+        # the loader hands out views of buffers its next call overwrites (TestDataLoader.sampling_lp)
+        data_head, data_tail = ({k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in d.items()}
+                                for d in (data_head, data_tail))
         datas.append((data_head, data_tail))
         head, rel, tail = int(data_tail['batch_h'][0]), int(data_head['batch_r'][0]), int(data_head['batch_t'][0])
         for u in range(man_pu.next_universe_id):
