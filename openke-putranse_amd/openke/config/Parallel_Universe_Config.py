@@ -901,10 +901,54 @@ class Parallel_Universe_Config(Tester):
         return mrr, mr, hit10, hit3, hit1
 
     def run_triple_classification(self, threshlod=None):
-        # Parallel_Universe_Config.py:745-749 (the static split; the incremental-file variants are outside
-        # the accelerated path)
+        # Parallel_Universe_Config.py:745-749 (the test split, negatives from getTestBatch)
         acc, threshlod = super().run_triple_classification(threshlod)
         print("Accuracy is: {}".format(acc))
+        return acc, threshlod
+
+    # file-driven triple classification (:751-818): labelled `h t r truth` files of a snapshot folder
+    # `<in_path>/incremental/<snapshot>/`, scored by the same GPU predicts as the test split
+    def tc_datastructure_adapter(self, pos_h, pos_t, pos_r, neg_h, neg_t, neg_r):
+        """:753-765: one (positives, negatives) pair in the shape Tester.run_triple_classification iterates."""
+        def arr(x):
+            return np.asarray(x, dtype=np.int64) if len(x) else np.empty(0, dtype=np.int64)
+        return [({'batch_h': arr(pos_h), 'batch_t': arr(pos_t), 'batch_r': arr(pos_r), "mode": "normal"},
+                 {'batch_h': arr(neg_h), 'batch_t': arr(neg_t), 'batch_r': arr(neg_r), "mode": "normal"})]
+
+    def load_triple_classification_file(self, file):
+        """:767-789: `head tail rel truth_value` lines; truth 1 = positive, 0 = negative, others skipped."""
+        pos, neg = ([], [], []), ([], [], [])
+        with open(str(file), "rt", encoding="UTF-8") as f:
+            for line in f:
+                head, tail, rel, truth_value = line.split()
+                dst = pos if truth_value == "1" else (neg if truth_value == "0" else None)
+                if dst is not None:
+                    dst[0].append(int(head))
+                    dst[1].append(int(tail))
+                    dst[2].append(int(rel))
+        return pos[0], pos[1], pos[2], neg[0], neg[1], neg[2]
+
+    def run_classification_of_deleted_triples(self, snapshot_idx, threshlod):
+        """:791-800: accuracy at `threshlod` on every `tc_*` file of the snapshot folder."""
+        folder = os.path.join(self.data_loader.in_path, "incremental", str(snapshot_idx))
+        for name in sorted(os.listdir(folder)):
+            if not name.startswith("tc_"):
+                continue
+            tc_data = self.tc_datastructure_adapter(*self.load_triple_classification_file(os.path.join(folder, name)))
+            acc, _ = Tester.run_triple_classification(self, threshlod, data_iterator=tc_data)
+            print("Accuracy for {} is: {}".format(name, acc))
+
+    def run_triple_classification_from_files(self, snapshot):
+        """:802-815: threshold and accuracy on the snapshot's prepared test examples, then the deleted-triple
+        files at that threshold."""
+        folder = os.path.join(self.data_loader.in_path, "incremental", str(snapshot))
+        name = "triple_classification_prepared_test_examples.txt"
+        tc_data = self.tc_datastructure_adapter(*self.load_triple_classification_file(os.path.join(folder, name)))
+        acc, threshlod = Tester.run_triple_classification(self, data_iterator=tc_data)
+        print("Accuracy for {} is: {}".format(name, acc))
+        print("Determined threshold: {}".format(threshlod))
+        print("Run negative triple classification...")
+        self.run_classification_of_deleted_triples(snapshot, threshlod)
         return acc, threshlod
 
     def reset_evaluation_helpers(self):

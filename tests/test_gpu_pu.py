@@ -356,6 +356,37 @@ def test_pu_triple_classification_matches_reference(path, tmp_path):
 
 
 @pytest.mark.parametrize("path", golden("universes_u*.npz")[:2], ids=lambda p: p.split("/")[-1])
+def test_pu_triple_classification_from_files_matches_reference(path, tmp_path):
+    """run_triple_classification_from_files (:802-815): the same positives and negatives written as a
+    snapshot's labelled file give the reference's accuracy and threshold (those of the golden run);
+    the deleted-triple files are classified at that threshold."""
+    import os
+    z = load(path)
+    pu = _pu(z, tmp_path)
+    _inject_reference_universes(pu, z)
+    pu.set_random_seed(4321)
+    pu.data_loader.set_sampling_mode('classification')
+    pos, neg = next(iter(pu.data_loader))
+    snap = tmp_path / "incremental" / "0"
+    os.makedirs(str(snap))
+    with open(str(snap / "triple_classification_prepared_test_examples.txt"), "w") as f:
+        for d, truth in ((pos, 1), (neg, 0)):
+            for h, t, r in zip(d["batch_h"], d["batch_t"], d["batch_r"]):
+                f.write("%d %d %d %d\n" % (h, t, r, truth))
+    with open(str(snap / "tc_deleted.txt"), "w") as f:
+        for h, t, r in zip(neg["batch_h"][:10], neg["batch_t"][:10], neg["batch_r"][:10]):
+            f.write("%d %d %d 0\n" % (h, t, r))
+    pu.data_loader.in_path = str(tmp_path) + "/"
+    acc, thr = pu.run_triple_classification_from_files(0)
+    assert acc == float(z["tc_acc"]), (acc, float(z["tc_acc"]))
+    want = float(z["tc_threshold"])
+    if np.isinf(want) or np.isnan(want):
+        assert (thr is None and np.isnan(want)) or float(thr) == want, (thr, want)
+    else:
+        np.testing.assert_allclose(float(thr), want, rtol=1e-5)
+
+
+@pytest.mark.parametrize("path", golden("universes_u*.npz")[:2], ids=lambda p: p.split("/")[-1])
 def test_pu_type_constrained_ranks_match_oracle(path, tmp_path):
     """run_link_prediction(type_constrain=True): constrained ranks on the GPU (k_rank_types) == the
     oracle's literal restatement of testHead/testTail's constrained branch (Test.h:127-502, pinned to the
