@@ -27,7 +27,9 @@ class Validator(Tester):
         dl = self.valid_dataloader
         h, t, r = dl.eval_triples()
         n = np.float32(max(len(h), 1))
-        _, fh, _, ft = self._rank_all(h, t, r, dl.get_ent_tot())
+        ranks = self._rank_all(h, t, r, dl.get_ent_tot())
+        self.last_ranks = tuple(ranks[:4])
+        _, fh, _, ft = self.last_ranks
         l_tot = np.float32(np.count_nonzero(fh < 10)) / n
         r_tot = np.float32(np.count_nonzero(ft < 10)) / n
         return float((l_tot + r_tot) / np.float32(2))

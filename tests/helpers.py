@@ -137,3 +137,19 @@ def assert_close_vs_oracle(ours, ref, orc, atol=1e-5, factor=10.0):
     bound = np.maximum(atol, factor * np.abs(orc - ref))
     bad = err > bound
     assert not bad.any(), "max err %g (bound %g) at %d entries" % (err[bad].max(), bound[bad].min(), bad.sum())
+
+
+def assert_ranks_match(ours, ref_ranks, con_h, con_t, rel_tol=1e-6):
+    """Per-query ranks (raw/filtered head, raw/filtered tail) equal, except where the truth's score is
+    within float rounding of competing candidates' in the oracle's candidate-order vectors (summation
+    order decides such near-ties): there a rank may differ by at most the number of near-tied
+    candidates. Returns the number of such differences."""
+    mism = 0
+    for k, (a, b) in enumerate(zip(ours, ref_ranks)):
+        con = con_h if k < 2 else con_t
+        for q in np.nonzero(np.asarray(a) != np.asarray(b))[0]:
+            s0 = con[q][0]
+            ties = np.count_nonzero(np.abs(con[q][1:] - s0) <= rel_tol * max(1.0, abs(float(s0))))
+            assert abs(int(a[q]) - int(b[q])) <= ties, (k, q, a[q], b[q], ties)
+            mism += 1
+    return mism
