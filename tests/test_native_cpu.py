@@ -207,3 +207,23 @@ def test_classification_without_threshold_raises_like_reference():
     # a usable threshold: the reference's accuracy formula (Tester.py:182-190)
     acc, thr = t.run_triple_classification(data_iterator=[([0.1, 0.2], [0.9, 0.3])])
     assert thr == np.float32(0.2) and acc == 1.0
+
+
+def test_import_type_files_matches_oracle_reader():
+    """importTypeFiles (Reader.h:352-396) in the library's global context: per-relation [lef, rig) and
+    the sorted type lists == the oracle's reading of the same type_constrain.txt (host code only)."""
+    L = _native.lib()
+    L.setInPath(ctypes.create_string_buffer(KG_SMALL.encode(), len(KG_SMALL) * 2))
+    L.importTrainFiles()   # sets relationTotal (its device upload is irrelevant here)
+    R = L.getRelationTotal()
+    L.importTypeFiles()
+    want = oracle.read_types(KG_SMALL + "type_constrain.txt", R)
+    for side in (0, 1):
+        n = L.pt_legacy_types(side, None, None, None)
+        assert n >= 0
+        lef, rig = np.zeros(R, dtype=np.int64), np.zeros(R, dtype=np.int64)
+        lst = np.zeros(max(n, 1), dtype=np.int64)
+        assert L.pt_legacy_types(side, lef.ctypes.data, rig.ctypes.data, lst.ctypes.data) == n
+        np.testing.assert_array_equal(lef, want[3 * side])
+        np.testing.assert_array_equal(rig, want[3 * side + 1])
+        np.testing.assert_array_equal(lst[:n], want[3 * side + 2][:n])
