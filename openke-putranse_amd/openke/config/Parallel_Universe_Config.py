@@ -336,12 +336,13 @@ class Parallel_Universe_Config(Tester):
         self.trained_embedding_spaces[self.next_universe_id] = embedding_space
 
     # ------------------------------------------------------------------ training ----------------
-    def _check_setup(self):
+    def _batched(self):
+        """The multi-universe kernel draws normal-mode entity corruptions; cross sampling or relation
+        corruption train universe by universe (the reference's protocol on the fused trainer)."""
         dl = self.train_dataloader
-        if dl.sampling_mode != "normal":
-            raise NotImplementedError("PuTransE trains with sampling_mode='normal' (TrainDataLoader.sampling)")
-        if dl.negative_rel != 0:
-            raise NotImplementedError("neg_rel > 0 is outside the accelerated path")
+        return dl.sampling_mode == "normal" and dl.negative_rel == 0
+
+    def _check_setup(self):
         if self.embedding_model is None or getattr(self.embedding_model, "native_model", None) is None:
             raise NotImplementedError("embedding_model must be openke.module.model.TransE or TransH")
         _native.require_gpu()
@@ -478,6 +479,7 @@ class Parallel_Universe_Config(Tester):
         print('universe information-------------------')
         print('--- num of training triples: %d' % triple_constraint)
         self.train_dataloader.compile_universe_dataset(triple_constraint, balance_param)
+        self._compiled_draws = (triple_constraint, balance_param)
         self.process_universe_mappings()
         lib = self.train_dataloader.lib
         print('--- num of universe entities: %d' % lib.getEntityTotalUniverse())
@@ -510,7 +512,8 @@ class Parallel_Universe_Config(Tester):
         trainer.run()
         self.train_dataloader.reset_universe()
         self.universe_hparams[self.next_universe_id] = {
-            "tc": None, "balance": None, "margin": margin, "epochs": train_times, "lr": lr,
+            "tc": getattr(self, "_compiled_draws", (None, None))[0],
+            "balance": getattr(self, "_compiled_draws", (None, None))[1], "margin": margin, "epochs": train_times, "lr": lr,
             "batch_size": model.batch_size, "train_total": train_total_universe}
         return model.model
 
@@ -524,9 +527,50 @@ class Parallel_Universe_Config(Tester):
         self.universe_hparams[uid] = {k: rec[k] for k in ("tc", "balance", "margin", "epochs", "lr", "batch_size",
                                                          "train_total")}
 
+    def _after_universe(self, universe_id):
+        """Validation / early stopping / checkpoint schedule after universe `universe_id` of this call
+        (Parallel_Universe_Config.py:329-365); True when training stops early."""
+        if (universe_id + 1) % self.valid_steps == 0:
+            print("Universe %d has finished, validating..." % (self.next_universe_id - 1))
+            self.eval_universes(eval_mode='valid')
+            hit10 = self.valid()
+            print("Current hit@10: {}".format(hit10))
+            if hit10 > self.best_hit10:
+                self.best_hit10 = hit10
+                print("Best model | hit@10 of valid set is %f" % self.best_hit10)
+                print('Save model at universe %d.' % self.next_universe_id)
+                self.save_model("Best_model_Pu{}_{}.ckpt".format(self.embedding_model.__name__,
+                                                                 self.training_identifier))
+                self.bad_counts = 0
+            else:
+                print("Hit@10 of valid set is %f | bad count is %d" % (hit10, self.bad_counts))
+                self.bad_counts += 1
+            if self.bad_counts == self.early_stopping_patience:
+                print("Early stopping at universe {}".format(self.next_universe_id - 1))
+                self.get_best_state()
+                return True
+        if self.save_steps and self.checkpoint_dir and (universe_id + 1) % self.save_steps == 0:
+            print('Save model at universe %d.' % self.next_universe_id)
+            self.save_model()
+        return False
+
     def train_parallel_universes(self, num_of_embedding_spaces):
         self._check_setup()
         training_duration = 0.0
+        if not self._batched():
+            # cross sampling / relation corruption: the reference's loop (:320-327), one universe at a time
+            for universe_id in range(num_of_embedding_spaces):
+                t0 = time.time()
+                self.set_random_seed(self.initial_random_seed + self.next_universe_id)
+                self.compile_train_datset()
+                embedding_space = self.train_embedding_space()
+                self.add_embedding_space(embedding_space)
+                self.next_universe_id += 1
+                training_duration += time.time() - t0
+                if self._after_universe(universe_id):
+                    break
+            print('Time took for creation of embedding spaces: {:5.3f}s'.format(training_duration), end='\n')
+            return
         done = 0
         stop = False
         while done < num_of_embedding_spaces and not stop:
@@ -542,29 +586,9 @@ class Parallel_Universe_Config(Tester):
                 universe_id = done
                 self._commit(rec)
                 training_duration += per_universe
-                if (universe_id + 1) % self.valid_steps == 0:
-                    print("Universe %d has finished, validating..." % (self.next_universe_id - 1))
-                    self.eval_universes(eval_mode='valid')
-                    hit10 = self.valid()
-                    print("Current hit@10: {}".format(hit10))
-                    if hit10 > self.best_hit10:
-                        self.best_hit10 = hit10
-                        print("Best model | hit@10 of valid set is %f" % self.best_hit10)
-                        print('Save model at universe %d.' % self.next_universe_id)
-                        self.save_model("Best_model_Pu{}_{}.ckpt".format(self.embedding_model.__name__,
-                                                                         self.training_identifier))
-                        self.bad_counts = 0
-                    else:
-                        print("Hit@10 of valid set is %f | bad count is %d" % (hit10, self.bad_counts))
-                        self.bad_counts += 1
-                    if self.bad_counts == self.early_stopping_patience:
-                        print("Early stopping at universe {}".format(self.next_universe_id - 1))
-                        self.get_best_state()
-                        stop = True
-                        break
-                if self.save_steps and self.checkpoint_dir and (universe_id + 1) % self.save_steps == 0:
-                    print('Save model at universe %d.' % self.next_universe_id)
-                    self.save_model()
+                if self._after_universe(universe_id):
+                    stop = True
+                    break
                 done += 1
         print('Time took for creation of embedding spaces: {:5.3f}s'.format(training_duration), end='\n')
 
