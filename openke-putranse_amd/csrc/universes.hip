@@ -608,8 +608,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     X(7, 2, 1, 1) X(8, 2, 1, 2) X(9, 2, 1, 4) X(10, 4, 1, 4) X(11, 8, 1, 4) X(12, 16, 1, 4)              \
     X(13, 32, 1, 4) X(14, 64, 1, 4) X(15, 64, 1, 8)                                                      \
     X(16, 2, 4, 4) X(17, 4, 4, 4) X(18, 8, 4, 4) X(19, 16, 4, 4) X(20, 32, 4, 4) X(21, 64, 4, 4)        \
-    X(22, 2, 1, 8) X(23, 4, 1, 8) X(24, 8, 1, 8) X(25, 16, 1, 8) X(26, 32, 1, 8)                        \
-    X(27, 2, 1, 16) X(28, 4, 1, 16) X(29, 8, 1, 16) X(30, 16, 1, 16) X(31, 32, 1, 16)
+    X(22, 2, 1, 8) X(23, 4, 1, 8) X(24, 8, 1, 8) X(25, 16, 1, 8) X(26, 32, 1, 8)
 
 // shape class (one kernel each): 0 = at most 4 floats per lane, 1 = 8, 2 = 16 (TransE's wide shapes)
 #define PT_UCLASS(V_, K_) ((V_) * (K_) <= 4 ? 0 : ((V_) * (K_) <= 8 ? 1 : 2))
@@ -663,14 +662,7 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
 Shape pick_universe_shape(int64_t D, bool wide) {
     const int VEC = D % 4 == 0 ? 4 : 1;
     const int64_t chunks = (D + VEC - 1) / VEC;
-    // PT_UNI_W16=1: wide rows of a dim that is no multiple of 4 (scalar chunks) take 16 floats per lane
-    // like the float4 wide shapes - half the lanes per row, twice the lane groups, half the rounds of a
-    // step's positives (default: 8 floats per lane)
-    static const bool w8 = [] {
-        const char *v = getenv("PT_UNI_W16");
-        return !(v && atoi(v) != 0);
-    }();
-    const int64_t per_lane = VEC == 4 ? (wide ? 4 : 2) : (wide ? (w8 ? 8 : 16) : 4);
+    const int64_t per_lane = (VEC == 4 ? 2 : 4) * (wide ? 2 : 1);
     int G = 2;
     while (G < 64 && (int64_t)G * per_lane < chunks) G <<= 1;
     int KCH = 1;
