@@ -102,6 +102,15 @@ int pt_trainer_step(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg,
 int pt_trainer_run(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
                    int64_t steps, float *d_losses, void *stream);
 
+/* Reference-order (deterministic) mode of a trainer: every later pt_trainer_step / pt_trainer_run sums each
+ * table row's gradient in slot order, lookup by lookup (batch_h, batch_t, batch_r; norm_vector(batch_r)),
+ * as torch's embedding_dense_backward + AccumulateGrad do for Trainer.train_one_step (Trainer.py:44-56),
+ * with sequential dot products / norms and IEEE division and square root. Results are bit-identical run to
+ * run (and to the CPU restatement oracle/oracle.c); the default fast path sums the same contributions in
+ * arrival order (float atomics) and is faster. on = 0 returns to the fast path. */
+int pt_trainer_set_deterministic(pt_trainer *t, int32_t on);
+int pt_trainer_get_deterministic(const pt_trainer *t);
+
 /* Measurement hook: `steps` in-kernel-sampled steps launched one by one (no graph) with an event pair
  * around every launch on `stream`. ms4[k] = total duration of kernel kind k divided by `steps`:
  * 0 batch sampling (k_sample_csr, large-neg path only, one launch per chunk of steps), 1 bucket scan
@@ -189,9 +198,16 @@ int pt_universe_set_free(pt_universe_set *s);
  * set's launch order) shader-clock cycles spent in epoch presampling, phase A, phase B, the step count,
  * batch size, dim and entity count (last train call; out[.][7] unused) */
 int pt_universe_set_profile(pt_universe_set *s, uint64_t *out);
+/* reference-order (deterministic) mode of a set (see pt_trainer_set_deterministic): one workgroup per
+ * universe runs its steps with the ordered per-row sums; its workspace is allocated on first use */
+int pt_universe_set_deterministic(pt_universe_set *s, int32_t on);
 /* create + train + free (synchronizes `stream`) */
 int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm, int32_t norm_flag,
                        int32_t opt, int64_t bern, int64_t filter, float *d_losses, void *stream);
+enum { PT_DETERMINISTIC = 1 };
+/* the same with flags (PT_DETERMINISTIC: reference-order mode) */
+int pt_universes_train_ex(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm, int32_t norm_flag,
+                          int32_t opt, int64_t bern, int64_t filter, int32_t flags, float *d_losses, void *stream);
 
 /* ------------------------------------------------------------------ link prediction --------- */
 /* Per-universe all-entity scoring with a float MIN reduction into per-key rows

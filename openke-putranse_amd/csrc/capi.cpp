@@ -16,6 +16,7 @@
 #include "common.h"
 #include "graph.h"
 #include "kernels.h"
+#include "ordered.h"
 #include "rng.h"
 #include "universe.h"
 #include "universes.h"
@@ -72,6 +73,13 @@ struct pt_trainer {
     int device = -1;
     hipStream_t cap = nullptr;
     std::map<GraphKey, hipGraphExec_t> graphs;
+    // reference-order (deterministic) mode: ordered.hip's step on k_sample batches (pt_trainer_set_deterministic)
+    bool ordered = false;
+    void *ord_block = nullptr;
+    size_t ord_cap = 0;
+    int64_t *ord_h = nullptr, *ord_t = nullptr, *ord_r = nullptr;
+    float *ord_y = nullptr, *ord_score = nullptr, *ord_ds = nullptr;
+    float *ord_g = nullptr;   // [4][seq][dim] per-slot gradient rows
     void drop_graphs() {
         for (auto &kv : graphs) (void)hipGraphExecDestroy(kv.second);
         graphs.clear();
@@ -84,6 +92,7 @@ struct pt_trainer {
         if (csr_block) (void)hipFree(csr_block);
         if (csr.prof) (void)hipFree(csr.prof);
         if (W.lpart) (void)hipFree(W.lpart);
+        if (ord_block) (void)hipFree(ord_block);
     }
 };
 
@@ -503,6 +512,76 @@ static int prepare_sampled(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg
     return PT_OK;
 }
 
+// ---- reference-order mode (ordered.hip): workspace for batches of up to `seq` slots
+static int ensure_ordered(pt_trainer *t, int64_t seq) {
+    const int64_t D = t->P.dim;
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t need = 3 * al(8 * seq) + 3 * al(4 * seq) + al(16 * (size_t)seq * D);
+    if (need <= t->ord_cap) return PT_OK;
+    PT_HIP(hipDeviceSynchronize());   // queued ordered steps may still use the old block
+    if (t->ord_block) (void)hipFree(t->ord_block);
+    t->ord_block = nullptr;
+    t->ord_cap = 0;
+    PT_HIP(hipMalloc(&t->ord_block, need));
+    t->ord_cap = need;
+    char *b = (char *)t->ord_block;
+    t->ord_h = (int64_t *)b; b += al(8 * seq);
+    t->ord_t = (int64_t *)b; b += al(8 * seq);
+    t->ord_r = (int64_t *)b; b += al(8 * seq);
+    t->ord_y = (float *)b; b += al(4 * seq);
+    t->ord_score = (float *)b; b += al(4 * seq);
+    t->ord_ds = (float *)b; b += al(4 * seq);
+    t->ord_g = (float *)b;
+    return PT_OK;
+}
+
+static int enqueue_ordered(pt_trainer *t, int64_t bs, int64_t neg, const int64_t *bh, const int64_t *bt,
+                           const int64_t *br, float *loss, int assign, hipStream_t st) {
+    const pt::StepParams &P = t->P;
+    pt::OrderedStep S{};
+    S.model = P.model; S.p_norm = P.p_norm; S.norm_flag = P.norm_flag; S.opt = P.opt;
+    S.lr = P.lr; S.margin = P.margin;
+    S.ent_total = P.ent_total; S.rel_total = P.rel_total; S.dim = P.dim;
+    S.ent = P.ent; S.rel = P.rel; S.normv = P.normv;
+    S.ent_acc = P.ent_acc; S.rel_acc = P.rel_acc; S.norm_acc = P.norm_acc;
+    S.h = bh; S.t = bt; S.r = br;
+    S.bs = bs; S.neg = neg; S.seq = bs * (1 + neg);
+    S.score = t->ord_score; S.ds = t->ord_ds;
+    S.gh = t->ord_g; S.gt = S.gh + S.seq * P.dim; S.gr = S.gt + S.seq * P.dim; S.gw = S.gr + S.seq * P.dim;
+    PT_HIP(pt::launch_ordered_step(S, loss, assign, st));
+    return PT_OK;
+}
+
+// `steps` sampled steps in reference order: k_sample's batch (bit-identical to sampling()), then the step
+static int enqueue_ordered_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
+                               int64_t steps, float *d_losses, int assign, hipStream_t st) {
+    PT_CHECK(s && s->g && s->d_states, PT_ESTATE, "in-kernel sampling needs a sampler bound to a graph");
+    PT_CHECK(s->g->ent_total > 1, PT_EINVAL, "graph needs at least two entities");
+    PT_CHECK(s->g->ent_total <= t->P.ent_total && s->g->rel_total <= t->P.rel_total, PT_EINVAL,
+             "graph ids exceed the model tables");
+    int rc = s->g->upload();
+    if (rc) return rc;
+    rc = ensure_ordered(t, bs * (1 + neg));
+    if (rc) return rc;
+    t->last_path = -1;
+    for (int64_t i = 0; i < steps; ++i) {
+        PT_HIP(pt::launch_sample(s->g->dev, s->d_states, s->threads, bs, neg, 0, 0, (int)bern, (int)filter, t->ord_h,
+                                 t->ord_t, t->ord_r, t->ord_y, st));
+        PT_HIP(pt::launch_advance(s->d_states, s->threads, bs, 1 + 2 * neg, st));
+        rc = enqueue_ordered(t, bs, neg, t->ord_h, t->ord_t, t->ord_r, d_losses ? d_losses + i : nullptr, assign, st);
+        if (rc) return rc;
+    }
+    return PT_OK;
+}
+
+extern "C" int pt_trainer_set_deterministic(pt_trainer *t, int32_t on) {
+    PT_CHECK(t, PT_EINVAL, "null trainer");
+    PT_CHECK(!on || pt::ordered_dim_supported(t->P.dim), PT_ENOTSUP, "reference-order mode: dim too large");
+    t->ordered = on != 0;
+    return PT_OK;
+}
+extern "C" int pt_trainer_get_deterministic(const pt_trainer *t) { return t && t->ordered ? 1 : 0; }
+
 extern "C" int pt_trainer_step(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
                                const int64_t *d_bh, const int64_t *d_bt, const int64_t *d_br, float *d_loss,
                                void *stream) {
@@ -510,10 +589,17 @@ extern "C" int pt_trainer_step(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t
     if (d_bh) {
         PT_CHECK(d_bt && d_br, PT_EINVAL, "external batch needs h, t and r arrays");
         PT_CHECK(bs > 0 && neg > 0, PT_EINVAL, "batch_size and neg_ent must be positive");
+        if (t->ordered) {
+            int rc = ensure_ordered(t, bs * (1 + neg));
+            if (rc) return rc;
+            return enqueue_ordered(t, bs, neg, d_bh, d_bt, d_br, d_loss, 0, (hipStream_t)stream);
+        }
         int rc = ensure_lpart(t, bs);
         if (rc) return rc;
         return enqueue_external(t, bs, neg, d_bh, d_bt, d_br, d_loss, (hipStream_t)stream);
     }
+    PT_CHECK(bs > 0 && neg > 0, PT_EINVAL, "batch_size and neg_ent must be positive");
+    if (t->ordered) return enqueue_ordered_run(t, s, bs, neg, bern, filter, 1, d_loss, 0, (hipStream_t)stream);
     int rc = prepare_sampled(t, s, bs, neg, 1);
     if (rc) return rc;
     return enqueue_run(t, s, bs, neg, bern, filter, 1, d_loss, (hipStream_t)stream);
@@ -525,6 +611,7 @@ extern "C" int pt_trainer_step(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t
 extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t bern,
                                     int64_t filter, int64_t steps, float *d_losses, float *ms4, void *stream) {
     PT_CHECK(t && ms4 && steps > 0, PT_EINVAL, "pt_trainer_run_timed: bad argument");
+    PT_CHECK(!t->ordered, PT_ENOTSUP, "pt_trainer_run_timed times the fast path (reference-order mode is on)");
     int rc = prepare_sampled(t, s, bs, neg, steps);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
@@ -689,6 +776,10 @@ extern "C" int pt_trainer_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t 
                               int64_t steps, float *d_losses, void *stream) {
     PT_CHECK(t && d_losses, PT_EINVAL, "pt_trainer_run: null argument");
     PT_CHECK(steps > 0, PT_EINVAL, "steps must be positive");
+    if (t->ordered) {
+        PT_CHECK(bs > 0 && neg > 0, PT_EINVAL, "batch_size and neg_ent must be positive");
+        return enqueue_ordered_run(t, s, bs, neg, bern, filter, steps, d_losses, 1, (hipStream_t)stream);
+    }
     int rc = prepare_sampled(t, s, bs, neg, steps);
     if (rc) return rc;
     GraphKey key{s, s->g->dev.rec, d_losses, s->d_states, bs, neg, bern, filter, steps};
@@ -859,11 +950,16 @@ struct pt_universe_set {
     std::vector<pt::UniverseDev> host;    // same order; loss pointers patched per train call
     std::vector<int64_t> host_loss_off;
     uint64_t *prof = nullptr;             // PT_UNI_PROF=1: [n][8] cycle counters + shape (device)
+    // reference-order (deterministic) mode (pt_universe_set_deterministic): ordered.hip's universe kernel
+    bool ordered = false;
+    void *ord_arena = nullptr;            // per universe [4][seq][dim] gradient rows
+    int64_t ord_max_seq = 0;
     ~pt_universe_set() {
         for (auto e : events) (void)hipEventDestroy(e);
         for (auto q : streams) (void)hipStreamDestroy(q);
         if (arena) (void)hipFree(arena);
         if (prof) (void)hipFree(prof);
+        if (ord_arena) (void)hipFree(ord_arena);
     }
 };
 
@@ -1075,6 +1171,30 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     return PT_OK;
 }
 
+extern "C" int pt_universe_set_deterministic(pt_universe_set *set, int32_t on) {
+    PT_CHECK(set, PT_EINVAL, "null universe set");
+    set->ordered = on != 0;
+    if (!set->ordered || set->ord_arena || set->host.empty()) return PT_OK;
+    auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
+    int64_t total = 0, max_seq = 0;
+    std::vector<int64_t> off(set->host.size());
+    for (size_t i = 0; i < set->host.size(); ++i) {
+        const pt::UniverseDev &U = set->host[i];
+        const int64_t seq = U.bs * (1 + set->neg);
+        off[i] = total;
+        total += al(16 * seq * U.dim);
+        max_seq = std::max(max_seq, seq);
+    }
+    int dev_lds = 64 << 10;
+    (void)hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, set->device);
+    PT_CHECK(pt::ordered_universe_lds_bytes(max_seq) <= std::min<int64_t>(dev_lds, 160 << 10), PT_ENOTSUP,
+             "reference-order mode: universe batch too large for the LDS plan");
+    PT_HIP(hipMalloc(&set->ord_arena, (size_t)std::max<int64_t>(total, 256)));
+    for (size_t i = 0; i < set->host.size(); ++i) set->host[i].ord = (float *)((char *)set->ord_arena + off[i]);
+    set->ord_max_seq = max_seq;
+    return PT_OK;
+}
+
 extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void *stream) {
     PT_CHECK(set, PT_EINVAL, "null universe set");
     if (set->host.empty()) return PT_OK;
@@ -1083,6 +1203,16 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
         set->host[i].losses = d_losses ? d_losses + set->host_loss_off[i] : nullptr;
     PT_HIP(hipMemcpyAsync(set->d_us, set->host.data(), sizeof(pt::UniverseDev) * set->host.size(),
                           hipMemcpyHostToDevice, st));
+    if (set->ordered) {
+        int cus = 0;
+        PT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, set->device));
+        const hipError_t e = pt::launch_universes_ordered(set->d_us, (int64_t)set->host.size(), set->d_counter, cus,
+                                                          set->model, set->p_norm, set->norm_flag, set->opt, set->neg,
+                                                          (int)set->bern, (int)set->filter, set->ord_max_seq, st);
+        if (e != hipSuccess) return pt::fail(PT_EHIP, std::string("launch_universes_ordered: ") + hipGetErrorString(e));
+        PT_HIP(hipStreamSynchronize(st));
+        return PT_OK;
+    }
     // one launch per shape class, concurrently on a side stream, each over its share of the CUs (set at
     // creation); joined back into `st`
     const size_t ng = set->groups.size();
@@ -1130,6 +1260,21 @@ extern "C" int pt_universe_set_free(pt_universe_set *set) {
     if (set) (void)hipDeviceSynchronize();
     delete set;
     return PT_OK;
+}
+
+extern "C" int pt_universes_train_ex(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm,
+                                     int32_t norm_flag, int32_t opt, int64_t bern, int64_t filter, int32_t flags,
+                                     float *d_losses, void *stream) {
+    PT_CHECK((flags & ~PT_DETERMINISTIC) == 0, PT_EINVAL, "pt_universes_train_ex: unknown flags");
+    pt_universe_set *set = nullptr;
+    int rc = pt_universe_set_create(jobs, n, model, p_norm, norm_flag, opt, bern, filter, &set);
+    if (rc) return rc;
+    if (flags & PT_DETERMINISTIC) rc = pt_universe_set_deterministic(set, 1);
+    if (!rc) rc = pt_universe_set_train(set, d_losses, stream);
+    const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    pt_universe_set_free(set);
+    if (!rc && e != hipSuccess) rc = pt::fail(PT_EHIP, std::string("pt_universes_train: ") + hipGetErrorString(e));
+    return rc;
 }
 
 extern "C" int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm,

@@ -18,6 +18,7 @@ struct UniverseDev {
     float *gent, *grel, *gnorm;                     // gradient rows, zero between steps
     int32_t *fent, *frel, *fnorm;                   // touched-row flags, zero between steps
     float *contrib;                                 // [bs*(4+neg)][dim] gradient-row contributions
+    float *ord;                                     // reference-order mode: [4][seq][dim] per-slot gradient rows
     float *losses;                                  // [epochs] Trainer.run's per-epoch loss sum (or null)
     uint64_t *prof;                                 // null, or [8]: cycles (presample, A, B), steps, bs, dim, E, 0
     int64_t threads, bs, nbatches, epochs, dim;

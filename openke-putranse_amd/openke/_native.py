@@ -20,6 +20,7 @@ c_f32p = ctypes.POINTER(ctypes.c_float)
 
 PT_TRANSE, PT_TRANSH = 0, 1
 PT_SGD, PT_ADAGRAD = 0, 1
+PT_DETERMINISTIC = 1   # pt_universes_train_ex flag: reference-order (deterministic) mode
 # sampling paths of the counting-sort (large neg) step (include/putranse.h PT_PATH_*)
 PT_PATH_TWO_PASS, PT_PATH_FUSED, PT_PATH_PART, PT_PATH_SAMPLED = 0, 1, 2, 3
 PATH_KERNELS = {PT_PATH_TWO_PASS: ("k_sample_csr", "k_scan_counts"), PT_PATH_FUSED: ("k_sample_sort", "k_advance"),
@@ -75,6 +76,8 @@ SIGNATURES = {
     "pt_trainer_run": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "pt_trainer_run_timed": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "pt_trainer_last_path": (ctypes.c_int, [c_vp]),
+    "pt_trainer_set_deterministic": (ctypes.c_int, [c_vp, c_i32]),
+    "pt_trainer_get_deterministic": (ctypes.c_int, [c_vp]),
     "pt_trainer_sample_csr": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, ctypes.c_int32, c_vp,
                                              c_vp, c_vp, c_vp, c_vp]),
     "pt_score": (ctypes.c_int, [ctypes.POINTER(ModelDesc), c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
@@ -95,8 +98,11 @@ SIGNATURES = {
     "pt_universe_set_train": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "pt_universe_set_free": (ctypes.c_int, [c_vp]),
     "pt_universe_set_profile": (ctypes.c_int, [c_vp, c_vp]),
+    "pt_universe_set_deterministic": (ctypes.c_int, [c_vp, c_i32]),
     "pt_universes_train": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
                                           c_i64, c_vp, c_vp]),
+    "pt_universes_train_ex": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
+                                             c_i64, c_i32, c_vp, c_vp]),
     "pt_lp_min_scores": (ctypes.c_int, [ctypes.POINTER(LpUniverse), c_i64, c_i32, c_i32, c_i32,
                                         ctypes.POINTER(LpPair), c_i64, c_i64, c_vp, c_vp, c_vp]),
     "pt_rank_rows": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),

@@ -212,7 +212,7 @@ class Parallel_Universe_Config(Tester):
                  save_steps=5, checkpoint_dir='./checkpoint/', valid_steps=5, early_stopping_patience=5,
                  training_setting="static",
                  incremental_strategy="normal",
-                 universe_wave_size=None):
+                 universe_wave_size=None, deterministic=False):
         super(Parallel_Universe_Config, self).__init__(data_loader=test_dataloader, use_gpu=torch.cuda.is_available())
         if training_setting != "static":
             raise NotImplementedError("the incremental setting is outside the accelerated path")
@@ -288,6 +288,9 @@ class Parallel_Universe_Config(Tester):
 
         """ MI355X build """
         self.universe_wave_size = universe_wave_size
+        # reference-order mode (ordered.hip): every universe's per-row gradient sums in slot order,
+        # bit-identical run to run; the default fast kernel sums them in arrival order
+        self.deterministic = bool(deterministic)
         self.last_universe_losses = {}    # universe_id -> per-epoch loss sums of Trainer.run
         self.universe_hparams = {}        # universe_id -> tc, balance, margin, epochs, lr, batch_size
         self._stores = {}                 # 'test' / 'valid' -> _KeyStore
@@ -420,10 +423,11 @@ class Parallel_Universe_Config(Tester):
                 total_epochs = sum(int(j.epochs) for j in jobs)
                 losses = torch.zeros(max(total_epochs, 1), dtype=torch.float32, device=dev)
                 arr = (_native.UniverseJob * len(jobs))(*jobs)
-                _native.check(L.pt_universes_train(arr, len(jobs), kge0.native_model, int(kge0.p_norm),
-                                                   1 if kge0.norm_flag else 0, _native.PT_ADAGRAD,
-                                                   int(dl.bern), int(dl.filter), _native.ptr(losses),
-                                                   _native.stream()))
+                _native.check(L.pt_universes_train_ex(arr, len(jobs), kge0.native_model, int(kge0.p_norm),
+                                                      1 if kge0.norm_flag else 0, _native.PT_ADAGRAD,
+                                                      int(dl.bern), int(dl.filter),
+                                                      _native.PT_DETERMINISTIC if self.deterministic else 0,
+                                                      _native.ptr(losses), _native.stream()))
                 lh = losses.cpu().numpy()
                 off = 0
                 for j, (_, _, rec) in zip(jobs, keep):
@@ -503,7 +507,7 @@ class Parallel_Universe_Config(Tester):
             else randrange(self.min_num_epochs, self.max_num_epochs)
         lr = round(uniform(self.min_lr, self.max_lr), len(str(self.min_lr).split('.')[1]))
         trainer = Trainer(model=model, data_loader=self.train_dataloader, train_times=train_times, alpha=lr,
-                          use_gpu=True, opt_method='Adagrad')
+                          use_gpu=True, opt_method='Adagrad', deterministic=self.deterministic)
         print('hyperparams for universe %d------------' % self.next_universe_id)
         print('--- epochs: %d' % train_times)
         print('--- learning rate:', lr)

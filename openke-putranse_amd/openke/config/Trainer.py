@@ -38,7 +38,7 @@ class NativeOptimizer(object):
 class Trainer(object):
 
     def __init__(self, model=None, data_loader=None, valid_dataloader=None, train_times=1000, alpha=0.5,
-                 use_gpu=True, opt_method="sgd", save_steps=None, checkpoint_dir=None):
+                 use_gpu=True, opt_method="sgd", save_steps=None, checkpoint_dir=None, deterministic=False):
         self.work_threads = 8
         self.train_times = train_times
         self.opt_method = opt_method
@@ -53,6 +53,9 @@ class Trainer(object):
         self.checkpoint_dir = checkpoint_dir
         self._native = None
         self._native_key = None
+        # reference-order mode (pt_trainer_set_deterministic): per-row gradient sums in slot order, lookup by
+        # lookup, as embedding_dense_backward does (bit-identical run to run); off = the fused fast path
+        self.deterministic = bool(deterministic)
 
     # ------------------------------------------------------------------ native setup ------------
     def _parts(self):
@@ -95,6 +98,7 @@ class Trainer(object):
         elif key != self._native_key:
             _native.check(L.pt_trainer_update_desc(self._native, ctypes.byref(desc)))
         self._native_key = key
+        _native.check(L.pt_trainer_set_deterministic(self._native, 1 if self.deterministic else 0))
         return ns, kge, loss
 
     def __del__(self):
@@ -157,6 +161,13 @@ class Trainer(object):
                 mode = -1 if dl.cross_sampling_flag == 0 else 1
             _native.check(L.pt_sampler_sample_ex(sampler, bs, neg, neg_rel, mode, bern, dl.filter, _native.ptr(h),
                                                  _native.ptr(t), _native.ptr(r), _native.ptr(y), st))
+            if mode != 0:
+                # sampling_head / sampling_tail hand the model only the first bs relations and fixed-side
+                # entities (TrainDataLoader.py:212-217, :231-236) and TransE/TransH broadcast them over every
+                # negative (TransE.py:51-58): a relation-corruption slot trains as a copy of its positive
+                fixed = t if mode == -1 else h
+                fixed.view(-1, bs)[1:] = fixed[:bs]
+                r.view(-1, bs)[1:] = r[:bs]
             _native.check(L.pt_trainer_step(self._native, None, bs, neg + neg_rel, 0, 0, _native.ptr(h),
                                             _native.ptr(t), _native.ptr(r), _native.ptr(losses[i:i + 1]), st))
 
@@ -187,6 +198,7 @@ class Trainer(object):
                 losses.zero_()
                 self._run_batches(L, sampler, bern, bs, nb, losses, buf)
             host = losses.cpu().numpy()
+            self.last_step_losses = host[:nb].copy()
             res = float(host[:nb].sum())
             loss_v = float(host[nb - 1]) if nb > 0 else 0.0
             training_range.set_description("Epoch %d | loss: %f" % (epoch, loss_v))
@@ -228,3 +240,6 @@ class Trainer(object):
 
     def set_checkpoint_dir(self, checkpoint_dir):
         self.checkpoint_dir = checkpoint_dir
+
+    def set_deterministic(self, deterministic):
+        self.deterministic = bool(deterministic)

@@ -6,6 +6,7 @@
 #include "oracle.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -585,110 +586,370 @@ void oracle_score(int model, int p, int norm_flag, int mode, int64_t d, const fl
 
 static void apply_update(int opt, float lr, float *w, float *acc, const float *g, int64_t n) {
     if (opt == 0) {
-        for (int64_t i = 0; i < n; ++i) w[i] = w[i] + (-lr) * g[i];
+        for (int64_t i = 0; i < n; ++i) w[i] = w[i] + (-lr) * g[i];   /* SGD add_(grad, alpha=-lr) */
     } else {
-        for (int64_t i = 0; i < n; ++i) {
+        for (int64_t i = 0; i < n; ++i) {                               /* Adagrad, eps 1e-10, lr_decay 0 */
             acc[i] = acc[i] + g[i] * g[i];
             w[i] = w[i] + (-lr) * g[i] / (sqrtf(acc[i]) + 1e-10f);
         }
     }
 }
 
+/* ---------------------------------------------------------------- the step in reference order -- */
+/* One step of Trainer.train_one_step (Trainer.py:44-56) in the order torch's autograd sums it:
+ *   1. score every slot with the pre-step tables (TransE.py:46-74 / TransH.py:52-93);
+ *   2. MarginLoss (MarginLoss.py:24-28) over NegativeSampling's (bs, neg) view (NegativeSampling.py:13-31):
+ *      loss summed in (positive, negative) order, per-slot score gradients ds;
+ *   3. per slot with ds != 0 its gradient rows: the h lookup's, the t lookup's, the r lookup's (and the
+ *      norm_vector lookup's for TransH, the two _transfer calls' normalize backwards added, TransH.py:68-76);
+ *   4. per table row the lookups' rows summed in slot order, each lookup separately, then the two entity
+ *      lookups added (embedding_dense_backward per lookup, then AccumulateGrad, Trainer.py:52-55);
+ *   5. the optimizer on every row with a gradient (a dense SGD / Adagrad step leaves the others unchanged).
+ * Steps 1, 3 and 5 are independent per slot / per row; `workers` > 1 runs them on that many threads and
+ * the result is bit-identical to workers = 1 (every float sum keeps its order). */
+typedef struct {
+    int model, p, norm_flag, opt;
+    float lr, margin;
+    int64_t E, R, d, bs, neg, seq;
+    float *ent, *rel, *normv, *ent_acc, *rel_acc, *norm_acc;
+    const int64_t *h, *t, *r;
+    /* scratch */
+    float *score, *ds;
+    float *gh, *gt, *gr, *gw;                     /* [seq][d] */
+    int64_t *hoff, *hlist, *toff, *tlist, *roff, *rlist;
+    int64_t cap_seq, cap_e, cap_r, cap_d;
+} ostep;
+
+static void slot_ws_bind(slot_ws *ws, float *buf, int64_t d) {
+    memset(ws, 0, sizeof(*ws));
+    ws->d = d;
+    ws->hp = buf; ws->tp = buf + d; ws->nh = buf + 2 * d; ws->nt = buf + 3 * d; ws->nr = buf + 4 * d;
+    ws->nw = buf + 5 * d; ws->v = buf + 6 * d;
+}
+
+/* d loss / d rows of slot s (step 3): writes gh/gt/gr(/gw) rows of the slot */
+static void slot_backward(const ostep *S, slot_ws *ws, float *tmpb, int64_t s) {
+    const int64_t d = S->d;
+    const float *he = S->ent + S->h[s] * d, *te = S->ent + S->t[s] * d, *re = S->rel + S->r[s] * d;
+    const float *W = S->model == 1 ? S->normv + S->r[s] * d : NULL;
+    const float dsv = S->ds[s];
+    float sc = slot_forward(S->model, S->p, S->norm_flag, 0, ws, he, te, re, W);
+    float *gv = tmpb, *tmp = tmpb + d, *x1 = tmpb + 2 * d, *x2 = tmpb + 3 * d;
+    float *ga = S->gh + s * d, *gb = S->gr + s * d, *gc = S->gt + s * d;
+    for (int64_t i = 0; i < d; ++i) {
+        if (S->p == 1) gv[i] = ws->v[i] > 0 ? dsv : (ws->v[i] < 0 ? -dsv : 0.0f);   /* sign(v), sign(0) = 0 */
+        else gv[i] = sc == 0.0f ? 0.0f : ws->v[i] * (dsv / sc);
+        tmp[i] = -gv[i];   /* d/d(nt) = -gv; d/d(nh) = d/d(nr) = gv */
+    }
+    const float *hsrc = S->model == 1 ? ws->hp : he, *tsrc = S->model == 1 ? ws->tp : te;
+    if (S->norm_flag) {
+        normalize_backward(hsrc, ws->hpn, gv, ga, d);
+        normalize_backward(re, ws->rn, gv, gb, d);
+        normalize_backward(tsrc, ws->tpn, tmp, gc, d);
+    } else {
+        memcpy(ga, gv, sizeof(float) * (size_t)d);
+        memcpy(gb, gv, sizeof(float) * (size_t)d);
+        memcpy(gc, tmp, sizeof(float) * (size_t)d);
+    }
+    if (S->model == 1) {
+        /* e_perp = e - (e.n) n:  g_e = g_p - n (n.g_p);  g_n = -((e.n) g_p + (n.g_p) e), per _transfer call,
+         * each through its own F.normalize(norm) backward */
+        const float nga = vdot(ws->nw, ga, d), ngc = vdot(ws->nw, gc, d);
+        for (int64_t i = 0; i < d; ++i) {
+            tmp[i] = -(ws->hdot * ga[i] + nga * he[i]);
+            gv[i] = -(ws->tdot * gc[i] + ngc * te[i]);
+        }
+        normalize_backward(W, ws->wn, tmp, x1, d);
+        normalize_backward(W, ws->wn, gv, x2, d);
+        float *gw = S->gw + s * d;
+        for (int64_t i = 0; i < d; ++i) {
+            gw[i] = x1[i] + x2[i];
+            ga[i] = ga[i] - ws->nw[i] * nga;
+            gc[i] = gc[i] - ws->nw[i] * ngc;
+        }
+    }
+}
+
+/* step 4 + 5 for one row: the listed slots' rows summed in slot order (per lookup), then the update */
+static void row_update(const ostep *S, float *w, float *acc, const float *ga, const int64_t *la, int64_t na,
+                       const float *gb, const int64_t *lb, int64_t nb, float *g) {
+    const int64_t d = S->d;
+    for (int64_t i = 0; i < d; ++i) {
+        float a = 0.0f, b = 0.0f;
+        for (int64_t k = 0; k < na; ++k) a += ga[la[k] * d + i];
+        for (int64_t k = 0; k < nb; ++k) b += gb[lb[k] * d + i];
+        g[i] = nb ? a + b : a;
+    }
+    apply_update(S->opt, S->lr, w, acc, g, d);
+}
+
+/* counting sort of the slots with ds != 0 by key (stable: slots ascending inside a key) */
+static void slot_csr(const ostep *S, const int64_t *key, int64_t nkeys, int64_t *off, int64_t *list) {
+    memset(off, 0, sizeof(int64_t) * (size_t)(nkeys + 1));
+    for (int64_t s = 0; s < S->seq; ++s)
+        if (S->ds[s] != 0.0f) off[key[s] + 1] += 1;
+    for (int64_t k = 0; k < nkeys; ++k) off[k + 1] += off[k];
+    int64_t *cur = malloc(sizeof(int64_t) * (size_t)(nkeys ? nkeys : 1));
+    memcpy(cur, off, sizeof(int64_t) * (size_t)nkeys);
+    for (int64_t s = 0; s < S->seq; ++s)
+        if (S->ds[s] != 0.0f) list[cur[key[s]]++] = s;
+    free(cur);
+}
+
+typedef struct {
+    const ostep *S;
+    int phase;
+    int64_t lo, hi;
+} ojob;
+
+static void run_range(const ostep *S, int phase, int64_t lo, int64_t hi) {
+    const int64_t d = S->d;
+    float *buf = calloc((size_t)(12 * d), sizeof(float));
+    slot_ws ws;
+    slot_ws_bind(&ws, buf, d);
+    float *tmpb = buf + 7 * d;
+    if (phase == 0) {
+        for (int64_t s = lo; s < hi; ++s)
+            S->score[s] = slot_forward(S->model, S->p, S->norm_flag, 0, &ws, S->ent + S->h[s] * d,
+                                       S->ent + S->t[s] * d, S->rel + S->r[s] * d,
+                                       S->model == 1 ? S->normv + S->r[s] * d : NULL);
+    } else if (phase == 1) {
+        for (int64_t s = lo; s < hi; ++s)
+            if (S->ds[s] != 0.0f) slot_backward(S, &ws, tmpb, s);
+    } else {
+        /* rows: entities [0, E), relations [E, E + R), norm_vector rows [E + R, E + 2R) */
+        for (int64_t q = lo; q < hi; ++q) {
+            if (q < S->E) {
+                const int64_t na = S->hoff[q + 1] - S->hoff[q], nb = S->toff[q + 1] - S->toff[q];
+                if (na + nb == 0) continue;
+                /* the two lookups' dense gradients added: a row only one lookup touched is that lookup's sum */
+                if (na)
+                    row_update(S, S->ent + q * d, S->opt ? S->ent_acc + q * d : NULL, S->gh, S->hlist + S->hoff[q], na,
+                               S->gt, S->tlist + S->toff[q], nb, tmpb);
+                else
+                    row_update(S, S->ent + q * d, S->opt ? S->ent_acc + q * d : NULL, S->gt, S->tlist + S->toff[q], nb,
+                               S->gt, NULL, 0, tmpb);
+            } else if (q < S->E + S->R) {
+                const int64_t k = q - S->E, n = S->roff[k + 1] - S->roff[k];
+                if (n)
+                    row_update(S, S->rel + k * d, S->opt ? S->rel_acc + k * d : NULL, S->gr, S->rlist + S->roff[k], n,
+                               S->gr, NULL, 0, tmpb);
+            } else {
+                const int64_t k = q - S->E - S->R, n = S->roff[k + 1] - S->roff[k];
+                if (n)
+                    row_update(S, S->normv + k * d, S->opt ? S->norm_acc + k * d : NULL, S->gw, S->rlist + S->roff[k],
+                               n, S->gw, NULL, 0, tmpb);
+            }
+        }
+    }
+    free(buf);
+}
+
+static void *run_job(void *arg) {
+    const ojob *j = (const ojob *)arg;
+    run_range(j->S, j->phase, j->lo, j->hi);
+    return NULL;
+}
+
+static void parallel_phase(const ostep *S, int phase, int64_t n, int64_t workers) {
+    if (workers <= 1 || n < 2 * workers) {
+        run_range(S, phase, 0, n);
+        return;
+    }
+    pthread_t th[256];
+    ojob jobs[256];
+    if (workers > 256) workers = 256;
+    for (int64_t w = 0; w < workers; ++w) {
+        jobs[w].S = S;
+        jobs[w].phase = phase;
+        jobs[w].lo = n * w / workers;
+        jobs[w].hi = n * (w + 1) / workers;
+        pthread_create(&th[w], NULL, run_job, &jobs[w]);
+    }
+    for (int64_t w = 0; w < workers; ++w) pthread_join(th[w], NULL);
+}
+
+static void ostep_reserve(ostep *S) {
+    const int64_t seq = S->seq, d = S->d;
+    if (seq > S->cap_seq || d != S->cap_d) {
+        free(S->score); free(S->ds); free(S->gh); free(S->gt); free(S->gr); free(S->gw);
+        free(S->hlist); free(S->tlist); free(S->rlist);
+        S->score = malloc(sizeof(float) * (size_t)seq);
+        S->ds = malloc(sizeof(float) * (size_t)seq);
+        S->gh = malloc(sizeof(float) * (size_t)(seq * d));
+        S->gt = malloc(sizeof(float) * (size_t)(seq * d));
+        S->gr = malloc(sizeof(float) * (size_t)(seq * d));
+        S->gw = malloc(sizeof(float) * (size_t)(seq * d));
+        S->hlist = malloc(sizeof(int64_t) * (size_t)seq);
+        S->tlist = malloc(sizeof(int64_t) * (size_t)seq);
+        S->rlist = malloc(sizeof(int64_t) * (size_t)seq);
+        S->cap_seq = seq;
+        S->cap_d = d;
+    }
+    if (S->E > S->cap_e) {
+        free(S->hoff); free(S->toff);
+        S->hoff = malloc(sizeof(int64_t) * (size_t)(S->E + 1));
+        S->toff = malloc(sizeof(int64_t) * (size_t)(S->E + 1));
+        S->cap_e = S->E;
+    }
+    if (S->R > S->cap_r) {
+        free(S->roff);
+        S->roff = malloc(sizeof(int64_t) * (size_t)(S->R + 1));
+        S->cap_r = S->R;
+    }
+}
+
+static void ostep_release(ostep *S) {
+    free(S->score); free(S->ds); free(S->gh); free(S->gt); free(S->gr); free(S->gw);
+    free(S->hlist); free(S->tlist); free(S->rlist); free(S->hoff); free(S->toff); free(S->roff);
+}
+
+static float ostep_run(ostep *S, int64_t workers) {
+    ostep_reserve(S);
+    const int64_t bs = S->bs, neg = S->neg, seq = S->seq;
+    parallel_phase(S, 0, seq, workers);
+    /* MarginLoss: mean(max(p - n, -m)) + m; NegativeSampling reshape n[i][k] = score[bs + k*bs + i] */
+    double lsum = 0;
+    const float inv = 1.0f / (float)(bs * neg), margin = S->margin;
+    memset(S->ds, 0, sizeof(float) * (size_t)seq);
+    for (int64_t i = 0; i < bs; ++i)
+        for (int64_t k = 0; k < neg; ++k) {
+            const float a = S->score[i] - S->score[bs + k * bs + i];
+            const float mx = a > -margin ? a : -margin;
+            lsum += mx;
+            const float c = a > -margin ? inv : (a == -margin ? inv / 2 : 0.0f);
+            S->ds[i] += c;
+            S->ds[bs + k * bs + i] -= c;
+        }
+    const float loss = (float)(lsum / (double)(bs * neg)) + margin;
+    parallel_phase(S, 1, seq, workers);
+    slot_csr(S, S->h, S->E, S->hoff, S->hlist);
+    slot_csr(S, S->t, S->E, S->toff, S->tlist);
+    slot_csr(S, S->r, S->R, S->roff, S->rlist);
+    parallel_phase(S, 2, S->E + S->R * (S->model == 1 ? 2 : 1), workers);
+    return loss;
+}
+
 float oracle_train_step(int model, int p, int norm_flag, int opt, float lr, float margin, int64_t E, int64_t R,
                         int64_t d, float *ent, float *rel, float *normv, float *ent_acc, float *rel_acc,
                         float *norm_acc, const int64_t *h, const int64_t *t, const int64_t *r, int64_t bs,
                         int64_t neg) {
-    int64_t seq = bs * (1 + neg);
-    float *score = malloc(sizeof(float) * (size_t)seq);
-    float *ds = calloc((size_t)seq, sizeof(float));
-    float *ge = calloc((size_t)(E * d), sizeof(float)), *gr = calloc((size_t)(R * d), sizeof(float));
-    float *gw = model == 1 ? calloc((size_t)(R * d), sizeof(float)) : NULL;
-    float *buf = calloc((size_t)(20 * d), sizeof(float));
-    slot_ws ws = {d, 0, 0, 0, 0, buf, buf + d, buf + 2 * d, buf + 3 * d, buf + 4 * d, buf + 5 * d, buf + 6 * d,
-                  0, 0, 0, 0, 0, 0, 0, 0};
-    float *gv = buf + 7 * d, *ga = buf + 8 * d, *gb = buf + 9 * d, *gc = buf + 10 * d, *gn = buf + 11 * d;
-    float *tmp = buf + 12 * d;
-    const float *W = normv;
-    /* forward, all slots with pre-step tables (Trainer.py:44-56 is minibatch-synchronous) */
-    for (int64_t s = 0; s < seq; ++s)
-        score[s] = slot_forward(model, p, norm_flag, 0, &ws, ent + h[s] * d, ent + t[s] * d, rel + r[s] * d,
-                                model == 1 ? W + r[s] * d : NULL);
-    /* MarginLoss: mean(max(p - n, -m)) + m; NegativeSampling reshape n[i][k] = score[bs + k*bs + i] */
-    double lsum = 0;
-    float inv = 1.0f / (float)(bs * neg);
-    for (int64_t i = 0; i < bs; ++i)
-        for (int64_t k = 0; k < neg; ++k) {
-            float a = score[i] - score[bs + k * bs + i];
-            float mx = a > -margin ? a : -margin;
-            lsum += mx;
-            float c = a > -margin ? inv : (a == -margin ? inv / 2 : 0.0f);
-            ds[i] += c;
-            ds[bs + k * bs + i] -= c;
-        }
-    float loss = (float)(lsum / (double)(bs * neg)) + margin;
-    /* backward per slot, scatter-sum into dense grads (embedding_dense_backward) */
-    for (int64_t s = 0; s < seq; ++s) {
-        if (ds[s] == 0.0f) continue;
-        const float *he = ent + h[s] * d, *te = ent + t[s] * d, *re = rel + r[s] * d;
-        float sc = slot_forward(model, p, norm_flag, 0, &ws, he, te, re, model == 1 ? W + r[s] * d : NULL);
-        for (int64_t i = 0; i < d; ++i) {
-            if (p == 1) gv[i] = ws.v[i] > 0 ? ds[s] : (ws.v[i] < 0 ? -ds[s] : 0.0f);
-            else gv[i] = sc == 0.0f ? 0.0f : ws.v[i] * (ds[s] / sc);
-        }
-        /* d/d(nh) = gv, d/d(nr) = gv, d/d(nt) = -gv */
-        for (int64_t i = 0; i < d; ++i) tmp[i] = -gv[i];
-        const float *hsrc = model == 1 ? ws.hp : he, *tsrc = model == 1 ? ws.tp : te;
-        if (norm_flag) {
-            normalize_backward(hsrc, ws.hpn, gv, ga, d);
-            normalize_backward(re, ws.rn, gv, gb, d);
-            normalize_backward(tsrc, ws.tpn, tmp, gc, d);
+    return oracle_train_step_mt(model, p, norm_flag, opt, lr, margin, E, R, d, ent, rel, normv, ent_acc, rel_acc,
+                                norm_acc, h, t, r, bs, neg, 1);
+}
+
+float oracle_train_step_mt(int model, int p, int norm_flag, int opt, float lr, float margin, int64_t E, int64_t R,
+                           int64_t d, float *ent, float *rel, float *normv, float *ent_acc, float *rel_acc,
+                           float *norm_acc, const int64_t *h, const int64_t *t, const int64_t *r, int64_t bs,
+                           int64_t neg, int64_t workers) {
+    ostep S;
+    memset(&S, 0, sizeof(S));
+    S.model = model; S.p = p; S.norm_flag = norm_flag; S.opt = opt; S.lr = lr; S.margin = margin;
+    S.E = E; S.R = R; S.d = d; S.bs = bs; S.neg = neg; S.seq = bs * (1 + neg);
+    S.ent = ent; S.rel = rel; S.normv = normv; S.ent_acc = ent_acc; S.rel_acc = rel_acc; S.norm_acc = norm_acc;
+    S.h = h; S.t = t; S.r = r;
+    const float loss = ostep_run(&S, workers);
+    ostep_release(&S);
+    return loss;
+}
+
+/* the sampler threads' slices of one sampling() call on `workers` threads (each slice owns its stream,
+ * Base.cpp:280-298, so the batch is the same as oracle_sampling's) */
+typedef struct {
+    const okg *g;
+    uint64_t *states;
+    int64_t threads, bs, neg, bern, filter, id0, id1;
+    int64_t *h, *t, *r;
+    float *y;
+} osamp;
+
+static void *samp_job(void *arg) {
+    const osamp *a = (const osamp *)arg;
+    for (int64_t id = a->id0; id < a->id1; ++id) {
+        /* one sampler thread = oracle_sampling_sides restricted to thread id's slice */
+        int64_t lef, rig;
+        if (a->bs % a->threads == 0) {
+            lef = id * (a->bs / a->threads);
+            rig = (id + 1) * (a->bs / a->threads);
         } else {
-            memcpy(ga, gv, sizeof(float) * (size_t)d);
-            memcpy(gb, gv, sizeof(float) * (size_t)d);
-            memcpy(gc, tmp, sizeof(float) * (size_t)d);
+            lef = id * (a->bs / a->threads + 1);
+            rig = (id + 1) * (a->bs / a->threads + 1);
+            if (rig > a->bs) rig = a->bs;
         }
-        float *Ge_h = ge + h[s] * d, *Ge_t = ge + t[s] * d, *Gr = gr + r[s] * d;
-        for (int64_t i = 0; i < d; ++i) Gr[i] += gb[i];
-        if (model == 1) {
-            /* e_perp = e - (e.n) n:  g_e = g_p - n (n.g_p);  g_n = -((e.n) g_p + (n.g_p) e) */
-            float nga = vdot(ws.nw, ga, d), ngc = vdot(ws.nw, gc, d);
-            for (int64_t i = 0; i < d; ++i) {
-                Ge_h[i] += ga[i] - ws.nw[i] * nga;
-                Ge_t[i] += gc[i] - ws.nw[i] * ngc;
-                gn[i] = -(ws.hdot * ga[i] + nga * he[i]) - (ws.tdot * gc[i] + ngc * te[i]);
-            }
-            normalize_backward(W + r[s] * d, ws.wn, gn, tmp, d);
-            float *Gw = gw + r[s] * d;
-            for (int64_t i = 0; i < d; ++i) Gw[i] += tmp[i];
-        } else {
-            for (int64_t i = 0; i < d; ++i) {
-                Ge_h[i] += ga[i];
-                Ge_t[i] += gc[i];
+        if (lef >= rig) continue;
+        uint64_t *s = &a->states[id];
+        const okg *g = a->g;
+        float prob = 500;
+        for (int64_t b = lef; b < rig; ++b) {
+            int64_t i = lcg_max(s, g->train_total);
+            otriple pp = g->train_list[i];
+            a->h[b] = pp.h; a->t[b] = pp.t; a->r[b] = pp.r; a->y[b] = 1;
+            int64_t last = a->bs;
+            for (int64_t k = 0; k < a->neg; ++k) {
+                if (a->bern) prob = 1000 * g->right_mean[pp.r] / (g->right_mean[pp.r] + g->left_mean[pp.r]);
+                if ((float)(lcg_next(s) % 1000) < prob) {
+                    a->h[b + last] = pp.h;
+                    a->t[b + last] = a->filter ? corrupt_filtered(g, 1, pp.h, pp.r, s) : corrupt_plain(g, pp.h, s);
+                } else {
+                    a->h[b + last] = a->filter ? corrupt_filtered(g, 0, pp.t, pp.r, s) : corrupt_plain(g, pp.t, s);
+                    a->t[b + last] = pp.t;
+                }
+                a->r[b + last] = pp.r;
+                a->y[b + last] = -1;
+                last += a->bs;
             }
         }
     }
-    apply_update(opt, lr, ent, ent_acc, ge, E * d);
-    apply_update(opt, lr, rel, rel_acc, gr, R * d);
-    if (model == 1) apply_update(opt, lr, normv, norm_acc, gw, R * d);
-    free(score); free(ds); free(ge); free(gr); free(gw); free(buf);
-    return loss;
+    return NULL;
+}
+
+static void sampling_mt(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
+                        int64_t filter, int64_t *h, int64_t *t, int64_t *r, float *y, int64_t workers) {
+    if (workers > threads) workers = threads;
+    if (workers <= 1) {
+        oracle_sampling(g, states, threads, bs, neg, bern, filter, h, t, r, y);
+        return;
+    }
+    pthread_t th[64];
+    osamp a[64];
+    for (int64_t w = 0; w < workers; ++w) {
+        a[w] = (osamp){g, states, threads, bs, neg, bern, filter, threads * w / workers, threads * (w + 1) / workers,
+                       h, t, r, y};
+        pthread_create(&th[w], NULL, samp_job, &a[w]);
+    }
+    for (int64_t w = 0; w < workers; ++w) pthread_join(th[w], NULL);
+}
+
+int64_t oracle_train_loop_mt(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
+                             int64_t filter, int model, int p, int norm_flag, int opt, float lr, float margin,
+                             int64_t d, float *ent, float *rel, float *normv, float *ent_acc, float *rel_acc,
+                             float *norm_acc, int64_t steps, int64_t workers, float *losses) {
+    int64_t seq = bs * (1 + neg);
+    int64_t *h = malloc(sizeof(int64_t) * (size_t)seq), *t = malloc(sizeof(int64_t) * (size_t)seq);
+    int64_t *r = malloc(sizeof(int64_t) * (size_t)seq);
+    float *y = malloc(sizeof(float) * (size_t)seq);
+    ostep S;
+    memset(&S, 0, sizeof(S));
+    S.model = model; S.p = p; S.norm_flag = norm_flag; S.opt = opt; S.lr = lr; S.margin = margin;
+    S.E = g->ent_total; S.R = g->rel_total; S.d = d; S.bs = bs; S.neg = neg; S.seq = seq;
+    S.ent = ent; S.rel = rel; S.normv = normv; S.ent_acc = ent_acc; S.rel_acc = rel_acc; S.norm_acc = norm_acc;
+    S.h = h; S.t = t; S.r = r;
+    for (int64_t s = 0; s < steps; ++s) {
+        sampling_mt(g, states, threads, bs, neg, bern, filter, h, t, r, y, workers);
+        const float l = ostep_run(&S, workers);
+        if (losses) losses[s] = l;
+    }
+    ostep_release(&S);
+    free(h); free(t); free(r); free(y);
+    return steps * seq;
 }
 
 int64_t oracle_train_loop(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
                           int64_t filter, int model, int p, int norm_flag, int opt, float lr, float margin, int64_t d,
                           float *ent, float *rel, float *normv, float *ent_acc, float *rel_acc, float *norm_acc,
                           int64_t steps) {
-    int64_t seq = bs * (1 + neg);
-    int64_t *h = malloc(sizeof(int64_t) * (size_t)seq), *t = malloc(sizeof(int64_t) * (size_t)seq);
-    int64_t *r = malloc(sizeof(int64_t) * (size_t)seq);
-    float *y = malloc(sizeof(float) * (size_t)seq);
-    for (int64_t s = 0; s < steps; ++s) {
-        oracle_sampling(g, states, threads, bs, neg, bern, filter, h, t, r, y);
-        oracle_train_step(model, p, norm_flag, opt, lr, margin, g->ent_total, g->rel_total, d, ent, rel, normv,
-                          ent_acc, rel_acc, norm_acc, h, t, r, bs, neg);
-    }
-    free(h); free(t); free(r); free(y);
-    return steps * seq;
+    return oracle_train_loop_mt(g, states, threads, bs, neg, bern, filter, model, p, norm_flag, opt, lr, margin, d,
+                                ent, rel, normv, ent_acc, rel_acc, norm_acc, steps, 1, NULL);
 }
 
 /* ---------------------------------------------------------------- link prediction ------------- */

@@ -65,6 +65,13 @@ float oracle_train_step(int model, int p_norm, int norm_flag, int opt, float lr,
                         float *rel_acc, float *norm_acc, const int64_t *h, const int64_t *t, const int64_t *r,
                         int64_t bs, int64_t neg);
 
+/* The same step on `workers` threads (scores, per-slot gradient rows and per-row sums in parallel; every
+ * float sum keeps its order, so the result is bit-identical to oracle_train_step). */
+float oracle_train_step_mt(int model, int p_norm, int norm_flag, int opt, float lr, float margin, int64_t ent_total,
+                           int64_t rel_total, int64_t dim, float *ent, float *rel, float *normv, float *ent_acc,
+                           float *rel_acc, float *norm_acc, const int64_t *h, const int64_t *t, const int64_t *r,
+                           int64_t bs, int64_t neg, int64_t workers);
+
 /* Scores as model.predict(...) computes them; mode 0 normal, 1 head_batch, 2 tail_batch (TransE.py:46-60). */
 void oracle_score(int model, int p_norm, int norm_flag, int mode, int64_t dim, const float *ent, const float *rel,
                   const float *normv, const int64_t *h, const int64_t *t, const int64_t *r, int64_t n, float *out);
@@ -86,6 +93,12 @@ int64_t oracle_train_loop(const okg *g, uint64_t *states, int64_t threads, int64
                           int64_t filter, int model, int p_norm, int norm_flag, int opt, float lr, float margin,
                           int64_t dim, float *ent, float *rel, float *normv, float *ent_acc, float *rel_acc,
                           float *norm_acc, int64_t steps);
+/* the same loop with the sampler slices and the step phases on `workers` threads (bit-identical results);
+ * losses (optional) receives each step's loss */
+int64_t oracle_train_loop_mt(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,
+                             int64_t filter, int model, int p_norm, int norm_flag, int opt, float lr, float margin,
+                             int64_t dim, float *ent, float *rel, float *normv, float *ent_acc, float *rel_acc,
+                             float *norm_acc, int64_t steps, int64_t workers, float *losses);
 /* type-constrained counts and metrics of testHead/testTail/test_link_prediction (Test.h:127-502); type
  * lists per relation [lef, rig) as importTypeFiles builds them (Reader.h:352-396) */
 void oracle_rank_constrained(int64_t E, const int64_t *ah, const int64_t *at, const int64_t *ar, int64_t n_all,
