@@ -203,6 +203,8 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
     uset = ctypes.c_void_p()
     _native.check(L.pt_universe_set_create(arr, len(jobs), mid, p_norm, 1, _native.PT_ADAGRAD, 0, 0,
                                            ctypes.byref(uset)))
+    if os.environ.get("PT_UNI_PROF") == "1":
+        _native.check(L.pt_universe_set_profiling(uset, 1))
     total_epochs = sum(int(j.epochs) for j in jobs)
     losses = torch.zeros(max(total_epochs, 1), device=dev)
     stream = _native.stream()

@@ -102,6 +102,11 @@ int pt_trainer_step(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg,
 int pt_trainer_run(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, int64_t bern, int64_t filter,
                    int64_t steps, float *d_losses, void *stream);
 
+/* Sampling path of the trainer's in-kernel-sampled chunks (neg >= 4): path = PT_PATH_FUSED / PT_PATH_PART /
+ * PT_PATH_TWO_PASS (where its LDS plan fits) or -1 (automatic: fused for chunks of >= 96 steps, else the split
+ * sampler); parts = workgroups per call of the split sampler (0 = automatic, ceil(512 / calls)). Every path
+ * draws the same batches (bit-exact); this selects only how. */
+int pt_trainer_set_sampling(pt_trainer *t, int32_t path, int64_t parts);
 /* Reference-order (deterministic) mode of a trainer: every later pt_trainer_step / pt_trainer_run sums each
  * table row's gradient in slot order, lookup by lookup (batch_h, batch_t, batch_r; norm_vector(batch_r)),
  * as torch's embedding_dense_backward + AccumulateGrad do for Trainer.train_one_step (Trainer.py:44-56),
@@ -194,10 +199,13 @@ int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, int32_t model
  * [sum of epochs] floats, job-order concatenation of Trainer.run's per-epoch loss sums */
 int pt_universe_set_train(pt_universe_set *s, float *d_losses, void *stream);
 int pt_universe_set_free(pt_universe_set *s);
-/* diagnostics of a set created with PT_UNI_PROF=1 in the environment: out[n][8], per universe (in the
- * set's launch order) shader-clock cycles spent in epoch presampling, phase A, phase B, the step count,
- * batch size, dim and entity count (last train call; out[.][7] unused) */
+/* per-universe cycle counters of the fast kernel (on = 1; off by default) and their readout: out[n][8], per
+ * universe (in the set's launch order) shader-clock cycles spent in epoch presampling, phase A, phase B, the
+ * step count, batch size, dim and entity count (last train call; out[.][7] unused) */
+int pt_universe_set_profiling(pt_universe_set *s, int32_t on);
 int pt_universe_set_profile(pt_universe_set *s, uint64_t *out);
+/* the current LCG states of job `job` (input order) of a set: `threads` values (host copy; synchronizes) */
+int pt_universe_set_states(pt_universe_set *s, int64_t job, uint64_t *out);
 /* reference-order (deterministic) mode of a set (see pt_trainer_set_deterministic): one workgroup per
  * universe runs its steps with the ordered per-row sums; its workspace is allocated on first use */
 int pt_universe_set_deterministic(pt_universe_set *s, int32_t on);

@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "tuning.h"
 #include "device.h"
 #include "graph.h"
 #include "kernels.h"
@@ -209,7 +210,7 @@ __global__ __launch_bounds__(256) void k_apply_buf(ApplyParams A) {
 #pragma unroll
             for (int q = 0; q < NC; ++q)
                 bload(c[u][q], c_rs,
-                      c0[u] + j + q < c1[u] ? (uint32_t)((A.dbg & 8) ? (c0[u] + j + q) & 4095 : c0[u] + j + q) * rowb
+                      c0[u] + j + q < c1[u] ? (uint32_t)(PT_ABLATE(A.dbg, 8) ? (c0[u] + j + q) & 4095 : c0[u] + j + q) * rowb
                                             : kOob,
                       D, lane);
 #pragma unroll
@@ -391,7 +392,7 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
     for (int i = 0; i < A.ntab; ++i) rows += A.t[i].rows;
     // float4 rows through raw buffers (PT_APPLY_OLD=1 keeps the kernels below)
     static const bool old_apply = [] {
-        const char *v = getenv("PT_APPLY_OLD");
+        const char *v = pt_tuning_env("PT_APPLY_OLD");
         return v && atoi(v) != 0;
     }();
     int64_t con_rows = 0;
@@ -405,8 +406,8 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
         // contribution rows in flight per lane group: 8 for one-chunk float4 rows (C2: the bucket of a row
         // - Poisson, mean 3.6 at C2 - mostly in one round trip; measured 12.0 vs 12.6 us), else 4
         int nc = G == 64 && KCH == 1 ? 8 : 4, rpw = 1;
-        if (const char *v = getenv("PT_APPLY_NC")) nc = atoi(v);
-        if (const char *v = getenv("PT_APPLY_RPW")) rpw = atoi(v);
+        if (const char *v = pt_tuning_env("PT_APPLY_NC")) nc = atoi(v);
+        if (const char *v = pt_tuning_env("PT_APPLY_RPW")) rpw = atoi(v);
         const int64_t gpb4 = 256 / G;
         const int64_t groups = (rows + rpw - 1) / rpw;
         const dim3 grid((unsigned)((groups + gpb4 - 1) / gpb4)), block(256);
@@ -424,7 +425,7 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
     const int64_t gpb = 256 / s.G;
     // PT_APPLY_RPW=2|4: several rows per lane group with one contribution stream (measured slower on
     // C2: 20.4 / 22.0 us vs 16.8 us for one row per group, which stays the default)
-    const char *rpw_env = getenv("PT_APPLY_RPW");
+    const char *rpw_env = pt_tuning_env("PT_APPLY_RPW");
     const int rpw = rpw_env ? atoi(rpw_env) : 1;
     if (rpw == 4 || rpw == 2) {
         const int64_t groups = (rows + rpw - 1) / rpw;

@@ -13,6 +13,7 @@
 #include <queue>
 #include <vector>
 
+#include "tuning.h"
 #include "common.h"
 #include "graph.h"
 #include "kernels.h"
@@ -73,6 +74,9 @@ struct pt_trainer {
     int device = -1;
     hipStream_t cap = nullptr;
     std::map<GraphKey, hipGraphExec_t> graphs;
+    int path_override = -1;                             // pt_trainer_set_sampling: PT_PATH_* or -1 (automatic)
+    int64_t parts_override = 0;                         // split-sampler workgroups per call (0: automatic)
+    int64_t prof_calls = 0, prof_parts = 0, prof_cap = 0;   // PT_PART_PROF (tuning build) record layout
     // reference-order (deterministic) mode: ordered.hip's step on k_sample batches (pt_trainer_set_deterministic)
     bool ordered = false;
     void *ord_block = nullptr;
@@ -119,14 +123,14 @@ int desc_to_params(const pt_model_desc *m, pt::StepParams &P) {
     P.dim = m->dim;
     P.ent = m->ent; P.rel = m->rel; P.normv = m->normv;
     P.ent_acc = m->ent_acc; P.rel_acc = m->rel_acc; P.norm_acc = m->norm_acc;
-    if (const char *v = getenv("PT_STEP_DBG")) P.dbg = atoi(v);
+    if (const char *v = pt_tuning_env("PT_STEP_DBG")) P.dbg = atoi(v);
     return PT_OK;
 }
 
 // negatives at or above this count take the counting-sort path (PT_CSR=0/1 overrides)
 bool use_csr(int64_t neg) {
     static int forced = [] {
-        const char *v = getenv("PT_CSR");
+        const char *v = pt_tuning_env("PT_CSR");
         return v ? atoi(v) : -1;
     }();
     return forced >= 0 ? forced != 0 : neg >= 4;
@@ -292,27 +296,29 @@ static const int64_t kSampleSortMinCalls = 96;
 // the split sampler (k_sample_part) runs ceil(kPartTarget / calls) workgroups per call
 static const int64_t kPartTarget = 512;
 
-// Sampling path for a chunk of `calls` steps: PT_SAMPLE_MODE = fused | part | twopass forces one (where
-// its plan fits; PT_SAMPLE_TWO_PASS=1 is the old switch for twopass); by default the fused kernel for
-// chunks of >= kSampleSortMinCalls steps, the split sampler below that.
-static int sample_mode() {
-    const char *tp = getenv("PT_SAMPLE_TWO_PASS");
+// Sampling path for a chunk of `calls` steps: pt_trainer_set_sampling forces one (where its plan fits;
+// the tuning build also reads PT_SAMPLE_MODE = fused | part | twopass and PT_SAMPLE_TWO_PASS=1); by default
+// the fused kernel for chunks of >= kSampleSortMinCalls steps, the split sampler below that.
+static int sample_mode(const pt_trainer *t) {
+    if (t->path_override >= 0) return t->path_override;
+    const char *tp = pt_tuning_env("PT_SAMPLE_TWO_PASS");
     if (tp && atoi(tp) != 0) return PT_PATH_TWO_PASS;
-    const char *v = getenv("PT_SAMPLE_MODE");
+    const char *v = pt_tuning_env("PT_SAMPLE_MODE");
     if (!v) return -1;
     if (!strcmp(v, "fused")) return PT_PATH_FUSED;
     if (!strcmp(v, "part")) return PT_PATH_PART;
     if (!strcmp(v, "twopass")) return PT_PATH_TWO_PASS;
     return -1;
 }
-static int64_t part_count(int64_t calls, int64_t bs) {
+static int64_t part_count(const pt_trainer *t, int64_t calls, int64_t bs) {
     int64_t p = (kPartTarget + calls - 1) / calls;
-    if (const char *v = getenv("PT_PART_COUNT")) p = atoll(v);
+    if (t->parts_override > 0) p = t->parts_override;
+    else if (const char *v = pt_tuning_env("PT_PART_COUNT")) p = atoll(v);
     if (p < 2) p = 2;
     return p > bs ? bs : p;
 }
 static int choose_path(const pt_trainer *t, int64_t calls, int64_t bs, int64_t neg, int forced) {
-    const bool part_ok = t->csr_part && pt::sample_part_fits(bs, neg, t->P.ent_total, part_count(calls, bs));
+    const bool part_ok = t->csr_part && pt::sample_part_fits(bs, neg, t->P.ent_total, part_count(t, calls, bs));
     if (forced == PT_PATH_FUSED && t->csr_fused) return PT_PATH_FUSED;
     if (forced == PT_PATH_PART && part_ok) return PT_PATH_PART;
     if (forced == PT_PATH_TWO_PASS) return PT_PATH_TWO_PASS;
@@ -363,10 +369,13 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     // (sets the kernels' LDS attributes here, outside any stream capture)
     t->csr_fused = pt::sample_sort_prepare(bs, neg, E, ss);
     t->csr_part = pt::sample_part_prepare(bs, neg, E, std::min<int64_t>(bs, kPartTarget));
-    if (const char *dd = getenv("PT_PART_DBG")) t->csr.dbg = atoi(dd);
+    if (const char *dd = pt_tuning_env("PT_PART_DBG")) t->csr.dbg = atoi(dd);
     // PT_PART_PROF=1: phase timestamps of the split sampler (reported by pt_trainer_run_timed)
-    if (const char *pp = getenv("PT_PART_PROF")) {
-        if (atoi(pp) != 0 && !t->csr.prof) PT_HIP(hipMalloc(&t->csr.prof, sizeof(uint64_t) * 8 * kCsrChunk * 1024));
+    if (const char *pp = pt_tuning_env("PT_PART_PROF")) {
+        if (atoi(pp) != 0 && !t->csr.prof) {
+            t->prof_cap = kCsrChunk * 1024;   // (call, part) records
+            PT_HIP(hipMalloc(&t->csr.prof, sizeof(uint64_t) * 8 * (size_t)t->prof_cap));
+        }
     }
     return PT_OK;
 }
@@ -427,8 +436,15 @@ static int enqueue_sample_chunk(pt_trainer *t, pt_sampler *s, pt::CsrWork &w, in
                                            t->P.ent_total, w, st));
         PT_TIMED(1, pt::launch_advance(s->d_states, s->threads, bs, dpp * calls, st));
     } else if (path == PT_PATH_PART) {
+        const int64_t parts = part_count(t, calls, bs);
+        pt::CsrWork wp = w;
+        if (wp.prof && calls * parts > t->prof_cap) wp.prof = nullptr;   // record only what the buffer holds
+        if (wp.prof) {
+            t->prof_calls = calls;
+            t->prof_parts = parts;
+        }
         PT_TIMED(0, pt::launch_sample_part(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls,
-                                           part_count(calls, bs), t->P.ent_total, w, st));
+                                           parts, t->P.ent_total, wp, st));
     } else {
         PT_TIMED(0, pt::launch_sample_csr(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls, w, st));
         PT_TIMED(1, pt::launch_scan_counts(w, t->P.ent_total, calls, s->d_states, s->threads, bs, dpp, st));
@@ -453,7 +469,7 @@ static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, in
         const int64_t chunk = t->csr_chunk;
         for (int64_t c0 = 0; c0 < steps; c0 += chunk) {
             const int64_t calls = std::min(chunk, steps - c0);
-            int rc = enqueue_sample_chunk(t, s, t->csr, bs, neg, bern, filter, calls, sample_mode(), st, tm);
+            int rc = enqueue_sample_chunk(t, s, t->csr, bs, neg, bern, filter, calls, sample_mode(t), st, tm);
             if (rc) return rc;
             for (int64_t j = 0; j < calls; ++j) {
                 const pt::CsrWork v = pt::csr_view(t->csr, j, bs, neg);
@@ -574,6 +590,16 @@ static int enqueue_ordered_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t
     return PT_OK;
 }
 
+extern "C" int pt_trainer_set_sampling(pt_trainer *t, int32_t path, int64_t parts) {
+    PT_CHECK(t, PT_EINVAL, "null trainer");
+    PT_CHECK(path >= -1 && path <= PT_PATH_PART, PT_EINVAL, "sampling path must be -1 or PT_PATH_FUSED/PART/TWO_PASS");
+    PT_CHECK(parts >= 0, PT_EINVAL, "parts must be >= 0");
+    t->path_override = path;
+    t->parts_override = parts;
+    t->drop_graphs();   // captured epochs hold the previous choice
+    return PT_OK;
+}
+
 extern "C" int pt_trainer_set_deterministic(pt_trainer *t, int32_t on) {
     PT_CHECK(t, PT_EINVAL, "null trainer");
     PT_CHECK(!on || pt::ordered_dim_supported(t->P.dim), PT_ENOTSUP, "reference-order mode: dim too large");
@@ -631,8 +657,8 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
         tot[std::get<0>(e)] += ms;
     }
     for (int k = 0; k < 4; ++k) ms4[k] = (float)(tot[k] / (double)steps);
-    if (t->csr.prof && t->last_path == PT_PATH_PART) {   // split sampler phases of the last chunk
-        const int64_t calls = std::min<int64_t>(steps, t->csr_chunk), parts = part_count(calls, bs);
+    if (t->csr.prof && t->last_path == PT_PATH_PART && t->prof_calls > 0) {   // split sampler phases of the last chunk
+        const int64_t calls = t->prof_calls, parts = t->prof_parts;
         std::vector<uint64_t> pr((size_t)(8 * calls * parts));
         PT_HIP(hipMemcpy(pr.data(), t->csr.prof, 8 * pr.size(), hipMemcpyDeviceToHost));
         uint64_t t0 = ~0ull, tend = 0;
@@ -746,7 +772,7 @@ extern "C" int pt_trainer_sample_csr(pt_trainer *t, pt_sampler *s, int64_t bs, i
     PT_CHECK(calls <= t->csr_chunk, PT_EINVAL, "pt_trainer_sample_csr: calls exceeds the workspace chunk");
     if (path == PT_PATH_FUSED) PT_CHECK(t->csr_fused, PT_ENOTSUP, "fused sampling plan does not fit LDS");
     if (path == PT_PATH_PART)
-        PT_CHECK(t->csr_part && pt::sample_part_fits(bs, neg, t->P.ent_total, part_count(calls, bs)), PT_ENOTSUP,
+        PT_CHECK(t->csr_part && pt::sample_part_fits(bs, neg, t->P.ent_total, part_count(t, calls, bs)), PT_ENOTSUP,
                  "split sampling plan does not fit LDS");
     hipStream_t st = (hipStream_t)stream;
     rc = enqueue_sample_chunk(t, s, t->csr, bs, neg, bern, filter, calls, path, st, nullptr);
@@ -949,6 +975,7 @@ struct pt_universe_set {
     pt::UniverseLaunch cfg;
     std::vector<pt::UniverseDev> host;    // same order; loss pointers patched per train call
     std::vector<int64_t> host_loss_off;
+    std::vector<int64_t> host_of_job;     // job index -> index in host / d_us
     uint64_t *prof = nullptr;             // PT_UNI_PROF=1: [n][8] cycle counters + shape (device)
     // reference-order (deterministic) mode (pt_universe_set_deterministic): ordered.hip's universe kernel
     bool ordered = false;
@@ -974,12 +1001,6 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     set->model = model; set->p_norm = p_norm; set->norm_flag = norm_flag; set->opt = opt;
     set->bern = bern; set->filter = filter;
     PT_HIP(hipGetDevice(&set->device));
-    if (const char *v = getenv("PT_UNI_PROF")) {
-        if (atoi(v) && n > 0) {
-            PT_HIP(hipMalloc((void **)&set->prof, 64 * (size_t)n));
-            PT_HIP(hipMemset(set->prof, 0, 64 * (size_t)n));
-        }
-    }
     int64_t neg = -1;
     // layout of the per-universe workspace in one arena
     auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
@@ -1114,10 +1135,12 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         U.fnorm = U.frel + g.rel_total;
         U.contrib = (float *)(base + slots[i].contrib);
         U.losses = nullptr;
-        U.prof = set->prof ? set->prof + 8 * (int64_t)set->host.size() : nullptr;
+        U.prof = nullptr;   // pt_universe_set_profiling
         U.threads = J.threads; U.bs = J.batch_size; U.nbatches = J.nbatches; U.epochs = J.epochs; U.dim = J.dim;
         U.lr = J.lr; U.margin = J.margin;
         U.shape = pt::universe_shape_id(J.dim, model);
+        if (set->host_of_job.empty()) set->host_of_job.assign((size_t)n, -1);
+        set->host_of_job[(size_t)i] = (int64_t)set->host.size();
         set->host.push_back(U);
         set->host_loss_off.push_back(loss_of[i]);
         max_bs = std::max(max_bs, J.batch_size);
@@ -1138,7 +1161,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     const int64_t relg_b = 4 * max_relg * (model == 1 ? 2 : 1);
     int64_t used = list_b;
     auto env_on = [](const char *name) {
-        const char *v = getenv(name);
+        const char *v = pt_tuning_env(name);
         return !v || atoi(v) != 0;
     };
     PT_CHECK(used <= lds_budget, PT_EINVAL, "universe batch too large for the LDS work list");
@@ -1163,7 +1186,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     C.lds_bytes = used;
     // agent-scope fences only while some gradient row is a global float atomic (or a flag global)
     C.agent_fence = !(C.contrib && (C.rel_list || (C.lds_relgrad && C.lds_flags)));
-    if (const char *v = getenv("PT_UNI_FENCE")) C.agent_fence = C.agent_fence || atoi(v) != 0;
+    if (const char *v = pt_tuning_env("PT_UNI_FENCE")) C.agent_fence = C.agent_fence || atoi(v) != 0;
     C.threads = 512;
     // tuning overrides (benchmarks): PT_UNI_RELGRAD / CONTRIB / LDSFLAGS / PRESAMPLE = 0 disable the
     // LDS placements above, PT_UNI_FENCE=1 forces agent-scope fences
@@ -1246,11 +1269,31 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
     return PT_OK;
 }
 
-// PT_UNI_PROF diagnostics: per universe (set order) cycles in presampling / phase A / phase B, steps,
-// batch size, dim and entities
+extern "C" int pt_universe_set_states(pt_universe_set *set, int64_t job, uint64_t *out) {
+    PT_CHECK(set && out, PT_EINVAL, "pt_universe_set_states: null argument");
+    PT_CHECK(job >= 0 && job < (int64_t)set->host_of_job.size(), PT_EINVAL, "pt_universe_set_states: bad job index");
+    const pt::UniverseDev &U = set->host[(size_t)set->host_of_job[(size_t)job]];
+    PT_HIP(hipDeviceSynchronize());
+    PT_HIP(hipMemcpy(out, U.states, sizeof(uint64_t) * (size_t)U.threads, hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+// per-universe cycle counters of the fast kernel (clock64 around its phases), off by default
+extern "C" int pt_universe_set_profiling(pt_universe_set *set, int32_t on) {
+    PT_CHECK(set, PT_EINVAL, "null universe set");
+    if (on && !set->prof && !set->host.empty()) {
+        PT_HIP(hipMalloc((void **)&set->prof, 64 * set->host.size()));
+        PT_HIP(hipMemset(set->prof, 0, 64 * set->host.size()));
+    }
+    for (size_t i = 0; i < set->host.size(); ++i) set->host[i].prof = on && set->prof ? set->prof + 8 * i : nullptr;
+    return PT_OK;
+}
+
+// diagnostics: per universe (set order) cycles in presampling / phase A / phase B, steps, batch size, dim and
+// entities of the last train call with profiling on
 extern "C" int pt_universe_set_profile(pt_universe_set *set, uint64_t *out) {
     PT_CHECK(set && out, PT_EINVAL, "null argument");
-    PT_CHECK(set->prof, PT_ESTATE, "set created without PT_UNI_PROF=1");
+    PT_CHECK(set->prof, PT_ESTATE, "profiling not enabled (pt_universe_set_profiling)");
     PT_HIP(hipDeviceSynchronize());
     PT_HIP(hipMemcpy(out, set->prof, 64 * set->host.size(), hipMemcpyDeviceToHost));
     return PT_OK;
@@ -1313,7 +1356,7 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
     int64_t n_keys = 0;
     for (int64_t i = 0; i < n_pairs; ++i) n_keys = std::max<int64_t>(n_keys, (int64_t)pairs[i].key + 1);
     int64_t batch_mb = 192;
-    if (const char *v = getenv("PT_LP_BATCH_MB")) batch_mb = std::max<int64_t>(1, atoll(v));
+    if (const char *v = pt_tuning_env("PT_LP_BATCH_MB")) batch_mb = std::max<int64_t>(1, atoll(v));
     const int64_t keys_per_batch =
         std::max<int64_t>(1, (batch_mb << 20) / (4 * std::max<int64_t>(global_ent_total, 1)));
     const int64_t n_batches = (n_keys + keys_per_batch - 1) / keys_per_batch;

@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "tuning.h"
 #include "device.h"
 #include "graph.h"
 #include "kernels.h"
@@ -136,7 +137,7 @@ __device__ __forceinline__ SlotDraw slot_prepare(const int32_t *q, int32_t k, in
     SlotDraw d;
     const uint64_t s1 = *reinterpret_cast<const uint64_t *>(q + 10);
     uint64_t s;
-    if (dbg & 2) s = s1 + k;
+    if (PT_ABLATE(dbg, 2)) s = s1 + k;
     else if (k < kJumpTab) { const Affine m = jt[k]; s = m.a * s1 + m.c; }
     else s = lcg_jump(s1, (uint64_t)(2 * k));
     d.side = (float)(lcg_next(s) % 1000ULL) < __int_as_float(q[0]) ? 1 : 0;
@@ -147,10 +148,10 @@ __device__ __forceinline__ SlotDraw slot_prepare(const int32_t *q, int32_t k, in
         const int32_t *vals = d.side ? g.head_t : g.tail_h;
         const int32_t lo = d.side ? q[1] : q[3], hi = d.side ? q[2] : q[4];
         const int32_t vlo = d.side ? q[5] : q[7], vhi = d.side ? q[6] : q[8];
-        const int64_t tmp = (dbg & 4) ? (int64_t)((uint32_t)lcg_next(s) & 8191) : rand_max(s, E - (hi - lo + 1));
+        const int64_t tmp = PT_ABLATE(dbg, 4) ? (int64_t)((uint32_t)lcg_next(s) & 8191) : rand_max(s, E - (hi - lo + 1));
         if (tmp < vlo) d.e = tmp;
         else if (tmp > vhi - hi + lo - 1) d.e = tmp + hi - lo + 1;
-        else if (dbg & 1) d.e = tmp;
+        else if (PT_ABLATE(dbg, 1)) d.e = tmp;
         else { d.search = true; d.q = run_search(vals, lo, hi, vlo, vhi, (int32_t)tmp); d.e = 0; }
     } else {
         const int64_t tmp = rand_max(s, E - 1);
@@ -850,7 +851,7 @@ hipError_t launch_sample_sort(const DeviceGraph &g, const uint64_t *states, int6
 // split sampler: threads per workgroup (PT_PART_NT = 256 | 512 | 1024 for tuning), LDS plan
 static int part_nt() {
     static const int nt = [] {
-        const char *v = getenv("PT_PART_NT");
+        const char *v = pt_tuning_env("PT_PART_NT");
         const int x = v ? atoi(v) : 512;
         return x == 256 || x == 1024 ? x : 512;
     }();

@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "tuning.h"
 #include "device.h"
 #include "graph.h"
 #include "kernels.h"
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
         auto load_chunk = [&](Vec(&E)[NCH], int64_t c0) {
 #pragma unroll
             for (int k = 0; k < NCH; ++k)
-                if (c0 + k < k_hi && !(P.dbg & 4)) vload(E[k], P.ent + (mine[c0 + k] >> 1) * D, D, lane);
+                if (c0 + k < k_hi && !PT_ABLATE(P.dbg, 4)) vload(E[k], P.ent + (mine[c0 + k] >> 1) * D, D, lane);
         };
         load_chunk(EA, k_lo);
         // ---- positive forward
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
                 }
                 if constexpr (MODEL == 0) {
                     if constexpr (CSR) {
-                        if (!(P.dbg & 1)) vstore(gs, dst, D, lane);
+                        if (!PT_ABLATE(P.dbg, 1)) vstore(gs, dst, D, lane);
                     } else {
                         sink.ent(e, gs, D, lane);
                     }
@@ -304,7 +305,7 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
             aT.x[i] -= gv.x[i];
         }
         if constexpr (MODEL == 0) {
-            if (!(P.dbg & 2)) {
+            if (!PT_ABLATE(P.dbg, 2)) {
                 sink.rel(rp, aR, D, lane);
                 sink.ent(hp, aH, D, lane);
                 sink.ent(tp, aT, D, lane);
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
             for (int u = 0; u < NCH; ++u) {
                 const int kk = k0 + u < wend ? k0 + u : wend - 1;
                 const uint32_t e = (uint32_t)(gbcast<G>(rec, kk - w0) >> 1);
-                bload(E[u], ent_rs, (P.dbg & 4) ? kOob : e * rowb, D, lane);
+                bload(E[u], ent_rs, PT_ABLATE(P.dbg, 4) ? kOob : e * rowb, D, lane);
             }
         };
         if (w0 < wend) load_chunk(EA, w0);
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
                 // slot gradient d loss / d e-hat: -g for a corrupted tail, +g for a corrupted head
                 // (g = dL/dv); an inactive pair stores zeros (the reserved slot must be defined)
                 vpnorm_bwd<true>(vk, ns, p, tail_side ? c : -c, gs);
-                bstore(gs, con_rs, (P.dbg & 1) ? kOob : slot, D, lane);
+                bstore(gs, con_rs, PT_ABLATE(P.dbg, 1) ? kOob : slot, D, lane);
                 if (tail_side) {
 #pragma unroll
                     for (int i = 0; i < Vec::N; ++i) At.x[i] -= gs.x[i];
@@ -512,7 +513,7 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
     }
     if (!active) return;
     if (lane == 0 && sink.lpart) sink.lpart[b] = lsum;
-    if (uni<G>(csum) == 0.f || (P.dbg & 2)) return;   // no active pair: every accumulator is zero
+    if (uni<G>(csum) == 0.f || PT_ABLATE(P.dbg, 2)) return;   // no active pair: every accumulator is zero
     Vec gv, aH, aR, aT, vpos;
 #pragma unroll
     for (int i = 0; i < Vec::N; ++i) vpos.x[i] = bt.x[i] - th.x[i];
@@ -595,7 +596,7 @@ int pick_nch(int64_t neg, int kch) {
 // kernel k_step_sampled); raw-buffer byte offsets must fit in 31 bits
 static bool csr_fast_path(const StepParams &P) {
     static const bool old_step = [] {
-        const char *v = getenv("PT_STEP_OLD");
+        const char *v = pt_tuning_env("PT_STEP_OLD");
         return v && atoi(v) != 0;
     }();
     const int64_t lim = int64_t(1) << 31;
@@ -644,15 +645,15 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
         const int64_t chunks = P.dim / 4;
         int G = 2;
         while (G < chunks && G < 64) G <<= 1;
-        if (const char *v = getenv("PT_STEP_G")) G = atoi(v);
+        if (const char *v = pt_tuning_env("PT_STEP_G")) G = atoi(v);
         const int KCH = (int)((chunks + G - 1) / G);
         // split a positive's negatives over S lane groups of one block (more waves in flight: the step
         // is latency-bound when one group walks all negatives)
         int S = 1;
         while (S < 4 && S * 2 <= 256 / G && P.neg >= 6 * S * 2) S *= 2;
-        if (const char *v = getenv("PT_STEP_S")) S = atoi(v);
+        if (const char *v = pt_tuning_env("PT_STEP_S")) S = atoi(v);
         int nch = 2;   // C2 (S = 4, 7 negatives per group): chunks of 2 rows, double-buffered, measured fastest
-        if (const char *v = getenv("PT_STEP_NCH")) nch = atoi(v);
+        if (const char *v = pt_tuning_env("PT_STEP_NCH")) nch = atoi(v);
 #define PT_CSTEP(G_, K_, N_, S_)                                                                       \
         if (G == G_ && KCH == K_ && nch == N_ && S == S_) {                                          \
             constexpr int NT_ = S_ * G_ >= 256 || 256 % (S_ * G_) != 0 ? S_ * G_ : 256;             \
@@ -672,16 +673,16 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
         // split a positive's negatives over 4 lane groups when there are enough of them
         // (PT_STEP_S = 1 | 2 | 4 and PT_STEP_NCH override, for tuning)
         int S = (P.neg >= 8 && 256 / s.G >= 4) ? 4 : 1;
-        if (const char *v = getenv("PT_STEP_S")) {
+        if (const char *v = pt_tuning_env("PT_STEP_S")) {
             const int want = atoi(v);
             if ((want == 1 || want == 2 || want == 4) && 256 / s.G >= want) S = want;
         }
         const int64_t nper = (P.neg + S - 1) / S;
         int nch = pick_nch(nper, s.KCH * s.VEC);
-        if (const char *v = getenv("PT_STEP_NCH")) nch = atoi(v);
+        if (const char *v = pt_tuning_env("PT_STEP_NCH")) nch = atoi(v);
         // double-buffer the negative rows when a lane group takes more than one chunk (PT_STEP_DB=0 off)
         bool db = nper > nch;
-        if (const char *v = getenv("PT_STEP_DB")) db = db && atoi(v) != 0;
+        if (const char *v = pt_tuning_env("PT_STEP_DB")) db = db && atoi(v) != 0;
         const int64_t gpb = 256 / s.G, ppb = gpb / S;
         const dim3 grid((unsigned)((P.batch_size + ppb - 1) / ppb)), block(256);
         size_t lds = (size_t)ppb * (size_t)P.neg * sizeof(int64_t) * (csr ? 2 : 1);

@@ -29,6 +29,7 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "tuning.h"
 #include "device.h"
 #include "kernels.h"
 #include "universes.h"
@@ -675,7 +676,7 @@ int universe_shape_id(int64_t D, int model) {
     // TransE (few live rows per step) takes the wide shapes: twice the lane groups, half the rounds of a
     // step's positives (PT_UNI_NARROW=1: the narrow ones)
     static const bool narrow = [] {
-        const char *v = getenv("PT_UNI_NARROW");
+        const char *v = pt_tuning_env("PT_UNI_NARROW");
         return v && atoi(v) != 0;
     }();
     const Shape s = pick_universe_shape(D, model == 0 && !narrow);

@@ -77,6 +77,7 @@ SIGNATURES = {
     "pt_trainer_run_timed": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "pt_trainer_last_path": (ctypes.c_int, [c_vp]),
     "pt_trainer_set_deterministic": (ctypes.c_int, [c_vp, c_i32]),
+    "pt_trainer_set_sampling": (ctypes.c_int, [c_vp, c_i32, c_i64]),
     "pt_trainer_get_deterministic": (ctypes.c_int, [c_vp]),
     "pt_trainer_sample_csr": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, ctypes.c_int32, c_vp,
                                              c_vp, c_vp, c_vp, c_vp]),
@@ -99,6 +100,8 @@ SIGNATURES = {
     "pt_universe_set_free": (ctypes.c_int, [c_vp]),
     "pt_universe_set_profile": (ctypes.c_int, [c_vp, c_vp]),
     "pt_universe_set_deterministic": (ctypes.c_int, [c_vp, c_i32]),
+    "pt_universe_set_profiling": (ctypes.c_int, [c_vp, c_i32]),
+    "pt_universe_set_states": (ctypes.c_int, [c_vp, c_i64, c_vp]),
     "pt_universes_train": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
                                           c_i64, c_vp, c_vp]),
     "pt_universes_train_ex": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,

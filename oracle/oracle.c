@@ -966,6 +966,35 @@ static int find_triple(const otriple *all, int64_t n, int64_t h, int64_t t, int6
     return bsearch(&key, all, (size_t)n, sizeof(otriple), cmp_head) != NULL;
 }
 
+/* filtered MRR / MR / Hits@10/3/1 from the per-query filtered ranks, with the reference's float
+ * accumulators per side (Test.h:213-223, :333-343, :398-454) */
+void oracle_metrics_from_ranks(int64_t n_test, const int64_t *frank_head, const int64_t *frank_tail, float *metrics) {
+    float l_filter_tot = 0, l3_filter_tot = 0, l1_filter_tot = 0, l_filter_rank = 0, l_filter_reci = 0;
+    float r_filter_tot = 0, r3_filter_tot = 0, r1_filter_tot = 0, r_filter_rank = 0, r_filter_reci = 0;
+    for (int64_t q = 0; q < n_test; ++q) {
+        const int64_t fh = frank_head[q], ft = frank_tail[q];
+        if (fh < 10) l_filter_tot += 1;
+        if (fh < 3) l3_filter_tot += 1;
+        if (fh < 1) l1_filter_tot += 1;
+        l_filter_rank += (float)(fh + 1);
+        l_filter_reci = (float)((double)l_filter_reci + 1.0 / (double)(fh + 1));
+        if (ft < 10) r_filter_tot += 1;
+        if (ft < 3) r3_filter_tot += 1;
+        if (ft < 1) r1_filter_tot += 1;
+        r_filter_rank += (float)(1 + ft);
+        r_filter_reci = (float)((double)r_filter_reci + 1.0 / (double)(1 + ft));
+    }
+    float nt = (float)n_test;
+    l_filter_rank /= nt; r_filter_rank /= nt; l_filter_reci /= nt; r_filter_reci /= nt;
+    l_filter_tot /= nt; l3_filter_tot /= nt; l1_filter_tot /= nt;
+    r_filter_tot /= nt; r3_filter_tot /= nt; r1_filter_tot /= nt;
+    metrics[0] = (l_filter_reci + r_filter_reci) / 2;       /* Test.h:450-454 */
+    metrics[1] = (l_filter_rank + r_filter_rank) / 2;
+    metrics[2] = (l_filter_tot + r_filter_tot) / 2;
+    metrics[3] = (l3_filter_tot + r3_filter_tot) / 2;
+    metrics[4] = (l1_filter_tot + r1_filter_tot) / 2;
+}
+
 void oracle_link_prediction(int64_t E, const int64_t *ah, const int64_t *at, const int64_t *ar, int64_t n_all,
                             const int64_t *th, const int64_t *tt, const int64_t *tr, int64_t n_test,
                             const float *con_head, const float *con_tail, int64_t *rank_head, int64_t *frank_head,
@@ -973,8 +1002,6 @@ void oracle_link_prediction(int64_t E, const int64_t *ah, const int64_t *at, con
     otriple *all = malloc(sizeof(otriple) * (size_t)(n_all ? n_all : 1));
     for (int64_t i = 0; i < n_all; ++i) { all[i].h = ah[i]; all[i].t = at[i]; all[i].r = ar[i]; }
     qsort(all, (size_t)n_all, sizeof(otriple), cmp_head);
-    float l_filter_tot = 0, l3_filter_tot = 0, l1_filter_tot = 0, l_filter_rank = 0, l_filter_reci = 0;
-    float r_filter_tot = 0, r3_filter_tot = 0, r1_filter_tot = 0, r_filter_rank = 0, r_filter_reci = 0;
     for (int64_t q = 0; q < n_test; ++q) {
         int64_t h = th[q], t = tt[q], r = tr[q];
         for (int side = 0; side < 2; ++side) {     /* 0: testHead (Test.h:118-238), 1: testTail (:240-359) */
@@ -1002,30 +1029,12 @@ void oracle_link_prediction(int64_t E, const int64_t *ah, const int64_t *at, con
             }
             if (side == 0) {
                 rank_head[q] = raw; frank_head[q] = filt;
-                if (filt < 10) l_filter_tot += 1;
-                if (filt < 3) l3_filter_tot += 1;
-                if (filt < 1) l1_filter_tot += 1;
-                l_filter_rank += (float)(filt + 1);
-                l_filter_reci = (float)((double)l_filter_reci + 1.0 / (double)(filt + 1));
             } else {
                 rank_tail[q] = raw; frank_tail[q] = filt;
-                if (filt < 10) r_filter_tot += 1;
-                if (filt < 3) r3_filter_tot += 1;
-                if (filt < 1) r1_filter_tot += 1;
-                r_filter_rank += (float)(1 + filt);
-                r_filter_reci = (float)((double)r_filter_reci + 1.0 / (double)(1 + filt));
             }
         }
     }
-    float nt = (float)n_test;
-    l_filter_rank /= nt; r_filter_rank /= nt; l_filter_reci /= nt; r_filter_reci /= nt;
-    l_filter_tot /= nt; l3_filter_tot /= nt; l1_filter_tot /= nt;
-    r_filter_tot /= nt; r3_filter_tot /= nt; r1_filter_tot /= nt;
-    metrics[0] = (l_filter_reci + r_filter_reci) / 2;       /* Test.h:450-454 */
-    metrics[1] = (l_filter_rank + r_filter_rank) / 2;
-    metrics[2] = (l_filter_tot + r_filter_tot) / 2;
-    metrics[3] = (l3_filter_tot + r3_filter_tot) / 2;
-    metrics[4] = (l1_filter_tot + r1_filter_tot) / 2;
+    oracle_metrics_from_ranks(n_test, frank_head, frank_tail, metrics);
     free(all);
 }
 

@@ -87,6 +87,9 @@ void oracle_link_prediction(int64_t ent_total, const int64_t *all_h, const int64
                             int64_t n_test, const float *con_head, const float *con_tail, int64_t *rank_head,
                             int64_t *frank_head, int64_t *rank_tail, int64_t *frank_tail, float *metrics);
 
+/* metrics[5] from filtered ranks alone (the accumulation of oracle_link_prediction) */
+void oracle_metrics_from_ranks(int64_t n_test, const int64_t *frank_head, const int64_t *frank_tail, float *metrics);
+
 /* Reference-faithful sequential step timing helper for bench.py's cpu_baseline leg: samples and trains
  * `steps` steps with the restated sampler + step (single thread). Returns total slots processed. */
 int64_t oracle_train_loop(const okg *g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg, int64_t bern,

@@ -59,6 +59,14 @@ def lib():
                                              [ctypes.c_int64] + [f32p] * 2 + [i64p] * 4 + [f32p])
         L.oracle_rank_constrained.argtypes = ([ctypes.c_int64] + [i64p] * 3 + [ctypes.c_int64] + [i64p] * 3 +
                                               [ctypes.c_int64] + [f32p] * 2 + [i64p] * 6 + [i64p] * 4 + [f32p])
+        L.oracle_metrics_from_ranks.argtypes = [ctypes.c_int64, i64p, i64p, f32p]
+        L.oracle_train_step_mt.restype = ctypes.c_float
+        L.oracle_train_step_mt.argtypes = ([ctypes.c_int] * 4 + [ctypes.c_float] * 2 + [ctypes.c_int64] * 3 +
+                                           [f32p] * 6 + [i64p] * 3 + [ctypes.c_int64] * 3)
+        L.oracle_train_loop_mt.restype = ctypes.c_int64
+        L.oracle_train_loop_mt.argtypes = ([ctypes.c_void_p, u64p] + [ctypes.c_int64] * 5 + [ctypes.c_int] * 4 +
+                                           [ctypes.c_float] * 2 + [ctypes.c_int64] + [f32p] * 6 +
+                                           [ctypes.c_int64] * 2 + [f32p])
         L.oracle_train_loop.restype = ctypes.c_int64
         L.oracle_train_loop.argtypes = ([ctypes.c_void_p, u64p] + [ctypes.c_int64] * 5 + [ctypes.c_int] * 4 +
                                         [ctypes.c_float] * 2 + [ctypes.c_int64] + [f32p] * 6 + [ctypes.c_int64])
@@ -226,6 +234,28 @@ def link_prediction(E, all_triples, test, con_head, con_tail):
     return met, (rh, fh, rt, ft)
 
 
+def metrics_from_ranks(frank_head, frank_tail):
+    """Filtered {MRR, MR, Hits@10, Hits@3, Hits@1} of given per-query ranks (Test.h float accumulation)."""
+    fh = np.ascontiguousarray(frank_head, dtype=np.int64)
+    ft = np.ascontiguousarray(frank_tail, dtype=np.int64)
+    met = np.zeros(5, dtype=np.float32)
+    lib().oracle_metrics_from_ranks(len(fh), _p(fh, i64p), _p(ft, i64p), _p(met, f32p))
+    return met
+
+
+def train_step_mt(model, p, norm_flag, opt, lr, margin, ent, rel, normv, accs, h, t, r, bs, neg, workers):
+    """train_step on `workers` threads (bit-identical to train_step)."""
+    E, D = ent.shape
+    R = rel.shape[0]
+    dummy = np.zeros(1, dtype=np.float32)
+    nv = normv if normv is not None else dummy
+    ea, ra, na = (a if a is not None else dummy for a in accs)
+    h, t, r = (np.ascontiguousarray(x, dtype=np.int64) for x in (h, t, r))
+    return lib().oracle_train_step_mt(MODELS[model], p, int(norm_flag), OPTS[opt], lr, margin, E, R, D,
+                                      _p(ent, f32p), _p(rel, f32p), _p(nv, f32p), _p(ea, f32p), _p(ra, f32p),
+                                      _p(na, f32p), _p(h, i64p), _p(t, i64p), _p(r, i64p), bs, neg, workers)
+
+
 def read_types(path, rel_total):
     """importTypeFiles (Reader.h:352-396): `type_constrain.txt` = a count, then per relation two lines
     `r n e_1 .. e_n` (heads, then tails); relationTotal records read, each list sorted in place.
@@ -266,7 +296,10 @@ def rank_constrained(E, all_triples, test, con_head, con_tail, types):
     return met, (rh, fh, rt, ft)
 
 
-def train_loop(kg, states, threads, bs, neg, bern, filt, model, p, norm_flag, opt, lr, margin, tables, accs, steps):
+def train_loop(kg, states, threads, bs, neg, bern, filt, model, p, norm_flag, opt, lr, margin, tables, accs, steps,
+               workers=1, losses=None):
+    """`steps` sampling() calls + steps; workers > 1 runs the sampler slices and the step phases on that many
+    threads (bit-identical). Returns the slots processed; losses (float32 array) receives each step's loss."""
     ent, rel, normv = tables
     ea, ra, na = accs
     dummy = np.zeros(1, dtype=np.float32)
@@ -274,6 +307,8 @@ def train_loop(kg, states, threads, bs, neg, bern, filt, model, p, norm_flag, op
     ea = ea if ea is not None else dummy
     ra = ra if ra is not None else dummy
     na = na if na is not None else dummy
-    return lib().oracle_train_loop(kg.h, _p(states, u64p), threads, bs, neg, bern, filt, MODELS[model], p,
-                                   int(norm_flag), OPTS[opt], lr, margin, ent.shape[1], _p(ent, f32p),
-                                   _p(rel, f32p), _p(nv, f32p), _p(ea, f32p), _p(ra, f32p), _p(na, f32p), steps)
+    lp = _p(losses, f32p) if losses is not None else None
+    return lib().oracle_train_loop_mt(kg.h, _p(states, u64p), threads, bs, neg, bern, filt, MODELS[model], p,
+                                      int(norm_flag), OPTS[opt], lr, margin, ent.shape[1], _p(ent, f32p),
+                                      _p(rel, f32p), _p(nv, f32p), _p(ea, f32p), _p(ra, f32p), _p(na, f32p), steps,
+                                      workers, lp)

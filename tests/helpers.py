@@ -153,3 +153,41 @@ def assert_ranks_match(ours, ref_ranks, con_h, con_t, rel_tol=1e-6):
             assert abs(int(a[q]) - int(b[q])) <= ties, (k, q, a[q], b[q], ties)
             mism += 1
     return mism
+
+
+def step_noise(acc_before, acc_oracle, acc_ours, noise2=1e-14):
+    """Components whose Adagrad step was noise-decided in EITHER implementation: the squared-gradient
+    increment of the step is positive but below noise2 (|g| < 1e-7: the contributions cancelled to
+    rounding level, so the sign of g - and with it the +-lr step lr*g/(|g|+1e-10) - is set by the order of
+    the sum). Both increments are observable in a teacher-forced step (same input state)."""
+    if acc_before is None:
+        return None
+    a0 = np.asarray(acc_before, dtype=np.float64)
+    io = np.asarray(acc_oracle, dtype=np.float64) - a0
+    iu = np.asarray(acc_ours, dtype=np.float64) - a0
+    return ((io > 0) & (io < noise2)) | ((iu > 0) & (iu < noise2))
+
+
+def assert_step_close(ours, want, atol, mask=None, max_frac=1e-2, what="", before=None, rtol=1e-3):
+    """One step from the same state: |ours - want| <= atol + rtol * |want - before| (the step's own update
+    sets the scale: a component whose gradient partly cancelled carries a relative rounding error of its
+    sum, which Adagrad's lr * g / sqrt(A) passes on to the update), except on the step's noise-decided
+    components (mask), which must be rare (at most a few, or max_frac of a large table)."""
+    ours = np.asarray(ours, dtype=np.float64)
+    want = np.asarray(want, dtype=np.float64)
+    tol = atol if before is None else atol + rtol * np.abs(want - np.asarray(before, dtype=np.float64))
+    bad = np.abs(ours - want) > tol
+    if mask is not None:
+        assert mask.sum() <= max(4, max_frac * mask.size), "%s: %d noise-decided components" % (what,
+                                                                                              int(mask.sum()))
+        bad &= ~mask
+    assert not bad.any(), "%s: max err %g at %d entries (atol %g)" % (what, float(np.abs(ours - want)[bad].max()),
+                                                                      int(bad.sum()), atol)
+
+
+def metrics_match_ranks(metrics, ranks):
+    """The reported filtered metrics are those of the reported per-query filtered ranks (Test.h float
+    accumulation restated by the oracle)."""
+    import oracle
+    want = oracle.metrics_from_ranks(ranks[1], ranks[3])
+    np.testing.assert_allclose(np.asarray(metrics, dtype=np.float32)[:5], want, rtol=1e-6, atol=1e-7)

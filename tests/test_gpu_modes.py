@@ -102,6 +102,13 @@ def test_cross_and_relation_training_matches_oracle(case):
     total = 0.0
     for mode in modes:
         h, t, r, _ = kg.sample_ex(st, threads, bs, neg, neg_rel, mode, bern, filt)
+        if mode != 0:
+            # sampling_head / sampling_tail return the first bs relations and fixed-side entities, which the
+            # model broadcasts over every negative (TransE.py:51-58): relation-corruption slots become
+            # copies of their positive
+            fixed = t if mode == -1 else h
+            fixed.reshape(-1, bs)[1:] = fixed[:bs]
+            r.reshape(-1, bs)[1:] = r[:bs]
         total += oracle.train_step(model, p, True, opt, lr, margin, ent, rel, nv, accs, h, t, r, bs, neg + neg_rel)
     np.testing.assert_allclose(tr.last_epoch_loss, total, rtol=1e-5, atol=1e-6)
     for got, want in zip(_tables(kge), (ent, rel, nv)):

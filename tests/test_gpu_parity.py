@@ -10,8 +10,8 @@ import torch
 
 import oracle
 from conftest import KG_SMALL, KG_TINY, PKG
-from helpers import (DATASETS, IllConditioned, assert_close_vs_oracle, assert_ranks_match, assert_tables_close,
-                     golden, load, torch_init_tables)
+from helpers import (DATASETS, IllConditioned, assert_close_vs_oracle, assert_ranks_match, assert_step_close,
+                     assert_tables_close, golden, load, metrics_match_ranks, step_noise, torch_init_tables)
 
 pytestmark = pytest.mark.gpu
 
@@ -445,12 +445,12 @@ def test_triple_classification_matches_reference(path):
 
 
 # The fused LDS sampling + counting-sort kernel (k_sample_sort, taken once a run pre-samples >= 96 steps
-# in one chunk) against the two-pass form (k_sample_csr + k_scan_counts, PT_SAMPLE_TWO_PASS=1) and the
+# in one chunk) against the two-pass form (k_sample_csr + k_scan_counts, pt_trainer_set_sampling) and the
 # oracle over 120 steps: both forms draw the same batches (the per-step losses agree to float rounding:
 # only the order of the gradient sums inside an entity's bucket may differ) and land on the oracle's
 # tables. Tolerance: 1e-5 relative on every step's loss, 1e-4 absolute on the tables after 120 SGD steps.
 @pytest.mark.parametrize("model", ["TransE", "TransH"])
-def test_fused_sample_sort_matches_two_pass_and_oracle(model, monkeypatch):
+def test_fused_sample_sort_matches_two_pass_and_oracle(model):
     from openke.config import Trainer
     from openke.module.loss import MarginLoss
     from openke.module.model import TransE, TransH
@@ -458,8 +458,8 @@ def test_fused_sample_sort_matches_two_pass_and_oracle(model, monkeypatch):
     dim, p, bs, neg, steps, lr, margin, seed = 20, 1, 64, 5, 120, 0.05, 4.0, 5
     cls = TransE if model == "TransE" else TransH
     runs = {}
+    from openke import _native
     for two_pass in ("0", "1"):
-        monkeypatch.setenv("PT_SAMPLE_TWO_PASS", two_pass)
         dl = _loader_path(KG_SMALL, 8, bs, neg, 1, 1, seed)
         dl.nbatches = steps
         torch.manual_seed(19)
@@ -467,7 +467,12 @@ def test_fused_sample_sort_matches_two_pass_and_oracle(model, monkeypatch):
         t0 = _tables(kge)
         ns = NegativeSampling(model=kge, loss=MarginLoss(margin=margin), batch_size=bs)
         tr = Trainer(model=ns, data_loader=dl, train_times=1, alpha=lr, use_gpu=True, opt_method="sgd")
+        tr._setup()
+        _native.check(_native.lib().pt_trainer_set_sampling(tr._native, _native.PT_PATH_TWO_PASS if two_pass == "1"
+                                                            else -1, 0))
         tr.run()
+        assert _native.lib().pt_trainer_last_path(tr._native) == (_native.PT_PATH_TWO_PASS if two_pass == "1"
+                                                                 else _native.PT_PATH_FUSED)
         runs[two_pass] = (tr.last_epoch_loss, _tables(kge), t0)
     (lf, tf, t0), (lt, tt, _) = runs["0"], runs["1"]
     np.testing.assert_allclose(lf, lt, rtol=1e-5)
@@ -548,6 +553,7 @@ def test_static_experiment_flow(tmp_path):
     # near-ties (the tables come from float-atomic training, so ties differ from run to run)
     _, vr, vch, vct = oracle_ranks("valid2id.txt")
     mism = assert_ranks_match(validator.last_ranks, vr, vch, vct)
+    # hit@10 is the one of our ranks, which equal the oracle's up to float near-ties of the truth's score
     assert hits[-1] == pytest.approx(sys_test.valid_hit10(validator.last_ranks), rel=1e-6, abs=1e-7)
     if mism == 0:
         assert hits[-1] == pytest.approx(sys_test.valid_hit10(vr), rel=1e-6, abs=1e-7)
@@ -559,5 +565,87 @@ def test_static_experiment_flow(tmp_path):
     tester = Tester(model=transe, data_loader=TestDataLoader(KG_SMALL, "link", mode='test'), use_gpu=True)
     res = tester.run_link_prediction(type_constrain=False)
     met, tr_, tch, tct = oracle_ranks("test2id.txt")
+    metrics_match_ranks(res, tester.last_ranks)
     if assert_ranks_match(tester.last_ranks, tr_, tch, tct) == 0:
         np.testing.assert_allclose(np.array(res, dtype=np.float32), met, rtol=1e-5, atol=1e-6)
+
+
+# The fast single-model trainer teacher-forced: every step starts from the oracle's state (tables, Adagrad
+# state, sampler streams) and must equal the oracle's step - loss within 1e-5 relative, tables within 2e-6
+# absolute + 1e-3 of the step's own update (helpers.assert_step_close), except on the components whose
+# Adagrad update was noise-decided in either implementation
+# (helpers.step_noise). Covers the small-neg in-step sampler path and the counting-sort path (neg >= 4)
+# with its split sampler, TransE / TransH, p 1 / 2, SGD / Adagrad, the odd dims. Whole trajectories are
+# compared bit for bit in deterministic mode (test_gpu_ordered.py).
+TF_CASES = [
+    # model, dim, p, norm_flag, opt, bs, neg, bern, filter, steps
+    ("TransE", 20, 1, True, "adagrad", 50, 1, 0, 0, 25),
+    ("TransE", 69, 1, True, "adagrad", 64, 3, 1, 1, 15),
+    ("TransE", 23, 2, True, "adagrad", 40, 6, 0, 1, 15),
+    ("TransE", 200, 2, True, "sgd", 120, 25, 1, 1, 6),
+    ("TransE", 100, 2, False, "adagrad", 48, 12, 1, 1, 10),
+    ("TransH", 23, 1, True, "adagrad", 48, 1, 0, 0, 20),
+    ("TransH", 69, 2, True, "adagrad", 32, 5, 1, 1, 10),
+    ("TransH", 20, 2, False, "sgd", 70, 2, 1, 0, 10),
+]
+
+
+@pytest.mark.parametrize("case", TF_CASES, ids=lambda c: "%s-d%d-p%d-nf%d-%s-bs%d-neg%d" % (c[0], c[1], c[2], c[3],
+                                                                                         c[4], c[5], c[6]))
+def test_fast_trainer_steps_teacher_forced(case):
+    from openke import _native
+    from openke.module.model import TransE, TransH
+    model, dim, p, nf, opt, bs, neg, bern, filt, steps = case
+    lr, margin, seed = (0.5 if opt == "sgd" else 0.05), 3.0, 23
+    L = _native.lib()
+    kg = oracle.KG.load(KG_SMALL)
+    E, R = kg.ent_total, kg.rel_total
+    torch.manual_seed(dim + neg)
+    kge = (TransE if model == "TransE" else TransH)(E, R, dim=dim, p_norm=p, norm_flag=nf).cuda()
+    ada = opt == "adagrad"
+    devt = [t for t in kge.tables()]
+    dacc = [None if t is None else torch.zeros_like(t) for t in devt] if ada else [None, None, None]
+    ent, rel, nv = (None if t is None else t.detach().cpu().numpy().copy() for t in devt)
+    accs = [np.zeros_like(ent), np.zeros_like(rel), None if nv is None else np.zeros_like(nv)] if ada else [None] * 3
+    desc = kge.native_desc(_native.PT_ADAGRAD if ada else _native.PT_SGD, lr, margin, tuple(dacc))
+    g, smp, tr = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    _native.check(L.pt_graph_load(KG_SMALL.encode(), ctypes.byref(g)))
+    st = oracle.GlibcRand(seed).rand_reset(8)
+    _native.check(L.pt_sampler_create(g, 8, st.ctypes.data, ctypes.byref(smp)))
+    _native.check(L.pt_trainer_create(ctypes.byref(desc), ctypes.byref(tr)))
+    try:
+        loss = torch.zeros(1, device="cuda")
+        for k in range(steps):
+            with torch.no_grad():
+                for d_, h_ in zip(devt, (ent, rel, nv)):
+                    if h_ is not None:
+                        d_.copy_(torch.from_numpy(h_))
+                for d_, h_ in zip(dacc, accs):
+                    if h_ is not None:
+                        d_.copy_(torch.from_numpy(h_))
+            _native.check(L.pt_sampler_set_seeds(smp, st.ctypes.data))
+            loss.zero_()
+            _native.check(L.pt_trainer_step(tr, smp, bs, neg, bern, filt, None, None, None, _native.ptr(loss),
+                                            _native.stream()))
+            got = [None if t is None else t.detach().cpu().numpy() for t in devt]
+            got_acc = [None if t is None else t.cpu().numpy() for t in dacc]
+            acc0 = [None if a is None else a.copy() for a in accs]
+            tab0 = [None if a is None else a.copy() for a in (ent, rel, nv)]
+            h, t, r, _ = kg.sample(st, 8, bs, neg, bern, filt)
+            want = oracle.train_step(model, p, nf, opt, lr, margin, ent, rel, nv, accs, h, t, r, bs, neg)
+            assert abs(float(loss.item()) - want) <= 1e-5 * max(1.0, abs(want)), (k, float(loss.item()), want)
+            for i, name in enumerate(("ent", "rel", "norm")):
+                w = (ent, rel, nv)[i]
+                if w is None:
+                    continue
+                mask = step_noise(acc0[i], accs[i], got_acc[i]) if ada else None
+                assert_step_close(got[i], w, 2e-6, mask, what="step %d %s" % (k, name), before=tab0[i])
+        # the streams advanced exactly like one sampling() call per step
+        nxt = np.zeros(8, dtype=np.uint64)
+        _native.check(L.pt_sampler_get_seeds(smp, nxt.ctypes.data))
+        np.testing.assert_array_equal(nxt, st)
+    finally:
+        torch.cuda.synchronize()
+        L.pt_trainer_free(tr)
+        L.pt_sampler_free(smp)
+        L.pt_graph_free(g)

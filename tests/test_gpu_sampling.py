@@ -138,12 +138,13 @@ def test_sampling_path_matches_oracle(case, path):
 
 
 @pytest.mark.parametrize("parts", [2, 3, 7, 64, 200])
-def test_split_sampler_any_part_count(parts, monkeypatch):
-    """k_sample_part with part counts from 2 to one positive per part (PT_PART_COUNT): identical batches."""
-    monkeypatch.setenv("PT_PART_COUNT", str(parts))
+def test_split_sampler_any_part_count(parts):
+    """k_sample_part with part counts from 2 to one positive per part (pt_trainer_set_sampling): identical
+    batches."""
     bs, neg, bern, filt, calls, seed = 200, 13, 1, 1, 5, 13
     want, E = _oracle_batches(seed, bs, neg, bern, filt, calls)
     ctx = _Ctx(seed)
+    ctx.n.check(ctx.L.pt_trainer_set_sampling(ctx.t, -1, parts))
     try:
         _check_batches(ctx.sample(bs, neg, bern, filt, calls, PATHS["part"]), want, E, bs, neg)
     finally:
