@@ -10,8 +10,10 @@ touched rows. Inputs (graph, tables) are resident in HBM before timing starts.
 
 C2 is a single model, so N > 1 runs N independent replicas (one per GPU, "replicas only", weak
 scaling, no collective in the data path); value = slots of all ranks / max-over-ranks time.
-Prints ONE JSON line on rank 0 with roofline (live HIP-event kernel timing) and cpu_baseline (the
-oracle's single-thread C restatement timed on a bounded sample of the same workload, rank 0, N = 1).
+Prints ONE JSON line on rank 0 with roofline (live HIP-event kernel timing, per-kernel counted bytes from
+the committed PMC summary) and cpu_baseline (the oracle's C restatement on the host's cores, at most 16
+threads, timed on a bounded sample of the same workload, rank 0, N = 1); the pu_c3 field (C3 universes)
+carries its own cpu_baseline.
 """
 import argparse
 import ctypes
@@ -81,11 +83,24 @@ def all_reduce(t, op):
         t.copy_(h)
 
 
-def cpu_baseline(path, wl, seconds=15.0):
-    """Oracle (single-thread C restatement of the reference sampler + step) on a bounded sample."""
+def cpu_workers():
+    """Host threads for the CPU baseline: the cores this process may run on, at most 16 (a one-GPU box's
+    CPU share; the reference's sampler uses 8 pthreads, Base.cpp:266-310)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(path, wl, seconds=12.0):
+    """The CPU restatement (oracle/oracle.c: the reference's sampler + the step in reference order) on
+    `cpu_workers()` threads - sampler slices and the per-slot / per-row phases in parallel, bit-identical
+    to its single-thread form - over a bounded sample of the same workload."""
     sys.path.insert(0, HERE)
     import oracle
     shape, model, dim, p, opt, lr, margin, bs, neg, bern, filt = wl
+    workers = cpu_workers()
     kg = oracle.KG.load(path)
     st = oracle.GlibcRand(4).rand_reset(8)
     rng = np.random.default_rng(0)
@@ -94,16 +109,18 @@ def cpu_baseline(path, wl, seconds=15.0):
     rel = rng.uniform(-bound, bound, (kg.rel_total, dim)).astype(np.float32)
     nv = rng.uniform(-bound, bound, (kg.rel_total, dim)).astype(np.float32) if model == "TransH" else None
     accs = (np.zeros_like(ent), np.zeros_like(rel), None if nv is None else np.zeros_like(nv))
-    oracle.train_loop(kg, st, 8, bs, neg, bern, filt, model, p, True, opt, lr, margin, (ent, rel, nv), accs, 1)
+    oracle.train_loop(kg, st, 8, bs, neg, bern, filt, model, p, True, opt, lr, margin, (ent, rel, nv), accs, 1,
+                      workers=workers)
     steps, slots, t0 = 0, 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         slots += oracle.train_loop(kg, st, 8, bs, neg, bern, filt, model, p, True, opt, lr, margin,
-                                   (ent, rel, nv), accs, 1)
+                                   (ent, rel, nv), accs, 1, workers=workers)
         steps += 1
     el = time.perf_counter() - t0
-    return {"value": slots / el, "unit": "triples/s", "cores": 1, "kind": "port",
+    return {"value": slots / el, "unit": "triples/s", "cores": workers, "kind": "port",
             "sample": "%d steps of the same workload (batch %d x (1+%d), dim %d) on the same synthetic graph, "
-                      "oracle/oracle.c single thread, %.1f s" % (steps, bs, neg, dim, el)}
+                      "oracle/oracle.c on %d threads (sampler slices + per-slot / per-row phases), %.1f s"
+                      % (steps, bs, neg, dim, workers, el)}
 
 
 # PuTransE workloads (BASELINE.json configs[2..4]); ranges from the reference's experiments
@@ -268,35 +285,54 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
 
 
 def universe_cpu_baseline(path, name, seconds):
-    """Oracle (single-thread C restatement) training whole universes of the same workload, in id
-    order, until `seconds` have elapsed: universe construction + epochs x 20 Adagrad steps each."""
+    """The CPU restatement training whole universes of the same workload on `cpu_workers()` threads (one
+    universe per thread at a time, taken in id order; the reference trains them one after another on one
+    process, Parallel_Universe_Config.py:316-327): construction + epochs x 20 Adagrad steps each, new
+    universes started until `seconds` have elapsed, the clock stopped when the last one finishes."""
+    import threading
     sys.path.insert(0, HERE)
     import oracle
     shape, n_univ, model, dim_spec, p_norm, tc_range, margin_range, _ = PU_WORKLOADS[name]
+    workers = cpu_workers()
     kg = oracle.KG.load(path)
-    slots, n, t0 = 0, 0, time.perf_counter()
-    for k in range(n_univ):
-        if time.perf_counter() - t0 >= seconds:
-            break
-        tc, bal, margin, epochs, lr = universe_draws(k, tc_range, margin_range)
-        D = int(np.random.default_rng(1000 + k).integers(dim_spec[0], dim_spec[1] + 1)) \
-            if isinstance(dim_spec, tuple) else dim_spec
-        rng_c = oracle.GlibcRand(4 + k)
-        st = rng_c.rand_reset(8)
-        ug, _, _ = kg.universe(rng_c, tc, bal)
-        bs = ug.train_total // 20
-        rng = np.random.default_rng(k)
-        ent = _xavier(rng, ug.ent_total, D)
-        rel = _xavier(rng, ug.rel_total, D)
-        nv = _xavier(rng, ug.rel_total, D) if model == "TransH" else None
-        accs = (np.zeros_like(ent), np.zeros_like(rel), None if nv is None else np.zeros_like(nv))
-        slots += oracle.train_loop(ug, st, 8, bs, 1, 0, 0, model, p_norm, True, "adagrad", lr, margin,
-                                   (ent, rel, nv), accs, epochs * 20)
-        n += 1
+    lock = threading.Lock()
+    state = {"next": 0, "slots": 0, "done": 0}
+    t0 = time.perf_counter()
+
+    def work():
+        while True:
+            with lock:
+                k = state["next"]
+                if k >= n_univ or time.perf_counter() - t0 >= seconds:
+                    return
+                state["next"] += 1
+            tc, bal, margin, epochs, lr = universe_draws(k, tc_range, margin_range)
+            D = int(np.random.default_rng(1000 + k).integers(dim_spec[0], dim_spec[1] + 1)) \
+                if isinstance(dim_spec, tuple) else dim_spec
+            rng_c = oracle.GlibcRand(4 + k)
+            st = rng_c.rand_reset(8)
+            ug, _, _ = kg.universe(rng_c, tc, bal)
+            bs = ug.train_total // 20
+            rng = np.random.default_rng(k)
+            ent = _xavier(rng, ug.ent_total, D)
+            rel = _xavier(rng, ug.rel_total, D)
+            nv = _xavier(rng, ug.rel_total, D) if model == "TransH" else None
+            accs = (np.zeros_like(ent), np.zeros_like(rel), None if nv is None else np.zeros_like(nv))
+            n = oracle.train_loop(ug, st, 8, bs, 1, 0, 0, model, p_norm, True, "adagrad", lr, margin,
+                                  (ent, rel, nv), accs, epochs * 20)
+            with lock:
+                state["slots"] += n
+                state["done"] += 1
+
+    ths = [threading.Thread(target=work) for _ in range(workers)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
     el = time.perf_counter() - t0
-    return {"value": slots / el, "unit": "triples/s", "cores": 1, "kind": "port",
+    return {"value": state["slots"] / el, "unit": "triples/s", "cores": workers, "kind": "port",
             "sample": "%d whole universes (construction + epochs x 20 Adagrad steps) of the same workload, "
-                      "oracle/oracle.c single thread, %.1f s" % (n, el)}
+                      "oracle/oracle.c, one universe per thread on %d threads, %.1f s" % (state["done"], workers, el)}
 
 
 def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
@@ -379,6 +415,17 @@ def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
             "note": "universe scoring 4D+4 B per (key, universe entity); ranking 4 B per (query, entity)"}
 
 
+def load_traffic_by_kernel(tag):
+    """Per-kernel (2 x FETCH_SIZE + WRITE_SIZE) bytes per step from the committed PMC summary, if present."""
+    f = os.path.join(HERE, "profiles", "pmc_%s.json" % tag)
+    if not os.path.exists(f):
+        return None
+    try:
+        return json.load(open(f)).get("bytes_per_step_by_kernel")
+    except Exception:
+        return None
+
+
 def load_traffic(tag):
     """Per-launch HBM bytes of k_step + k_apply from a committed rocprofv3 --pmc summary, if present."""
     f = os.path.join(HERE, "profiles", "pmc_%s.json" % tag)
@@ -397,7 +444,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS) + sorted(PU_WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "putranse_bench"))
     ap.add_argument("--no-c3", action="store_true", help="skip the PuTransE universe workload (C3) field")
     ap.add_argument("--c3-steps", type=int, default=2)
@@ -496,8 +543,15 @@ def main():
     step_kernel_s = sum(per_kernel.values()) * 1e-3
     achieved = bytes_step / step_kernel_s / 1e9
     traffic = load_traffic(args.workload)
+    counted = load_traffic_by_kernel(args.workload)
+    kernel_detail = {}
+    for kname, ms in per_kernel.items():
+        b = next((v for k, v in counted.items() if kname in k), None) if counted else None
+        kernel_detail[kname] = {"ms": ms, "counted_bytes": b,
+                                "counted_TBps": None if b is None or ms <= 0 else b / (ms * 1e-3) / 1e12}
+    contrib_rt = 2 * bs * neg * dim * 4   # gradient rows of the corrupted entities: stored by the step, read by apply
 
-    c3 = None if args.no_c3 else run_universes(args, ws, rank, dev, "c3", cpu=False)
+    c3 = None if args.no_c3 else run_universes(args, ws, rank, dev, "c3", cpu=True)
     # universe weak scaling (512 universes per GPU, no collective): at N = 1 it is the strong line
     c3w = None if args.no_c3 or ws == 1 else run_universes(args, ws, rank, dev, "c3", cpu=False, per_gpu=True)
     if rank != 0:
@@ -529,12 +583,20 @@ def main():
                      "kernel": "one training step = " + " + ".join(per_kernel),
                      "ms_per_kernel": per_kernel,
                      "algorithmic_bytes_per_step": bytes_step,
-                     "hbm_frac": None if traffic is None else traffic / (step_kernel_s * 1e9) / HBM_PEAK_GBS,
+                     "counted_frac": None if traffic is None else traffic / (step_kernel_s * 1e9) / HBM_PEAK_GBS,
+                     "per_kernel": kernel_detail,
+                     "contrib_roundtrip_bytes": contrib_rt if spath != _native.PT_PATH_SAMPLED else 0,
+                     "contrib_share_of_counted": None if traffic is None or spath == _native.PT_PATH_SAMPLED
+                     else contrib_rt / traffic,
                      "note": "achieved / frac: SURVEY 8(d) algorithmic bytes per step over the summed kernel time "
-                             "(HIP events); traffic: measured HBM bytes per step (rocprofv3 PMC, profiles/"
-                             "pmc_c2.json), lower than the algorithmic count because the %.1f MB entity table is "
-                             "Infinity-Cache resident; hbm_frac = measured traffic over the same time vs the "
-                             "HBM peak" % (4e-6 * dl.get_ent_tot() * dim)},
+                             "(HIP events on the launch stream). traffic / counted_bytes: (2 x FETCH_SIZE + "
+                             "WRITE_SIZE) per step from rocprofv3 PMC passes (profiles/pmc_%s.json): the L2 <-> "
+                             "fabric bytes, Infinity-Cache hits included (MI355X_MICROARCH.md), so it is below the "
+                             "algorithmic count where repeated rows (%.1f MB entity table, hub entities, the "
+                             "positive rows shared by 25 negatives) hit in L2; counted_frac = that traffic over the "
+                             "same kernel time vs 8 TB/s. contrib_roundtrip_bytes: the corrupted entities' gradient "
+                             "rows written by the step kernel and read back by the apply pass" %
+                             (args.workload, 4e-6 * dl.get_ent_tot() * dim)},
         "loss_last_step": loss_last,
     }
     if c3 is not None:

@@ -97,6 +97,99 @@ __device__ __forceinline__ void vatomic(const V<G, VEC, KCH> &o, float *__restri
     }
 }
 
+// Address-space-typed pointers: rows reached through pointers loaded from memory (a universe descriptor)
+// or selected at run time between LDS and HBM are generic ("flat") to the compiler, and a flat access
+// counts in BOTH vmcnt and lgkmcnt - every LDS wait then also waits for the in-flight HBM loads. Kernels
+// that know where a row lives cast once to these types, so each access is a global_* or ds_* instruction.
+typedef __attribute__((address_space(1))) float gfloat;
+typedef __attribute__((address_space(3))) float lfloat;
+typedef __attribute__((address_space(1))) int32_t gint32;
+typedef __attribute__((address_space(3))) int32_t lint32;
+typedef __attribute__((address_space(3))) int lint;
+typedef __attribute__((address_space(3))) uint64_t luint64;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) f32x4 gf32x4;
+typedef __attribute__((address_space(3))) f32x4 lf32x4;
+typedef __attribute__((address_space(1))) i32x4 gi32x4;
+
+template <typename FP, typename F4P, int G, int VEC, int KCH>
+__device__ __forceinline__ void vload_t(V<G, VEC, KCH> &o, FP row, int D, int lane) {
+#pragma unroll
+    for (int k = 0; k < KCH; ++k) {
+        const int c = k * G + lane;
+        if ((k + 1) * G * VEC <= D || c * VEC < D) {
+            if constexpr (VEC == 4) {
+                const f32x4 f = *reinterpret_cast<F4P>(row + c * 4);
+                o.x[k * 4 + 0] = f.x; o.x[k * 4 + 1] = f.y; o.x[k * 4 + 2] = f.z; o.x[k * 4 + 3] = f.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) o.x[k * VEC + q] = row[c * VEC + q];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) o.x[k * VEC + q] = 0.f;
+        }
+    }
+}
+template <typename FP, typename F4P, int G, int VEC, int KCH>
+__device__ __forceinline__ void vstore_t(const V<G, VEC, KCH> &o, FP row, int D, int lane) {
+#pragma unroll
+    for (int k = 0; k < KCH; ++k) {
+        const int c = k * G + lane;
+        if ((k + 1) * G * VEC <= D || c * VEC < D) {
+            if constexpr (VEC == 4) {
+                const f32x4 f = {o.x[k * 4 + 0], o.x[k * 4 + 1], o.x[k * 4 + 2], o.x[k * 4 + 3]};
+                *reinterpret_cast<F4P>(row + c * 4) = f;
+            } else {
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) row[c * VEC + q] = o.x[k * VEC + q];
+            }
+        }
+    }
+}
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void vload(V<G, VEC, KCH> &o, const gfloat *row, int D, int lane) {
+    vload_t<const gfloat *, const gf32x4 *>(o, row, D, lane);
+}
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void vload(V<G, VEC, KCH> &o, const lfloat *row, int D, int lane) {
+    vload_t<const lfloat *, const lf32x4 *>(o, row, D, lane);
+}
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void vstore(const V<G, VEC, KCH> &o, gfloat *row, int D, int lane) {
+    vstore_t<gfloat *, gf32x4 *>(o, row, D, lane);
+}
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void vstore(const V<G, VEC, KCH> &o, lfloat *row, int D, int lane) {
+    vstore_t<lfloat *, lf32x4 *>(o, row, D, lane);
+}
+// float atomic adds into an LDS row (ds_add_f32) / an HBM row (global_atomic_add_f32)
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void vatomic(const V<G, VEC, KCH> &o, lfloat *row, int D, int lane) {
+#pragma unroll
+    for (int k = 0; k < KCH; ++k) {
+        const int c = k * G + lane;
+        if (c * VEC < D) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q)
+                __hip_atomic_fetch_add(row + c * VEC + q, o.x[k * VEC + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void vatomic(const V<G, VEC, KCH> &o, gfloat *row, int D, int lane) {
+#pragma unroll
+    for (int k = 0; k < KCH; ++k) {
+        const int c = k * G + lane;
+        if (c * VEC < D) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q)
+                __hip_atomic_fetch_add(row + c * VEC + q, o.x[k * VEC + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 template <int G, int VEC, int KCH>
 __device__ __forceinline__ float vdot(const V<G, VEC, KCH> &a, const V<G, VEC, KCH> &b) {
     float s = 0.f;
@@ -276,13 +369,13 @@ __device__ __forceinline__ int64_t rs_entity(const RunSearch &q) { return (int64
 // (trainHead[].t for corrupt_head, trainTail[].h for corrupt_tail) and [lo, hi] the run of known
 // partners of the positive's (entity, relation) - the [ll, rr] of the reference's two binary searches,
 // precomputed per triple (TripleRec). The draw, the early exits and the boundary are the reference's.
-__device__ __forceinline__ int64_t corrupt_in_run(const int32_t *__restrict__ vals, int64_t lo, int64_t hi, int64_t E,
-                                                  uint64_t &s) {
+template <typename VP>
+__device__ __forceinline__ int64_t corrupt_in_run(VP vals, int64_t lo, int64_t hi, int64_t E, uint64_t &s) {
     const int64_t tmp = rand_max(s, E - (hi - lo + 1));
     const int32_t vlo = vals[lo], vhi = vals[hi];
     if (tmp < vlo) return tmp;
     if (tmp > vhi - hi + lo - 1) return tmp + hi - lo + 1;
-    RunSearch q = run_search(vals, (int32_t)lo, (int32_t)hi, vlo, vhi, (int32_t)tmp);
+    RunSearch q = run_search(nullptr, (int32_t)lo, (int32_t)hi, vlo, vhi, (int32_t)tmp);   // (vals read here)
     while (rs_open(q)) {
         const int32_t m = rs_probe(q);
         rs_update(q, m, vals[m]);
@@ -292,8 +385,9 @@ __device__ __forceinline__ int64_t corrupt_in_run(const int32_t *__restrict__ va
 
 // state of the sampler stream that produces positive b of call `call` after the current states
 // (Base.cpp:200-207 split: thread id owns positives [id*per, min((id+1)*per, bs)) of every call)
-__device__ __forceinline__ uint64_t positive_state(const uint64_t *states, int64_t threads, int64_t bs, int64_t b,
-                                                   int64_t dpp, int64_t call = 0) {
+template <typename SP>
+__device__ __forceinline__ uint64_t positive_state(SP states, int64_t threads, int64_t bs, int64_t b, int64_t dpp,
+                                                   int64_t call = 0) {
     const int64_t per = bs % threads == 0 ? bs / threads : bs / threads + 1;
     const int64_t id = b / per;
     int64_t len = bs - id * per;
@@ -308,20 +402,44 @@ struct PosDraw {
     int64_t idx;   // trainList index of the positive
 };
 
+// The training graph as HBM-typed pointers (DeviceGraph's fields are generic: fine as kernel arguments,
+// which the compiler promotes to global, but flat when loaded from a descriptor in memory)
+struct DeviceGraphG {
+    int64_t ent_total, rel_total, train_total;
+    const gi32x4 *rec;          // TripleRec[train_total] as pairs of int4
+    const gint32 *head_t, *tail_h;
+    const gfloat *bern_prob;
+};
+__device__ __forceinline__ DeviceGraphG as_global(const DeviceGraph &g) {
+    return DeviceGraphG{g.ent_total, g.rel_total, g.train_total, (const gi32x4 *)(const void *)g.rec,
+                        (const gint32 *)g.head_t, (const gint32 *)g.tail_h, (const gfloat *)g.bern_prob};
+}
+__device__ __forceinline__ void graph_rec(const DeviceGraph &g, int64_t i, i32x4 &a, i32x4 &c) {
+    const i32x4 *p = reinterpret_cast<const i32x4 *>(g.rec + i);
+    a = p[0];
+    c = p[1];
+}
+__device__ __forceinline__ void graph_rec(const DeviceGraphG &g, int64_t i, i32x4 &a, i32x4 &c) {
+    a = g.rec[2 * i];
+    c = g.rec[2 * i + 1];
+}
+
 // positive b: i = rand_max(trainTotal), trainList[i] (Base.cpp:210-215)
-__device__ __forceinline__ PosDraw draw_positive(const DeviceGraph &g, const uint64_t *states, int64_t threads,
-                                                 int64_t bs, int64_t b, int64_t dpp, int64_t call = 0) {
+template <typename GR, typename SP>
+__device__ __forceinline__ PosDraw draw_positive(const GR &g, SP states, int64_t threads, int64_t bs, int64_t b,
+                                                 int64_t dpp, int64_t call = 0) {
     uint64_t s = positive_state(states, threads, bs, b, dpp, call);
     const int64_t i = rand_max(s, g.train_total);
-    const int4 *p = reinterpret_cast<const int4 *>(g.rec + i);
-    const int4 a = p[0], c = p[1];
+    i32x4 a, c;
+    graph_rec(g, i, a, c);
     return PosDraw{a.x, a.y, a.z, a.w, c.x, c.y, c.z, s, i};
 }
 
 // negative k of a positive (stream offsets 1+2k coin, 2+2k corruption; Base.cpp:217-232): returns the
 // corrupted entity, *tail_side = 1 when the tail was replaced (corrupt_head), 0 when the head was
-__device__ __forceinline__ int64_t draw_negative(const DeviceGraph &g, const PosDraw &p, int64_t k, int bern,
-                                                 int filter, int *tail_side) {
+template <typename GR>
+__device__ __forceinline__ int64_t draw_negative(const GR &g, const PosDraw &p, int64_t k, int bern, int filter,
+                                                 int *tail_side) {
     uint64_t s = lcg_jump(p.s1, (uint64_t)(2 * k));
     const float prob = bern ? g.bern_prob[p.r] : 500.f;
     const int64_t E = g.ent_total;

@@ -673,13 +673,22 @@ static void slot_backward(const ostep *S, slot_ws *ws, float *tmpb, int64_t s) {
 /* step 4 + 5 for one row: the listed slots' rows summed in slot order (per lookup), then the update */
 static void row_update(const ostep *S, float *w, float *acc, const float *ga, const int64_t *la, int64_t na,
                        const float *gb, const int64_t *lb, int64_t nb, float *g) {
+    /* per element: 0 + the lookup's rows in slot order (row by row over the list: the same per-element
+     * order as element by element, with contiguous reads) */
     const int64_t d = S->d;
-    for (int64_t i = 0; i < d; ++i) {
-        float a = 0.0f, b = 0.0f;
-        for (int64_t k = 0; k < na; ++k) a += ga[la[k] * d + i];
-        for (int64_t k = 0; k < nb; ++k) b += gb[lb[k] * d + i];
-        g[i] = nb ? a + b : a;
+    float *b = g + d;
+    memset(g, 0, sizeof(float) * (size_t)d);
+    memset(b, 0, sizeof(float) * (size_t)d);
+    for (int64_t k = 0; k < na; ++k) {
+        const float *x = ga + la[k] * d;
+        for (int64_t i = 0; i < d; ++i) g[i] += x[i];
     }
+    for (int64_t k = 0; k < nb; ++k) {
+        const float *x = gb + lb[k] * d;
+        for (int64_t i = 0; i < d; ++i) b[i] += x[i];
+    }
+    if (nb)
+        for (int64_t i = 0; i < d; ++i) g[i] = g[i] + b[i];
     apply_update(S->opt, S->lr, w, acc, g, d);
 }
 
