@@ -48,15 +48,23 @@ struct V {
     float x[N];
 };
 
-template <int G, int VEC, int KCH>
+// TAIL = true: float4 chunks over a row whose length D need not be a multiple of 4 (and whose start need
+// only be 4-byte aligned: unaligned 16-B global accesses are legal on gfx950): the chunk holding the row's
+// last 1-3 floats is read / written element by element, the rest 16 B per lane
+template <int G, int VEC, int KCH, bool TAIL = false>
 __device__ __forceinline__ void vload(V<G, VEC, KCH> &o, const float *__restrict__ row, int D, int lane) {
 #pragma unroll
     for (int k = 0; k < KCH; ++k) {
         const int c = k * G + lane;
         if ((k + 1) * G * VEC <= D || c * VEC < D) {   // first test is group-uniform (no exec masking)
             if constexpr (VEC == 4) {
-                const float4 f = *reinterpret_cast<const float4 *>(row + c * 4);
-                o.x[k * 4 + 0] = f.x; o.x[k * 4 + 1] = f.y; o.x[k * 4 + 2] = f.z; o.x[k * 4 + 3] = f.w;
+                if (!TAIL || (c + 1) * 4 <= D) {
+                    const float4 f = *reinterpret_cast<const float4 *>(row + c * 4);
+                    o.x[k * 4 + 0] = f.x; o.x[k * 4 + 1] = f.y; o.x[k * 4 + 2] = f.z; o.x[k * 4 + 3] = f.w;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) o.x[k * 4 + q] = c * 4 + q < D ? row[c * 4 + q] : 0.f;
+                }
             } else {
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) o.x[k * VEC + q] = row[c * VEC + q];
@@ -68,15 +76,21 @@ __device__ __forceinline__ void vload(V<G, VEC, KCH> &o, const float *__restrict
     }
 }
 
-template <int G, int VEC, int KCH>
+template <int G, int VEC, int KCH, bool TAIL = false>
 __device__ __forceinline__ void vstore(const V<G, VEC, KCH> &o, float *__restrict__ row, int D, int lane) {
 #pragma unroll
     for (int k = 0; k < KCH; ++k) {
         const int c = k * G + lane;
         if ((k + 1) * G * VEC <= D || c * VEC < D) {
             if constexpr (VEC == 4) {
-                *reinterpret_cast<float4 *>(row + c * 4) =
-                    make_float4(o.x[k * 4 + 0], o.x[k * 4 + 1], o.x[k * 4 + 2], o.x[k * 4 + 3]);
+                if (!TAIL || (c + 1) * 4 <= D) {
+                    *reinterpret_cast<float4 *>(row + c * 4) =
+                        make_float4(o.x[k * 4 + 0], o.x[k * 4 + 1], o.x[k * 4 + 2], o.x[k * 4 + 3]);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (c * 4 + q < D) row[c * 4 + q] = o.x[k * 4 + q];
+                }
             } else {
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) row[c * VEC + q] = o.x[k * VEC + q];
@@ -85,14 +99,15 @@ __device__ __forceinline__ void vstore(const V<G, VEC, KCH> &o, float *__restric
     }
 }
 
-template <int G, int VEC, int KCH>
+template <int G, int VEC, int KCH, bool TAIL = false>
 __device__ __forceinline__ void vatomic(const V<G, VEC, KCH> &o, float *__restrict__ row, int D, int lane) {
 #pragma unroll
     for (int k = 0; k < KCH; ++k) {
         const int c = k * G + lane;
         if (c * VEC < D) {
 #pragma unroll
-            for (int q = 0; q < VEC; ++q) atomicAdd(row + c * VEC + q, o.x[k * VEC + q]);
+            for (int q = 0; q < VEC; ++q)
+                if (!TAIL || c * VEC + q < D) atomicAdd(row + c * VEC + q, o.x[k * VEC + q]);
         }
     }
 }
