@@ -40,7 +40,14 @@ int pt_version(void);                /* ABI version, bumped on incompatible chan
 /* A training graph: deduplicated triples in cmp_head order plus the helper indices the sampler
  * needs (replaces importTrainFiles + loadHelpers, Reader.h:58-234). */
 typedef struct pt_graph pt_graph;
-int pt_graph_load(const char *in_path, pt_graph **out);   /* headerless h t r files, line-counted */
+int pt_graph_load(const char *in_path, pt_graph **out);   /* h t r files; line-counted unless count-header */
+/* Record format of every *2id.txt reader in this library (pt_graph_load, importTrainFiles,
+ * importTestFiles), process-global like setInPath. 0 (default): the reference's contract, the line count
+ * is the record count (Reader.h:176-196, Utilities.h:47-57). 1: the first line holds the record count,
+ * the upstream OpenKE format of the FB15K237 / WN18RR / FB13 / WN11 / NELL folders (the fscanf this fork
+ * commented out at Reader.h:178,185,191); a malformed or short file is then an error. */
+int pt_set_count_header(int on);
+int pt_get_count_header(void);
 int pt_graph_free(pt_graph *g);
 int64_t pt_graph_ent_total(const pt_graph *g);
 int64_t pt_graph_rel_total(const pt_graph *g);
@@ -276,6 +283,9 @@ int pt_rank_queries(const pt_known *k, int64_t ent_total, const int64_t *h, cons
  * randReset and its graph follows importTrainFiles / swapHelpers), so pt_trainer_* can train on exactly
  * the batch stream the reference's TrainDataLoader.sampling() would produce. */
 pt_sampler *pt_legacy_sampler(void);
+/* PT_OK or the error of the last importTrainFiles / importTestFiles (which return void like the
+ * reference's and leave the previous data in place on failure; pt_last_error() has the message). */
+int pt_legacy_import_status(void);
 int64_t pt_legacy_bern(void);
 /* test (valid = 0) or valid (valid = 1) triples of the global context in ranking order; returns the
  * count, fills the arrays when non-NULL. The known-triple set used by the filtered rank. */

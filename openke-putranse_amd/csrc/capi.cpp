@@ -153,6 +153,14 @@ int check_step_args(const pt::StepParams &P, pt_sampler *s, int64_t bs, int64_t 
 }  // namespace
 
 // ======================================================================== graphs =================
+// Opt-in count-header record format for every *2id.txt reader (pt_graph_load, importTrainFiles,
+// importTestFiles); the default keeps the reference's line-count contract (Reader.h:176-196).
+extern "C" int pt_set_count_header(int on) {
+    pt::set_count_header(on != 0);
+    return PT_OK;
+}
+extern "C" int pt_get_count_header(void) { return pt::count_header() ? 1 : 0; }
+
 extern "C" int pt_graph_load(const char *in_path, pt_graph **out) {
     PT_CHECK(in_path && out, PT_EINVAL, "pt_graph_load: null argument");
     auto *g = new pt_graph();
@@ -1484,6 +1492,8 @@ struct Legacy {
     std::vector<uint64_t> states;
     std::unique_ptr<pt::Graph> train;        // importTrainFiles
     std::string train_path;
+    bool train_header = false;               // record format train was read with
+    int import_rc = PT_OK;                   // status of the last importTrainFiles / importTestFiles
     std::unique_ptr<pt::Universe> uni;       // getParallelUniverse
     bool swapped = false;
     pt_sampler sampler;                      // device states; g follows the active graph
@@ -1575,9 +1585,13 @@ extern "C" void importTrainFiles(void) {
     Legacy &l = L();
     std::lock_guard<std::mutex> lk(l.mu);
     printf("The toolkit is importing datasets.\n");
-    if (l.train && l.train_path == l.in_path && !l.swapped) return;   // identical re-import
+    if (l.train && l.train_path == l.in_path && l.train_header == pt::count_header() && !l.swapped) {
+        l.import_rc = PT_OK;
+        return;   // identical re-import
+    }
     auto g = std::make_unique<pt::Graph>();
     int rc = pt::load_graph(l.in_path, *g);
+    l.import_rc = rc;
     if (rc) {
         legacy_err(rc);
         return;
@@ -1585,12 +1599,15 @@ extern "C" void importTrainFiles(void) {
     (void)hipDeviceSynchronize();   // an older graph may still be read by queued kernels
     l.train = std::move(g);
     l.train_path = l.in_path;
+    l.train_header = pt::count_header();
     l.ent_total = l.train->ent_total;
     l.rel_total = l.train->rel_total;
     legacy_err(l.train->upload());
     legacy_err(legacy_sync_sampler(l));
     printf("The total of train triples is %ld.\n", (long)l.train->train_total);
 }
+// The reference's import functions return void and crash on bad input; ours report through this.
+extern "C" int pt_legacy_import_status(void) { return L().import_rc; }
 extern "C" int64_t getEntityTotal(void) { Legacy &l = L(); return l.active() ? l.active()->ent_total : l.ent_total; }
 extern "C" int64_t getRelationTotal(void) { Legacy &l = L(); return l.active() ? l.active()->rel_total : l.rel_total; }
 extern "C" int64_t getTrainTotal(void) { Legacy &l = L(); return l.active() ? l.active()->train_total : l.train_lines; }
@@ -1764,19 +1781,13 @@ extern "C" void resetUniverse(void) {
 }
 
 // ----------------------------------------------------------------------- test / valid ----------
+// A test / valid / train / triple2id list under the current record format (graph.h record_count).
 static bool read_list(const std::string &path, std::vector<pt::Triple> &out) {
     bool ok = true;
-    const int64_t n = pt::count_lines(path, &ok);
+    std::string err;
+    const int64_t n = pt::record_count(path, &ok, &err);
     if (!ok) return false;
-    FILE *f = fopen(path.c_str(), "r");
-    out.resize((size_t)n);
-    for (int64_t i = 0; i < n; ++i) {
-        long a, b, c;
-        if (fscanf(f, "%ld %ld %ld", &a, &b, &c) != 3) { out.resize((size_t)i); break; }
-        out[(size_t)i] = pt::Triple{a, c, b};   // file order h t r
-    }
-    fclose(f);
-    return true;
+    return pt::read_triples(path, n, out) && (!pt::count_header() || (int64_t)out.size() == n);
 }
 
 extern "C" void activateLoadOfAllTriples(int64_t) { L().load_all = true; }
@@ -1785,12 +1796,14 @@ extern "C" void importTestFiles(void) {
     Legacy &l = L();
     std::lock_guard<std::mutex> lk(l.mu);
     bool ok = true;
-    l.rel_total = pt::count_lines(l.in_path + "relation2id.txt", &ok);
-    l.ent_total = pt::count_lines(l.in_path + "entity2id.txt", &ok);
+    l.rel_total = pt::record_count(l.in_path + "relation2id.txt", &ok);
+    l.ent_total = pt::record_count(l.in_path + "entity2id.txt", &ok);
     std::vector<pt::Triple> train_all;
-    if (!read_list(l.in_path + "test2id.txt", l.test) || !read_list(l.in_path + "train2id.txt", train_all) ||
+    l.import_rc = PT_EIO;
+    if (!ok || !read_list(l.in_path + "test2id.txt", l.test) || !read_list(l.in_path + "train2id.txt", train_all) ||
         !read_list(l.in_path + "valid2id.txt", l.valid))
-        return legacy_err(pt::fail(PT_EIO, "importTestFiles: missing test/train/valid file under " + l.in_path));
+        return legacy_err(pt::fail(PT_EIO, "importTestFiles: missing or malformed test/train/valid file under " +
+                                               l.in_path));
     l.test_total = (int64_t)l.test.size();
     l.valid_total = (int64_t)l.valid.size();
     l.train_lines = (int64_t)train_all.size();
@@ -1810,6 +1823,7 @@ extern "C" void importTestFiles(void) {
     pt_known_create(h.data(), t.data(), r.data(), (int64_t)all.size(), &k);
     if (l.known) pt_known_free(l.known);
     l.known = k;
+    l.import_rc = PT_OK;
     std::sort(l.test.begin(), l.test.end(), pt::cmp_rel2);    // Reader.h:311-312
     std::sort(l.valid.begin(), l.valid.end(), pt::cmp_rel2);
     printf("The total of test triples is %ld.\n", (long)l.test_total);

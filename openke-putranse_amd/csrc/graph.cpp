@@ -2,6 +2,8 @@
 #include "graph.h"
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 
 namespace pt {
@@ -50,7 +52,37 @@ int64_t count_lines(const std::string &path, bool *ok) {
     return n;
 }
 
-static bool read_triples(const std::string &path, int64_t n, std::vector<Triple> &out) {
+static std::atomic<bool> g_count_header{false};
+void set_count_header(bool on) { g_count_header.store(on); }
+bool count_header() { return g_count_header.load(); }
+
+// Header line of a count-header file: exactly one non-negative integer (upstream OpenKE reads it with
+// fscanf("%ld"), the call this fork commented out at Reader.h:178/185/191).
+int64_t record_count(const std::string &path, bool *ok, std::string *err) {
+    if (!count_header()) return count_lines(path, ok);
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) {
+        *ok = false;
+        return 0;
+    }
+    char line[256] = {0};
+    const bool got = fgets(line, sizeof line, f) != nullptr;
+    fclose(f);
+    char *end = nullptr;
+    const long long v = got ? strtoll(line, &end, 10) : -1;
+    bool good = got && end != line && v >= 0;
+    for (const char *p = end; good && p && *p; ++p)
+        if (!(*p == ' ' || *p == '\t' || *p == '\r' || *p == '\n')) good = false;
+    if (!good) {
+        *ok = false;
+        if (err) *err = "count-header format: first line of " + path + " is not a record count";
+        return 0;
+    }
+    *ok = true;
+    return (int64_t)v;
+}
+
+bool read_triples(const std::string &path, int64_t n, std::vector<Triple> &out) {
     FILE *f = fopen(path.c_str(), "rb");
     if (!f) return false;
     out.resize((size_t)n);
@@ -66,6 +98,10 @@ static bool read_triples(const std::string &path, int64_t n, std::vector<Triple>
     }
     fclose(f);
     const char *p = data.data();
+    if (count_header()) {   // skip the count line
+        while (*p && *p != '\n') ++p;
+        if (*p) ++p;
+    }
     auto next_int = [&](int64_t &v) -> bool {
         while (*p && !(*p == '-' || (*p >= '0' && *p <= '9'))) ++p;
         if (!*p) return false;
@@ -136,16 +172,20 @@ void Graph::build_helpers() {
 
 int load_graph(const std::string &dir, Graph &g) {
     bool ok = true;
-    g.rel_total = count_lines(dir + "relation2id.txt", &ok);
-    PT_CHECK(ok, PT_EIO, "cannot open " + dir + "relation2id.txt");
-    g.ent_total = count_lines(dir + "entity2id.txt", &ok);
-    PT_CHECK(ok, PT_EIO, "cannot open " + dir + "entity2id.txt");
-    int64_t n = count_lines(dir + "train2id.txt", &ok);
-    PT_CHECK(ok, PT_EIO, "cannot open " + dir + "train2id.txt");
+    std::string err;
+    g.rel_total = record_count(dir + "relation2id.txt", &ok, &err);
+    PT_CHECK(ok, PT_EIO, err.empty() ? "cannot open " + dir + "relation2id.txt" : err);
+    g.ent_total = record_count(dir + "entity2id.txt", &ok, &err);
+    PT_CHECK(ok, PT_EIO, err.empty() ? "cannot open " + dir + "entity2id.txt" : err);
+    int64_t n = record_count(dir + "train2id.txt", &ok, &err);
+    PT_CHECK(ok, PT_EIO, err.empty() ? "cannot open " + dir + "train2id.txt" : err);
     PT_CHECK(read_triples(dir + "train2id.txt", n, g.list), PT_EIO, "cannot read " + dir + "train2id.txt");
+    PT_CHECK(!count_header() || (int64_t)g.list.size() == n, PT_EIO,
+             "count-header format: " + dir + "train2id.txt holds fewer triples than its header says");
+    const char *hint = count_header() ? "" : " (count-header file? see pt_set_count_header)";
     for (const Triple &x : g.list)
         PT_CHECK(x.h >= 0 && x.t >= 0 && x.r >= 0 && x.h < g.ent_total && x.t < g.ent_total && x.r < g.rel_total,
-                 PT_EIO, "triple id out of range in " + dir + "train2id.txt (count-header file?)");
+                 PT_EIO, "triple id out of range in " + dir + "train2id.txt" + hint);
     std::sort(g.list.begin(), g.list.end(), cmp_head);
     g.list.erase(std::unique(g.list.begin(), g.list.end(),
                              [](const Triple &a, const Triple &b) { return a.h == b.h && a.r == b.r && a.t == b.t; }),

@@ -52,6 +52,17 @@ struct Graph {
 int load_graph(const std::string &dir, Graph &g);   // importTrainFiles (Reader.h:169-234)
 int64_t count_lines(const std::string &path, bool *ok);
 
+// Record-file format. Default (false): the record count is the line count and every line is a record,
+// the reference's contract (Reader.h:176-196). true: the first line holds the record count (the
+// upstream OpenKE / benchmark count-header format) and the records follow it.
+void set_count_header(bool on);
+bool count_header();
+// Number of records in a *2id.txt file under the current format (0 and *ok=false when unreadable; a
+// malformed header also sets *ok=false and fills *err).
+int64_t record_count(const std::string &path, bool *ok, std::string *err = nullptr);
+// n "a b c" triples (file order h t r) after the header line when the count-header format is on.
+bool read_triples(const std::string &path, int64_t n, std::vector<Triple> &out);
+
 bool cmp_head(const Triple &a, const Triple &b);
 bool cmp_tail(const Triple &a, const Triple &b);
 bool cmp_rel(const Triple &a, const Triple &b);

@@ -58,6 +58,8 @@ SIGNATURES = {
     "pt_version": (ctypes.c_int, []),
     "pt_graph_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(c_vp)]),
     "pt_graph_free": (ctypes.c_int, [c_vp]),
+    "pt_set_count_header": (ctypes.c_int, [ctypes.c_int]),
+    "pt_get_count_header": (ctypes.c_int, []),
     "pt_graph_ent_total": (c_i64, [c_vp]),
     "pt_graph_rel_total": (c_i64, [c_vp]),
     "pt_graph_train_total": (c_i64, [c_vp]),
@@ -116,6 +118,7 @@ SIGNATURES = {
     "pt_known_free": (ctypes.c_int, [c_vp]),
     "pt_rank_queries": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64]),
     "pt_legacy_sampler": (c_vp, []),
+    "pt_legacy_import_status": (ctypes.c_int, []),
     "pt_legacy_bern": (c_i64, []),
     "pt_legacy_graph": (c_vp, []),
     "pt_legacy_eval_triples": (c_i64, [c_i32, c_vp, c_vp, c_vp]),

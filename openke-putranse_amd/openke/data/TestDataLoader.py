@@ -35,7 +35,7 @@ class TestDataSampler(object):
 class TestDataLoader(object):
 
     def __init__(self, in_path="./", sampling_mode='link', random_seed=4, mode='test', setting="static",
-                 load_all_triples=False):
+                 load_all_triples=False, count_header=False):
         self.lib = _native.lib()
         if setting != "static":
             raise NotImplementedError("only the static setting is part of the accelerated path")
@@ -45,6 +45,7 @@ class TestDataLoader(object):
         self.in_path = in_path
         self.sampling_mode = sampling_mode
         self.random_seed = random_seed
+        self.count_header = bool(count_header)   # see TrainDataLoader
         self.read()
 
     def set_path(self, in_path):
@@ -52,12 +53,15 @@ class TestDataLoader(object):
 
     def read(self):
         self.set_path(self.in_path)
+        _native.check(self.lib.pt_set_count_header(1 if self.count_header else 0))
         self.lib.setRandomSeed(self.random_seed)
         self.lib.randReset()
         self.lib.importTrainFiles()
+        _native.check(self.lib.pt_legacy_import_status())
         if self.load_all_triples:
             self.lib.activateLoadOfAllTriples(1)
         self.lib.importTestFiles()
+        _native.check(self.lib.pt_legacy_import_status())
         self.relTotal = self.lib.getRelationTotal()
         self.entTotal = self.lib.getEntityTotal()
         E = self.entTotal

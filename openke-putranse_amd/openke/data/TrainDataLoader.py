@@ -35,7 +35,7 @@ class TrainDataSampler(object):
 
 class TrainDataLoader(object):
     def __init__(self, in_path="./", batch_size=None, nbatches=None, threads=8, sampling_mode="normal", bern_flag=0,
-                 filter_flag=1, neg_ent=1, neg_rel=0, random_seed=2, incremental_setting=False):
+                 filter_flag=1, neg_ent=1, neg_rel=0, random_seed=2, incremental_setting=False, count_header=False):
         self.lib = _native.lib()
         if incremental_setting:
             raise NotImplementedError("incremental_setting is outside the accelerated path")
@@ -51,15 +51,20 @@ class TrainDataLoader(object):
         self.cross_sampling_flag = 0
         self.random_seed = random_seed
         self.incremental_setting = incremental_setting
+        # opt-in: *2id.txt files whose first line is the record count (upstream OpenKE format); the
+        # default keeps the reference's line-count reader (Reader.h:176-196)
+        self.count_header = bool(count_header)
         self.read()
 
     def read(self):
         self.lib.setInPath(ctypes.create_string_buffer(self.in_path.encode(), len(self.in_path) * 2))
+        _native.check(self.lib.pt_set_count_header(1 if self.count_header else 0))
         self.lib.setBern(self.bern)
         self.lib.setWorkThreads(self.work_threads)
         self.lib.setRandomSeed(self.random_seed)
         self.lib.randReset()
         self.lib.importTrainFiles()
+        _native.check(self.lib.pt_legacy_import_status())
         self.relTotal = self.lib.getRelationTotal()
         self.entTotal = self.lib.getEntityTotal()
         self.tripleTotal = self.lib.getTrainTotal()

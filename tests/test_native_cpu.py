@@ -227,3 +227,91 @@ def test_import_type_files_matches_oracle_reader():
         np.testing.assert_array_equal(lef, want[3 * side])
         np.testing.assert_array_equal(rig, want[3 * side + 1])
         np.testing.assert_array_equal(lst[:n], want[3 * side + 2][:n])
+
+
+def _header_copy(tmp_path, header_text=None):
+    """kg_small with a count line prepended to every *2id.txt file (the upstream OpenKE format)."""
+    d = tmp_path / "kg_small_header"
+    d.mkdir()
+    for name in ("entity2id.txt", "relation2id.txt", "train2id.txt", "test2id.txt", "valid2id.txt",
+                 "type_constrain.txt"):
+        body = open(KG_SMALL + name).read()
+        if name == "type_constrain.txt":
+            (d / name).write_text(body)
+            continue
+        head = header_text if header_text is not None and name == "train2id.txt" else "%d\n" % body.count("\n")
+        (d / name).write_text(head + body)
+    return str(d) + os.sep
+
+
+def _graph_arrays(L, g):
+    n = L.pt_graph_train_total(g)
+    arrs = [np.zeros(n, dtype=np.int64) for _ in range(3)]
+    _native.check(L.pt_graph_triples(g, *(a.ctypes.data for a in arrs)))
+    return (L.pt_graph_ent_total(g), L.pt_graph_rel_total(g)), arrs
+
+
+def test_count_header_reader_is_opt_in(tmp_path):
+    """Opt-in count-header format (pt_set_count_header): a header-prefixed copy of kg_small reads back the
+    same graph as the headerless original; the default line-count contract (Reader.h:176-196) rejects it."""
+    L = _native.lib()
+    hdr = _header_copy(tmp_path)
+    assert L.pt_get_count_header() == 0
+    g0 = _graph(KG_SMALL)
+    want_tot, want = _graph_arrays(L, g0)
+    L.pt_graph_free(g0)
+    # default: the header line is taken as a record and the ids go out of range -> a reported error
+    h = ctypes.c_void_p()
+    assert L.pt_graph_load(hdr.encode(), ctypes.byref(h)) == 2
+    assert b"count-header" in L.pt_last_error()
+    try:
+        _native.check(L.pt_set_count_header(1))
+        g1 = _graph(hdr)
+        got_tot, got = _graph_arrays(L, g1)
+        L.pt_graph_free(g1)
+        assert got_tot == want_tot
+        for a, b in zip(got, want):
+            np.testing.assert_array_equal(a, b)
+        # and a headerless folder under the header format is a reported error, never a silent misread
+        assert L.pt_graph_load(KG_SMALL.encode(), ctypes.byref(h)) == 2
+    finally:
+        L.pt_set_count_header(0)
+
+
+def test_count_header_legacy_loaders(tmp_path):
+    """The Base.so-compatible importTrainFiles / importTestFiles under the opt-in format: same totals and
+    ranking-order test/valid triples as the headerless folder; a malformed header is reported through
+    pt_legacy_import_status and leaves the format's error message."""
+    L = _native.lib()
+    hdr = _header_copy(tmp_path)
+    (tmp_path / "bad").mkdir()
+    bad = _header_copy(tmp_path / "bad", header_text="three thousand\n")
+
+    def load(path):
+        L.setInPath(ctypes.create_string_buffer(path.encode(), len(path) * 2))
+        L.importTrainFiles()
+        _native.check(L.pt_legacy_import_status())
+        L.importTestFiles()
+        _native.check(L.pt_legacy_import_status())
+        out = [L.getEntityTotal(), L.getRelationTotal(), L.getTrainTotal(), L.getTestTotal(), L.getValidTotal()]
+        for valid in (0, 1):
+            n = L.pt_legacy_eval_triples(valid, None, None, None)
+            arrs = [np.zeros(n, dtype=np.int64) for _ in range(3)]
+            L.pt_legacy_eval_triples(valid, *(a.ctypes.data for a in arrs))
+            out.append(np.stack(arrs))
+        return out
+
+    want = load(KG_SMALL)
+    try:
+        L.pt_set_count_header(1)
+        got = load(hdr)
+        assert got[:5] == want[:5] and want[:5] == [500, 7, 3000, 100, 100]
+        np.testing.assert_array_equal(got[5], want[5])
+        np.testing.assert_array_equal(got[6], want[6])
+        L.setInPath(ctypes.create_string_buffer(bad.encode(), len(bad) * 2))
+        L.importTrainFiles()
+        assert L.pt_legacy_import_status() == 2
+        assert b"not a record count" in L.pt_last_error()
+    finally:
+        L.pt_set_count_header(0)
+        load(KG_SMALL)   # leave the global context as other tests expect it
