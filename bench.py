@@ -154,7 +154,7 @@ def _xavier(rng, rows, dim):
 
 
 def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
-    """PuTransE / PuTransH universes: universe k on rank k % N (no collective in training), Adagrad,
+    """PuTransE / PuTransH universes placed over ranks by LPT (place_universes; no collective in training), Adagrad,
     neg 1, bern 0, filter 0, nbatches 20, 8 sampler threads. One step = every universe's full training
     run (all its epochs) in one persistent launch. C4 adds link prediction over the test split: each
     rank MINs its universes' scores into the key rows, one RCCL all_reduce(MIN), GPU ranking."""
@@ -168,12 +168,18 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
     path = synth_kg.ensure_dataset(os.path.join(args.data_dir, "rank%d" % rank), shape)
     g = ctypes.c_void_p()
     _native.check(L.pt_graph_load(path.encode(), ctypes.byref(g)))
-    own = [k for k in range(n_univ) if k % ws == rank]
-    draws = [universe_draws(k, tc_range, margin_range) for k in own]
+    from openke.config.Parallel_Universe_Config import place_universes, universe_cost
+    all_draws = [universe_draws(k, tc_range, margin_range) for k in range(n_univ)]
     if isinstance(dim_spec, tuple):
-        dims = [int(np.random.default_rng(1000 + k).integers(dim_spec[0], dim_spec[1] + 1)) for k in own]
+        all_dims = [int(np.random.default_rng(1000 + k).integers(dim_spec[0], dim_spec[1] + 1)) for k in range(n_univ)]
     else:
-        dims = [dim_spec] * len(own)
+        all_dims = [dim_spec] * n_univ
+    # LPT placement over ranks on the drawn sizes (tc approximates the universe's triple count)
+    owners = place_universes({k: universe_cost(all_draws[k][3], all_draws[k][0], all_dims[k]) for k in range(n_univ)},
+                             ws)
+    own = [k for k in range(n_univ) if owners[k] == rank]
+    draws = [all_draws[k] for k in own]
+    dims = [all_dims[k] for k in own]
     seeds = np.array([4 + k for k in own], dtype=np.int64)
     tcs = np.array([d[0] for d in draws], dtype=np.int64)
     bals = np.array([d[1] for d in draws], dtype=np.float32)
@@ -462,7 +468,7 @@ def main():
                    "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
                    "data": "synthetic %s-shaped graph (tools/synth_kg.py, seed 0), xavier-uniform tables" %
                            PU_WORKLOADS[args.workload][0],
-                   "config": {"workload": c3["workload"], "parallelism": "universes sharded k %% %d" % ws},
+                   "config": {"workload": c3["workload"], "parallelism": "universes placed by LPT over %d ranks" % ws},
                    "roofline": c3["roofline"], "universes_per_gpu": c3["universes_per_gpu"]}
             if "link_prediction" in c3:
                 rec["link_prediction"] = c3["link_prediction"]

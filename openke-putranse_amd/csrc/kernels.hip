@@ -427,13 +427,17 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
     } else {
         for (int64_t o = o0 + tid; o < o1; o += NT) noff[o] += lds_bucket<PACK>(cnt, nrec[o] >> 1);
     }
-    // every wave's count atomics have returned (their values were used): count this part done
+    // every wave's count atomics have returned (their values were used): count this part done. The fences
+    // make the ticket a release (this part's count adds and slot stores ordered before it) and, in the
+    // last part, an acquire (the other parts' adds ordered before its exchanges below).
+    __threadfence();
     __syncthreads();
     if (tid == 0) is_last = atomicAdd(&w.tick[call], 1) == (int32_t)(parts - 1);
     __syncthreads();
     PT_PHASE(4);
     if (prof && tid == 0) prof[7] = is_last;
     if (!is_last) return;
+    __threadfence();
     if (tid == 0) w.tick[call] = 0;   // read again only by a later launch
     // last part: the call's bucket sizes, exchanged with zeros (atomics on both sides: every part's adds
     // are seen, and the counts are clear for the next chunk) into LDS, 8 exchanges in flight per thread
@@ -484,10 +488,12 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
 #undef PT_PHASE
     // the last call's last part advances the sampler streams past every call's draws: every part of every
     // call read them (positive draws) before its count atomics and tickets
+    __threadfence();
     __syncthreads();
     if (tid == 0) is_last = atomicAdd(&w.tick[gridDim.x / parts], 1) == (int32_t)(gridDim.x / parts - 1);
     __syncthreads();
     if (!is_last) return;
+    __threadfence();
     if (tid == 0) w.tick[gridDim.x / parts] = 0;
     if (tid < 64) advance_states(states, threads, bs, dpp * (int64_t)(gridDim.x / parts), tid);
 }

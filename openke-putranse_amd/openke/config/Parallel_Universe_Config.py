@@ -69,8 +69,30 @@ def _dist():
 
 
 def universe_owner(universe_id, world_size):
-    """Rank that trains universe `universe_id` (universes are independent: round-robin sharding)."""
+    """Round-robin rank of universe `universe_id`: the owner of a universe no placement map names
+    (universes committed through add_universe / the one-universe protocol)."""
     return universe_id % world_size
+
+
+def universe_cost(epochs, triples, dim):
+    """Relative GPU time of training one universe: epochs x training triples (the slot count up to the
+    constant nbatches / negative factors) times the per-slot row work, dim floats per embedding row plus
+    ~32 floats' worth of fixed per-slot sampling / loss work (the universes kernel's step profile)."""
+    return float(max(epochs, 0)) * float(max(triples, 0)) * (float(dim) + 32.0)
+
+
+def place_universes(costs, world_size):
+    """LPT placement (longest processing time first) of independent universes over ranks: universes in
+    decreasing cost (ties by id) each go to the rank with the least cost so far (ties to the lowest
+    rank). `costs` maps universe id -> cost; returns {universe id: rank}. A pure function of its
+    arguments, so every rank computes the same map from the same draws with no communication."""
+    loads = [0.0] * max(int(world_size), 1)
+    owners = {}
+    for uid, c in sorted(costs.items(), key=lambda kv: (-kv[1], kv[0])):
+        r = min(range(len(loads)), key=lambda i: (loads[i], i))
+        owners[uid] = r
+        loads[r] += c
+    return owners
 
 
 def min_combine(tensors):
@@ -296,6 +318,9 @@ class Parallel_Universe_Config(Tester):
         self._stores = {}                 # 'test' / 'valid' -> _KeyStore
         self._remap_cache = {}            # universe_id -> (ent_remap, rel_remap, sorted helpers)
         self._dev_remaps = {}             # universe_id -> device int64 local -> global entity map
+        # multi-GPU: universe_id -> rank that trains / holds it (place_universes per training wave, re-made
+        # by load_parameters for the loading job's world size); ids absent here are round-robin
+        self.universe_owners = {}
 
     # ------------------------------------------------------------------ reference API -----------
     def get_default_value_list(self):
@@ -337,6 +362,11 @@ class Parallel_Universe_Config(Tester):
         for param in embedding_space.parameters():
             param.requires_grad = False
         self.trained_embedding_spaces[self.next_universe_id] = embedding_space
+
+    def owner(self, uid):
+        """Rank holding universe `uid` in this job."""
+        world, _ = _dist()
+        return self.universe_owners.get(uid, universe_owner(uid, world))
 
     # ------------------------------------------------------------------ training ----------------
     def _batched(self):
@@ -380,6 +410,11 @@ class Parallel_Universe_Config(Tester):
         recs, jobs, keep = [], [], []
         dev = torch.device("cuda", torch.cuda.current_device())
         try:
+            if world > 1:   # LPT over the wave from the draws and the built universes' sizes (same on every rank)
+                dim = int(self.embedding_model_param.get("dim", 100))
+                self.universe_owners.update(place_universes(
+                    {uid: universe_cost(draws[i][3], L.pt_universe_train_total(handles[i]), dim)
+                     for i, uid in enumerate(ids)}, world))
             for i, uid in enumerate(ids):
                 tc, balance, margin, epochs, lr = draws[i]
                 h = handles[i]
@@ -396,7 +431,7 @@ class Parallel_Universe_Config(Tester):
                        "balance": balance, "margin": margin, "epochs": epochs, "lr": lr, "batch_size": bs,
                        "train_total": N_u, "losses": None}
                 recs.append(rec)
-                if universe_owner(uid, world) != rank:
+                if self.owner(uid) != rank:
                     continue   # trained on another rank
                 kge.to(dev)
                 ent, rel, nv = kge.tables()
@@ -523,8 +558,8 @@ class Parallel_Universe_Config(Tester):
 
     def _commit(self, rec):
         assert rec["id"] == self.next_universe_id
-        world, rank = _dist()
-        uid = self.add_universe(rec["kge"] if universe_owner(rec["id"], world) == rank else None, rec["ent_remap"],
+        _, rank = _dist()
+        uid = self.add_universe(rec["kge"] if self.owner(rec["id"]) == rank else None, rec["ent_remap"],
                                 rec["rel_remap"])
         if rec["losses"] is not None:
             self.last_universe_losses[uid] = rec["losses"]
@@ -1110,14 +1145,74 @@ class Parallel_Universe_Config(Tester):
         self._remap_cache.clear()
         self._dev_remaps.clear()
 
+    def _gather_spaces(self):
+        """Every rank's trained universes, assembled on rank 0 in id order as CPU modules (None on the
+        other ranks): each rank sends (id, ent_tot, rel_tot, CPU state_dict) of the universes it holds with
+        one gather_object; rank 0 rebuilds the modules with the model factory under a forked RNG (its
+        torch stream is left untouched) and loads the gathered weights."""
+        import torch.distributed as dist
+        world, rank = _dist()
+        mine = []
+        for uid in sorted(self.trained_embedding_spaces):
+            sp = self.trained_embedding_spaces[uid]
+            mine.append((uid, int(sp.ent_tot), int(sp.rel_tot),
+                         {k: v.detach().cpu() for k, v in sp.state_dict().items()}))
+        got = [None] * world if rank == 0 else None
+        dist.gather_object(mine, got, dst=0)
+        if rank != 0:
+            return None
+        spaces = defaultdict(Model)
+        with torch.random.fork_rng(devices=[]):
+            for uid, E_u, R_u, sd in sorted((x for part in got for x in part), key=lambda x: x[0]):
+                if uid in spaces:
+                    raise RuntimeError("universe %d is held by more than one rank" % uid)
+                m = self.embedding_model(E_u, R_u, **self.embedding_model_param)
+                m.load_state_dict(sd)
+                for p in m.parameters():
+                    p.requires_grad = False
+                spaces[uid] = m
+        missing = [u for u in range(self.next_universe_id) if u not in spaces]
+        if missing:
+            raise RuntimeError("universes %s are held by no rank" % missing[:8])
+        return spaces
+
     def save_parameters(self, path):
-        torch.save(self.extend_state_dict(), path)
+        """One checkpoint file of the whole model, the reference's layout (:890-899). With several ranks
+        every universe is gathered to rank 0, which alone writes; all ranks leave after the file exists."""
+        world, rank = _dist()
+        if world == 1:
+            torch.save(self.extend_state_dict(), path)
+            return
+        import torch.distributed as dist
+        spaces = self._gather_spaces()
+        if rank == 0:
+            state = dict(self.extend_state_dict())
+            state['trained_embedding_spaces'] = spaces
+            torch.save(state, path)
+        dist.barrier()
 
     def load_parameters(self, filename):
+        """Load a save_parameters checkpoint (from any world size) and re-shard it over this job's ranks:
+        the universes are placed by LPT on their evaluation cost (entities x dim) and each rank keeps
+        only its own, moved to its GPU when there is one; the id maps stay complete on every rank."""
         # checkpoints written by save_parameters (models + python containers): a full unpickle of a
         # file this code wrote
-        state_dict = torch.load(self.checkpoint_dir + filename, weights_only=False)
+        state_dict = torch.load(self.checkpoint_dir + filename, weights_only=False, map_location="cpu")
         self.process_state_dict(state_dict)
+        world, rank = _dist()
+        spaces = self.trained_embedding_spaces
+        self.universe_owners = {}
+        if world > 1:
+            self.universe_owners = place_universes(
+                {uid: float(spaces[uid].ent_tot) * float(getattr(spaces[uid], "dim", 1)) for uid in spaces}, world)
+            kept = defaultdict(Model)
+            for uid in sorted(spaces):
+                if self.universe_owners[uid] == rank:
+                    kept[uid] = spaces[uid]
+            self.trained_embedding_spaces = spaces = kept
+        if torch.cuda.is_available():
+            for sp in spaces.values():
+                sp.cuda()
 
     def calculate_unembedded_ratio(self, mode='examine_entities'):
         num_unembedded = 0

@@ -116,3 +116,131 @@ def test_lookup_local_absent_and_empty():
     order = np.argsort(em)
     np.testing.assert_array_equal(lookup_local(em[order], order, [3, 4, 9, 100, -1]), [1, -1, 2, -1, -1])
     np.testing.assert_array_equal(lookup_local(np.zeros(0, np.int64), np.zeros(0, np.int64), [1, 2]), [-1, -1])
+
+
+# ---------------------------------------------------------------- placement + multi-rank checkpoints --
+from openke import _native  # noqa: E402
+from openke.config.Parallel_Universe_Config import Parallel_Universe_Config, place_universes, universe_cost  # noqa: E402
+from openke.module.model import TransE  # noqa: E402
+
+_CK_E, _CK_R, _CK_N = 60, 5, 7
+_CK_PARAM = {"dim": 8, "p_norm": 1, "norm_flag": True}
+
+
+def test_lpt_placement_balances_and_is_deterministic():
+    rng = np.random.default_rng(11)
+    costs = {k: universe_cost(int(rng.integers(50, 200)), int(rng.integers(500, 2000)), int(rng.integers(20, 101)))
+             for k in range(512)}
+    for world in (1, 2, 4, 8):
+        owners = place_universes(costs, world)
+        assert owners == place_universes(dict(reversed(list(costs.items()))), world)   # order-free
+        loads = np.zeros(world)
+        for k, r in owners.items():
+            loads[r] += costs[k]
+        # LPT bound: max load <= mean + the largest single cost
+        assert loads.max() <= loads.sum() / world + max(costs.values()) + 1e-6
+        rr = np.zeros(world)
+        for k in costs:
+            rr[k % world] += costs[k]
+        assert loads.max() <= rr.max() + 1e-6   # never worse than round-robin here
+    assert place_universes({}, 4) == {}
+    assert place_universes({3: 1.0, 1: 1.0}, 2) == {1: 0, 3: 1}   # ties by id, then the lowest rank
+
+
+class _StubTrainLoader(object):
+    """The attributes Parallel_Universe_Config reads from its train loader at construction."""
+
+    def __init__(self):
+        self.lib = _native.lib()
+        self.entTotal, self.relTotal = _CK_E, _CK_R
+        self.in_path = "unused/"
+        self.batch_size, self.nbatches = 10, 20
+
+
+def _ck_config(ckpt_dir):
+    return Parallel_Universe_Config(train_dataloader=_StubTrainLoader(), valid_dataloader=object(),
+                                    embedding_model=TransE, embedding_model_param=dict(_CK_PARAM),
+                                    checkpoint_dir=ckpt_dir, initial_num_universes=_CK_N)
+
+
+def _ck_inject(cfg):
+    """Commit _CK_N universes with seeded tables and id maps, as a training wave would (each rank keeps the
+    modules of the universes it owns)."""
+    for uid in range(_CK_N):
+        rng = np.random.default_rng(uid)
+        em = np.sort(rng.choice(_CK_E, 10 + 3 * uid, replace=False))
+        rm = np.sort(rng.choice(_CK_R, 2 + uid % 3, replace=False))
+        torch.manual_seed(100 + uid)
+        kge = TransE(len(em), len(rm), **_CK_PARAM)
+        cfg._commit({"id": uid, "kge": kge, "ent_remap": em, "rel_remap": rm, "losses": None, "tc": 100,
+                     "balance": 0.3, "margin": 1, "epochs": 1, "lr": 0.01, "batch_size": 5, "train_total": 100})
+
+
+def _ck_summary(cfg):
+    return {uid: {k: v.detach().cpu().numpy() for k, v in sp.state_dict().items()}
+            for uid, sp in cfg.trained_embedding_spaces.items()}
+
+
+def _ck_worker(rank, world, port, ckpt_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = _ck_config(ckpt_dir)
+        _ck_inject(cfg)
+        assert sorted(cfg.trained_embedding_spaces) == [u for u in range(_CK_N) if u % world == rank]
+        state = torch.get_rng_state()
+        cfg.save_model("multi.ckpt")
+        assert torch.equal(state, torch.get_rng_state())   # rank 0's rebuild ran under a forked RNG
+        assert os.path.exists(os.path.join(ckpt_dir, "multi.ckpt"))   # written before any rank returns
+        for name in ("single.ckpt", "multi.ckpt"):
+            re = _ck_config(ckpt_dir)
+            re.load_parameters(name)
+            np.save(os.path.join(ckpt_dir, "%s.rank%d.npy" % (name, rank)),
+                    np.array([re.next_universe_id, sorted(re.trained_embedding_spaces), _ck_summary(re),
+                              dict(re.universe_owners), {u: dict(m) for u, m in re.entity_id_mappings.items()}],
+                             dtype=object), allow_pickle=True)
+    finally:
+        dist.destroy_process_group()
+
+
+def _assert_same_spaces(a, b):
+    assert sorted(a) == sorted(b)
+    for uid in a:
+        assert sorted(a[uid]) == sorted(b[uid])
+        for k in a[uid]:
+            np.testing.assert_array_equal(a[uid][k], b[uid][k])
+
+
+def test_multi_rank_checkpoint_matches_single_process(tmp_path):
+    """two gloo ranks commit the same injected universes (each holding its share),
+    save_model gathers them to rank 0 which alone writes; the file equals the single-process checkpoint,
+    and load_parameters re-shards either file over the two ranks (a partition, LPT-placed, same weights)."""
+    ckpt_dir = str(tmp_path) + os.sep
+    single = _ck_config(ckpt_dir)
+    _ck_inject(single)
+    single.save_model("single.ckpt")
+    want = _ck_summary(single)
+    mp.spawn(_ck_worker, args=(2, _free_port(), ckpt_dir), nprocs=2, join=True)
+    a = torch.load(ckpt_dir + "single.ckpt", weights_only=False)
+    b = torch.load(ckpt_dir + "multi.ckpt", weights_only=False)
+    assert sorted(a) == sorted(b)
+    for k in a:
+        if k == "trained_embedding_spaces":
+            _assert_same_spaces({u: {n: t.numpy() for n, t in m.state_dict().items()} for u, m in a[k].items()},
+                                {u: {n: t.numpy() for n, t in m.state_dict().items()} for u, m in b[k].items()})
+        elif k in ("entity_id_mappings", "relation_id_mappings", "entity_universes", "relation_universes"):
+            assert {u: v for u, v in a[k].items() if v} == {u: v for u, v in b[k].items() if v}, k
+        elif k != "embedding_model":
+            assert a[k] == b[k], k
+    for name in ("single.ckpt", "multi.ckpt"):
+        parts = [np.load(os.path.join(ckpt_dir, "%s.rank%d.npy" % (name, r)), allow_pickle=True) for r in range(2)]
+        owners = parts[0][3]
+        assert owners == parts[1][3] and sorted(owners) == list(range(_CK_N))
+        got = {}
+        for r, p in enumerate(parts):
+            assert p[0] == _CK_N
+            assert p[1] == sorted(u for u, o in owners.items() if o == r)
+            assert p[4] == {u: dict(m) for u, m in single.entity_id_mappings.items()}   # maps stay complete
+            got.update(p[2])
+        _assert_same_spaces(got, want)

@@ -222,6 +222,26 @@ def test_pu_link_prediction_matches_reference(path, tmp_path):
                                    z["lp"].astype(np.float32), rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("path", golden("universes_*.npz")[:1], ids=lambda p: p.split("/")[-1])
+def test_pu_checkpoint_round_trip_on_gpu(path, tmp_path):
+    """save_model -> load_parameters (map_location cpu, then onto the GPU) keeps every universe and id map:
+    link prediction of the reloaded model equals the original's, rank for rank."""
+    z = load(path)
+    pu = _pu(z, tmp_path)
+    _inject_reference_universes(pu, z)
+    want = pu.run_link_prediction()
+    want_ranks = [np.array(r).copy() for r in pu.last_ranks]
+    pu.save_model("rt.ckpt")
+    re = _pu(z, tmp_path)
+    re.load_parameters("rt.ckpt")
+    assert re.next_universe_id == pu.next_universe_id
+    assert all(next(sp.parameters()).is_cuda for sp in re.trained_embedding_spaces.values())
+    got = re.run_link_prediction()
+    assert list(got) == list(want)
+    for a, b in zip(re.last_ranks, want_ranks):
+        np.testing.assert_array_equal(np.array(a), b)
+
+
 def _oracle_metrics(z, universes, split, missing="last_rank", with_con=False):
     model, dim, p = str(z["model"]), int(z["dim"]), int(z["p_norm"])
     kg = oracle.KG.load(KG_SMALL)
