@@ -1046,8 +1046,9 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     PT_HIP(hipMalloc(&set->arena, (size_t)total));
     char *base = (char *)set->arena;
     PT_HIP(hipMemset(base, 0, (size_t)us_off));
-    // LDS budget per universe workgroup: the device's per-workgroup limit, at most half a CU (so two
-    // universes share a CU), minus the kernel's static LDS
+    // LDS budget per universe workgroup: the device's per-workgroup limit, at most half a CU, minus the
+    // kernel's static LDS. (The workgroups run one per CU at 256 VGPRs, but the whole CU's LDS measured
+    // slower: C5 37.6 -> 352 ms, C4 104 -> 107 ms, C3 unchanged.)
     int max_lds = 64 << 10;
     (void)hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, set->device);
     const int64_t lds_budget = std::min<int64_t>(max_lds, 80 << 10) - 1024;
@@ -1173,6 +1174,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         return !v || atoi(v) != 0;
     };
     PT_CHECK(used <= lds_budget, PT_EINVAL, "universe batch too large for the LDS work list");
+    const int64_t per_batch = 12 * max_seq;
     // entity rows as contribution lists (heads for entities and relations, next per slot)
     const int64_t heads_b = a4(max_ent + 2 * max_rel) + a4(max_bs * (4 + set->neg));
     C.contrib = used + heads_b <= lds_budget && env_on("PT_UNI_CONTRIB");
@@ -1186,7 +1188,6 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     const int64_t flags_b = a4(nfl);
     C.lds_flags = nfl > 0 && used + flags_b <= lds_budget && env_on("PT_UNI_LDSFLAGS");
     used += C.lds_flags ? flags_b : 0;
-    const int64_t per_batch = 12 * max_seq;
     C.pchunk = env_on("PT_UNI_PRESAMPLE") && per_batch > 0 ? std::min<int64_t>(max_nb, (lds_budget - used) / per_batch)
                                                             : 0;
     if (C.pchunk < 0) C.pchunk = 0;
