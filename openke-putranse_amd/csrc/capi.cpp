@@ -1072,12 +1072,18 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         set->groups.back().work += work(order[k]);
     }
     PT_CHECK(set->groups.size() <= 64, PT_EINVAL, "too many universe shape classes");
-    // CU shares: model a universe's time as steps x (1 + rounds of its step's positives over the shape's
+    // CU shares: model a universe's time as steps x (fixed + rounds of its step's positives over the shape's
     // lane groups); give every group one CU, then each further CU to the group whose LPT makespan over
     // its current share is longest (the launches run concurrently, so the slowest group ends the set)
     {
         int cus = 0;
         PT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, set->device));
+        // a step's cost in rounds of its positives: its fixed part (presampling, the two barriers, phase B)
+        // is worth ~4 rounds (per-universe phase cycles, PT_UNI_PROF: a one-round step costs ~3/4 of a
+        // four-round one); 1 -> 4 moved C3 from 62.1 to 53.9 ms (8: 54.3; one workgroup per universe with
+        // the dispatcher interleaving the class launches, PT_UNI_GRID=1: 59.8)
+        double uni_fixed = 4.0;
+        if (const char *v = pt_tuning_env("PT_UNI_FIXED")) uni_fixed = atof(v);
         std::vector<std::vector<double>> tg(set->groups.size());
         for (size_t k = 0; k < set->groups.size(); ++k) {
             const auto &gr = set->groups[k];
@@ -1085,7 +1091,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
                 const pt_universe_job &J = jobs[order[q]];
                 const int64_t gpb = pt::universe_shape_groups(pt::universe_shape_id(J.dim, model));
                 const int64_t rounds = (std::max<int64_t>(J.batch_size, 1) + gpb - 1) / gpb;
-                tg[k].push_back((double)J.epochs * (double)J.nbatches * (double)(1 + rounds));
+                tg[k].push_back((double)J.epochs * (double)J.nbatches * (double)(uni_fixed + rounds));
             }
             std::sort(tg[k].begin(), tg[k].end(), std::greater<double>());
         }
@@ -1264,7 +1270,14 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
         const auto &gr = set->groups[k];
         const int64_t share = gr.share;
         hipStream_t q = k == 0 ? st : set->streams[k - 1];
-        const hipError_t e = pt::launch_universes(set->d_us + gr.off, gr.n, set->d_counter + k, gr.shape, share,
+        // PT_UNI_GRID=1 (tuning): one workgroup per universe in every launch, the hardware dispatcher
+        // interleaving the class launches as CUs free up, instead of a CU share per launch
+        static const bool per_universe = [] {
+            const char *v = pt_tuning_env("PT_UNI_GRID");
+            return v && atoi(v) != 0;
+        }();
+        const hipError_t e = pt::launch_universes(set->d_us + gr.off, gr.n, set->d_counter + k, gr.shape,
+                                                  per_universe ? gr.n : share,
                                                   set->model, set->p_norm, set->norm_flag, set->opt, set->neg,
                                                   (int)set->bern, (int)set->filter, set->cfg, q);
         if (e != hipSuccess) return pt::fail(PT_EHIP, std::string("launch_universes: ") + hipGetErrorString(e));

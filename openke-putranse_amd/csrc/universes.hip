@@ -53,6 +53,15 @@ __device__ __forceinline__ void phase_barrier(bool agent) {
     }
 }
 
+// Hardware sqrt / reciprocal (1 ulp, v_sqrt_f32 / v_rcp_f32), as in the C2 training step, for the row
+// shapes of at most 8 floats per lane: a correctly rounded division or square root is ~10 VALU
+// instructions in a kernel bound by instruction issue. The 16-float class (long TransE rows, C4) keeps the
+// IEEE forms: its register allocation with the hardware forms slowed its phase A by 25% (C4 105 -> 120 ms),
+// and there a 1-ulp difference in a normalization was seen amplified by a cancelling gradient sum to
+// 5.3e-6 (one component, above the teacher-forced tolerance). The reference-order kernel (ordered.hip)
+// keeps IEEE forms throughout.
+constexpr bool kUF = true;
+
 // Gradient sink of one universe.
 //   contrib != null: entity rows go to contribution slots (plain stores) linked per row in LDS
 //   (head[row] -> c -> next[c] -> ... -> -1); otherwise float atomics into gent.
@@ -124,6 +133,7 @@ template <int G, int VEC, int KCH, typename Sink, typename NegFn>
 __device__ __forceinline__ float transe_step(const StepParams &P, int64_t hp, int64_t rp, int64_t tp, int64_t neg,
                                              NegFn get_neg, const Sink &sink, int lane) {
     using Vec = V<G, VEC, KCH>;
+    constexpr bool kFm = kUF && VEC * KCH <= 8;   // hardware sqrt / rcp (see kUF)
     const int D = (int)P.dim;
     const int p = P.p_norm;
     const bool nf = P.norm_flag != 0;
@@ -143,13 +153,13 @@ __device__ __forceinline__ float transe_step(const StepParams &P, int64_t hp, in
         vload(x, P.ent + e * D, D, lane);
     }
     if (nf) {
-        vnormalize(hh, hh);
-        vnormalize(rh, rh);
-        vnormalize(th, th);
+        vnormalize<kFm>(hh, hh);
+        vnormalize<kFm>(rh, rh);
+        vnormalize<kFm>(th, th);
     }
 #pragma unroll
     for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
-    const float ps = vpnorm(vpos, p);
+    const float ps = vpnorm<kFm>(vpos, p);
     Vec aH, aT, aR;
     vzero(aH); vzero(aT); vzero(aR);
     float csum = 0.f, lsum = 0.f;
@@ -159,16 +169,16 @@ __device__ __forceinline__ float transe_step(const StepParams &P, int64_t hp, in
             get_neg(k, e, tail_side);
             vload(x, P.ent + e * D, D, lane);
         }
-        if (nf) vnormalize(x, x);
+        if (nf) vnormalize<kFm>(x, x);
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) x.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - x.x[i] : (x.x[i] + rh.x[i]) - th.x[i];
-        const float ns = vpnorm(x, p);
+        const float ns = vpnorm<kFm>(x, p);
         const float a = ps - ns;
         lsum += a > -m ? a : -m;
         const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
         if (c == 0.f) continue;
         csum += c;
-        vpnorm_bwd(x, ns, p, -c, x);   // x := d loss / d v_k
+        vpnorm_bwd<kFm>(x, ns, p, -c, x);   // x := d loss / d v_k
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) {
             aR.x[i] += x.x[i];
@@ -181,7 +191,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, int64_t hp, in
         sink.ent(e, x, D, lane);   // corrupted tail gets -g, corrupted head +g
     }
     if (csum != 0.f) {
-        vpnorm_bwd(vpos, ps, p, csum, vpos);
+        vpnorm_bwd<kFm>(vpos, ps, p, csum, vpos);
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) {
             aH.x[i] += vpos.x[i];
@@ -204,6 +214,7 @@ template <int G, int VEC, int KCH, typename Sink, typename NegFn>
 __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, int64_t rp, int64_t tp, int64_t neg,
                                              NegFn get_neg, const Sink &sink, int lane) {
     using Vec = V<G, VEC, KCH>;
+    constexpr bool kFm = kUF && VEC * KCH <= 8;   // hardware sqrt / rcp (see kUF)
     const int D = (int)P.dim;
     const int p = P.p_norm;
     const bool nf = P.norm_flag != 0;
@@ -219,7 +230,7 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
         get_neg(0, e, tail_side);
         vload(X, P.ent + e * D, D, lane);
     }
-    vnormalize(nW, nW);
+    vnormalize<kFm>(nW, nW);
     const float hdot = vdot(H, nW), tdot = vdot(T, nW);
 #pragma unroll
     for (int i = 0; i < Vec::N; ++i) {
@@ -228,13 +239,13 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
     }
     float hn = 0.f, tn = 0.f;
     if (nf) {
-        hn = vnormalize(hh, hh);
-        vnormalize(rh, rh);
-        tn = vnormalize(th, th);
+        hn = vnormalize<kFm>(hh, hh);
+        vnormalize<kFm>(rh, rh);
+        tn = vnormalize<kFm>(th, th);
     }
 #pragma unroll
     for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
-    const float ps = vpnorm(vpos, p);
+    const float ps = vpnorm<kFm>(vpos, p);
     Vec aH, aT, aR, aW;
     vzero(aH); vzero(aT); vzero(aR); vzero(aW);
     float csum = 0.f, lsum = 0.f;
@@ -249,17 +260,17 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) xs.x[i] = X.x[i] - ed * nW.x[i];
         float en = 0.f;
-        if (nf) en = vnormalize(xs, xh); else xh = xs;
+        if (nf) en = vnormalize<kFm>(xs, xh); else xh = xs;
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i)
             vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - xh.x[i] : (xh.x[i] + rh.x[i]) - th.x[i];
-        const float ns = vpnorm(vk, p);
+        const float ns = vpnorm<kFm>(vk, p);
         const float a = ps - ns;
         lsum += a > -m ? a : -m;
         const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
         if (c == 0.f) continue;
         csum += c;
-        vpnorm_bwd(vk, ns, p, -c, vk);   // vk := d loss / d v_k
+        vpnorm_bwd<kFm>(vk, ns, p, -c, vk);   // vk := d loss / d v_k
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) {
             aR.x[i] += vk.x[i];
@@ -267,7 +278,7 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
             xh.x[i] = tail_side ? -vk.x[i] : vk.x[i];   // d / d(normalized projected corrupted row)
         }
         Vec gp;
-        if (nf) vnormalize_bwd(xs, en, xh, gp); else gp = xh;
+        if (nf) vnormalize_bwd<kFm>(xs, en, xh, gp); else gp = xh;
         const float ng = vdot(nW, gp);
         Vec gw;
 #pragma unroll
@@ -280,7 +291,7 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
         sink.ent(e, xh, D, lane);
     }
     if (csum != 0.f) {
-        vpnorm_bwd(vpos, ps, p, csum, vpos);
+        vpnorm_bwd<kFm>(vpos, ps, p, csum, vpos);
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) {
             aH.x[i] += vpos.x[i];
@@ -296,7 +307,7 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
         Vec es, gp;
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) es.x[i] = E.x[i] - edot * nW.x[i];
-        if (nf) vnormalize_bwd(es, en, acc, gp); else gp = acc;
+        if (nf) vnormalize_bwd<kFm>(es, en, acc, gp); else gp = acc;
         const float ng = vdot(nW, gp);
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) {
@@ -496,6 +507,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             const int n = s_count;
             // (TransH: 2 rows of 8 floats per lane in flight spill its step's registers; TransE keeps 2)
             constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? (MODEL == 1 ? 1 : 2) : 4);
+            constexpr bool kFastUpd = kUF && VEC * KCH <= 8;
             // (guards, not breaks, inside the unrolled loops: the row arrays must stay in registers)
             for (int i0 = grp * RB; i0 < n; i0 += GPB * RB) {
                 Vec x[RB], gs[RB], a[RB], y[RB];
@@ -547,8 +559,8 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     const bool jac = table == 0 ? (MODEL == 0 && norm_flag) : (table == 1 ? norm_flag != 0 : true);
                     Vec gg;
                     if (jac) {
-                        const float nx = sqrtf(vdot(x[u], x[u]));
-                        vnormalize_bwd(x[u], nx, gs[u], gg);
+                        const float nx = fsqrt<kFastUpd>(vdot(x[u], x[u]));
+                        vnormalize_bwd<kFastUpd>(x[u], nx, gs[u], gg);
                     } else {
                         gg = gs[u];
                     }
@@ -559,7 +571,10 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
 #pragma unroll
                         for (int j = 0; j < Vec::N; ++j) {
                             a[u].x[j] = a[u].x[j] + gg.x[j] * gg.x[j];
-                            x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j] / (sqrtf(a[u].x[j]) + 1e-10f);
+                            if constexpr (kFastUpd)
+                                x[u].x[j] = x[u].x[j] + (-U.lr) * (gg.x[j] * frcp<true>(fsqrt<true>(a[u].x[j]) + 1e-10f));
+                            else
+                                x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j] / (sqrtf(a[u].x[j]) + 1e-10f);
                         }
                         vstore(a[u], ap, (int)D, lane);
                     }
