@@ -1,679 +1,8 @@
-// Persistent multi-universe trainer (PuTransE / PuTransH, BASELINE configs C3-C5).
-//
-// The reference trains its universes one after another, each with Trainer.run over
-// epochs x nbatches tiny minibatches (Parallel_Universe_Config.py:228-258, Trainer.py:90-104); a
-// universe step is ~25-100 positives, far too small for a launch per step. Here ONE workgroup owns
-// ONE universe for its whole training run: every epoch and minibatch is a loop iteration inside the
-// kernel, with two workgroup barriers per step that give the reference's minibatch-synchronous
-// semantics (every gradient of a step sees the pre-step tables):
-//
-//   sample   every `pchunk` steps the next pchunk batches (TrainDataLoader.sampling() calls) are drawn
-//            at once into LDS, lane-parallel (stream jumps, rng.h);
-//   phase A  each lane group takes positives b = grp, grp + GPB, ... of the step and runs group_step
-//            (forward, MarginLoss, backward). Gradient rows leave it through the sink:
-//              entity rows  -> written with plain stores to a per-universe contribution slot and
-//                              linked into the row's LDS list (no float atomics: 512 universes x
-//                              ~40 K row-element atomics per step saturate the L2 atomic units);
-//              relation / norm_vector rows -> LDS float atomics into LDS gradient rows (a universe
-//                              has few relations, and every positive of a step hits its relation);
-//            the first touch of a row appends it to an LDS work list;
-//   phase B  lane groups walk the work list, RB rows at a time: sum the row's contributions, normalize
-//            Jacobian of the pre-step row where the gradient is in normalized space, Adagrad (or SGD)
-//            update, reset the row's LDS state.
-//
-// Whatever does not fit the LDS budget falls back to global memory (atomic gradient rows, flag arrays,
-// per-step sampling). Universes are independent, so thousands run concurrently (one per workgroup,
-// several per CU); universes of different row shapes run as separate launches on separate streams.
-#include <hip/hip_runtime.h>
-
-#include <cstdint>
-#include <cstdlib>
-
-#include "tuning.h"
-#include "device.h"
-#include "kernels.h"
-#include "universes.h"
+// Persistent multi-universe trainer: host side (row shapes, shape classes, the LDS plan dispatch) and the
+// general (plan 0) kernels. Device code in universes_kern.h; plans 1 and 2 in universes_p1.hip / _p2.hip.
+#include "universes_kern.h"
 
 namespace pt {
-namespace dev {
-
-// release / acquire at agent scope around the workgroup barrier: stores of one phase are visible to
-// loads of the next phase from any wave (L1 invalidated), independent of L1 write policy
-// (needed while gradient rows are float atomics performed at L2: a later plain load must not hit a
-// stale L1 line). Without global atomics in the step (contribution lists + LDS relation rows + LDS
-// flags) every cross-wave exchange is plain stores / loads or LDS within the workgroup, which the
-// workgroup barrier alone orders (all waves of a workgroup share the CU's L1).
-__device__ __forceinline__ void phase_barrier(bool agent) {
-    if (agent) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    } else {
-        __syncthreads();
-    }
-}
-
-// Hardware sqrt / reciprocal (1 ulp, v_sqrt_f32 / v_rcp_f32), as in the C2 training step, for the row
-// shapes of at most 8 floats per lane: a correctly rounded division or square root is ~10 VALU
-// instructions in a kernel bound by instruction issue. The 16-float class (long TransE rows, C4) keeps the
-// IEEE forms: its register allocation with the hardware forms slowed its phase A by 25% (C4 105 -> 120 ms),
-// and there a 1-ulp difference in a normalization was seen amplified by a cancelling gradient sum to
-// 5.3e-6 (one component, above the teacher-forced tolerance). The reference-order kernel (ordered.hip)
-// keeps IEEE forms throughout.
-constexpr bool kUF = true;
-
-// Gradient sink of one universe.
-//   contrib != null: entity rows go to contribution slots (plain stores) linked per row in LDS
-//   (head[row] -> c -> next[c] -> ... -> -1); otherwise float atomics into gent.
-//   grel / gnorm point to LDS gradient rows or to global ones (float atomics either way).
-struct UniverseSink {
-    float *gent, *grel, *gnorm;
-    int32_t *fent, *frel, *fnorm;
-    int32_t *list;
-    int *count;
-    float *contrib;      // [ccap][D] (global) or null: entity rows as contribution lists
-    int32_t *head;       // [E + 2R] LDS list heads (entity rows, then relation rows, then norm_vector rows)
-    int32_t *next;       // [ccap] LDS
-    int *ccount;         // LDS counter of contribution slots
-    int64_t E, R;
-    bool rel_list;       // relation / norm_vector rows as contribution lists too
-    // next contribution slot of the lane group's current positive: positive b owns the static slots
-    // [b * per_pos, (b + 1) * per_pos), per_pos = neg + 2 (+2 with relation lists) >= its links
-    mutable int slot = 0;
-    __device__ __forceinline__ void touch(int32_t *flag, int64_t row, int table) const {
-        if (atomicExch(flag + row, 1) == 0) list[atomicAdd(count, 1)] = (int32_t)(row << 2) | table;
-    }
-    // plain store of the row gradient into a fresh contribution slot, linked into the row's list
-    template <int G, int VEC, int KCH>
-    __device__ __forceinline__ void link(int32_t *h, int64_t row, int table, const V<G, VEC, KCH> &g, int D,
-                                         int lane) const {
-        const int c = slot++;   // group-uniform: every lane of the group makes the same calls
-        vstore(g, contrib + (int64_t)c * D, D, lane);
-        if (lane == 0) {
-            const int32_t prev = atomicExch(h + row, c);
-            next[c] = prev;
-            if (prev < 0) list[atomicAdd(count, 1)] = (int32_t)(row << 2) | table;
-        }
-    }
-    template <int G, int VEC, int KCH>
-    __device__ __forceinline__ void ent(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
-        if (contrib) {
-            link(head, row, 0, g, D, lane);
-        } else {
-            vatomic(g, gent + row * D, D, lane);
-            if (lane == 0) touch(fent, row, 0);
-        }
-    }
-    template <int G, int VEC, int KCH>
-    __device__ __forceinline__ void rel(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
-        if (rel_list) {
-            link(head + E, row, 1, g, D, lane);
-        } else {
-            vatomic(g, grel + row * D, D, lane);
-            if (lane == 0) touch(frel, row, 1);
-        }
-    }
-    template <int G, int VEC, int KCH>
-    __device__ __forceinline__ void norm(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
-        if (rel_list) {
-            link(head + E + R, row, 2, g, D, lane);
-        } else {
-            vatomic(g, gnorm + row * D, D, lane);
-            if (lane == 0) touch(fnorm, row, 2);
-        }
-    }
-};
-
-// TransE step of one positive whose negatives each replace ONE side with entity e (the sampler's
-// structure, Base.cpp:217-232): the same forward / MarginLoss / backward as group_step with a smaller
-// live set (normalized rows kept in place, no per-negative row-role bookkeeping), so the universe
-// kernel stays under 128 VGPRs. get_neg(k, &e, &tail_side). Gradients in normalized space, like
-// group_step for TransE; a corrupted row equal to a positive row is simply a separate contribution.
-template <int G, int VEC, int KCH, typename Sink, typename NegFn>
-__device__ __forceinline__ float transe_step(const StepParams &P, int64_t hp, int64_t rp, int64_t tp, int64_t neg,
-                                             NegFn get_neg, const Sink &sink, int lane) {
-    using Vec = V<G, VEC, KCH>;
-    constexpr bool kFm = kUF && VEC * KCH <= 8;   // hardware sqrt / rcp (see kUF)
-    const int D = (int)P.dim;
-    const int p = P.p_norm;
-    const bool nf = P.norm_flag != 0;
-    Vec hh, th, rh, vpos;
-    vload(hh, P.ent + hp * D, D, lane);
-    vload(th, P.ent + tp * D, D, lane);
-    vload(rh, P.rel + rp * D, D, lane);
-    // long wide rows (16 floats per lane over >= 16 lanes, D > 128): the first negative's row loads
-    // with the positive's, the rest one at a time in the loop (measured: C4, D = 200, 129 -> 108 ms; for
-    // the short rows of C3 the extra live row costs more than the round trip it hides, 66 -> 74 ms)
-    constexpr bool kPrefetch = VEC * KCH >= 16 && G >= 16;
-    int64_t e = 0;
-    bool tail_side = false;
-    Vec x;
-    if (kPrefetch && neg > 0) {
-        get_neg(0, e, tail_side);
-        vload(x, P.ent + e * D, D, lane);
-    }
-    if (nf) {
-        vnormalize<kFm>(hh, hh);
-        vnormalize<kFm>(rh, rh);
-        vnormalize<kFm>(th, th);
-    }
-#pragma unroll
-    for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
-    const float ps = vpnorm<kFm>(vpos, p);
-    Vec aH, aT, aR;
-    vzero(aH); vzero(aT); vzero(aR);
-    float csum = 0.f, lsum = 0.f;
-    const float m = P.margin, inv = P.inv_count;
-    for (int64_t k = 0; k < neg; ++k) {
-        if (!kPrefetch || k > 0) {
-            get_neg(k, e, tail_side);
-            vload(x, P.ent + e * D, D, lane);
-        }
-        if (nf) vnormalize<kFm>(x, x);
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) x.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - x.x[i] : (x.x[i] + rh.x[i]) - th.x[i];
-        const float ns = vpnorm<kFm>(x, p);
-        const float a = ps - ns;
-        lsum += a > -m ? a : -m;
-        const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
-        if (c == 0.f) continue;
-        csum += c;
-        vpnorm_bwd<kFm>(x, ns, p, -c, x);   // x := d loss / d v_k
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            aR.x[i] += x.x[i];
-            if (tail_side) aH.x[i] += x.x[i]; else aT.x[i] -= x.x[i];
-        }
-        if (tail_side) {
-#pragma unroll
-            for (int i = 0; i < Vec::N; ++i) x.x[i] = -x.x[i];
-        }
-        sink.ent(e, x, D, lane);   // corrupted tail gets -g, corrupted head +g
-    }
-    if (csum != 0.f) {
-        vpnorm_bwd<kFm>(vpos, ps, p, csum, vpos);
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            aH.x[i] += vpos.x[i];
-            aR.x[i] += vpos.x[i];
-            aT.x[i] -= vpos.x[i];
-        }
-    }
-    if (vnonzero(aR)) sink.rel(rp, aR, D, lane);
-    if (vnonzero(aH)) sink.ent(hp, aH, D, lane);
-    if (vnonzero(aT)) sink.ent(tp, aT, D, lane);
-    return lsum;
-}
-
-// TransH counterpart of transe_step (group_step's TransH algebra with the sampler's one-side negatives):
-// the relation, its normal vector and the uncorrupted side are the positive's, kept on chip; the
-// projected positive rows are re-formed where the backward needs them instead of being held (the
-// universe kernel's register budget). Entity gradients leave raw (projection and normalize Jacobians
-// applied here, they depend on the relation), rel in normalized space, norm_vector in n-hat space.
-template <int G, int VEC, int KCH, typename Sink, typename NegFn>
-__device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, int64_t rp, int64_t tp, int64_t neg,
-                                             NegFn get_neg, const Sink &sink, int lane) {
-    using Vec = V<G, VEC, KCH>;
-    constexpr bool kFm = kUF && VEC * KCH <= 8;   // hardware sqrt / rcp (see kUF)
-    const int D = (int)P.dim;
-    const int p = P.p_norm;
-    const bool nf = P.norm_flag != 0;
-    Vec H, T, rh, nW, hh, th, vpos;
-    vload(H, P.ent + hp * D, D, lane);
-    vload(T, P.ent + tp * D, D, lane);
-    vload(rh, P.rel + rp * D, D, lane);
-    vload(nW, P.normv + rp * D, D, lane);
-    int64_t e = 0;   // the first negative's row loads with the positive's
-    bool tail_side = false;
-    Vec X;
-    if (neg > 0) {
-        get_neg(0, e, tail_side);
-        vload(X, P.ent + e * D, D, lane);
-    }
-    vnormalize<kFm>(nW, nW);
-    const float hdot = vdot(H, nW), tdot = vdot(T, nW);
-#pragma unroll
-    for (int i = 0; i < Vec::N; ++i) {
-        hh.x[i] = H.x[i] - hdot * nW.x[i];
-        th.x[i] = T.x[i] - tdot * nW.x[i];
-    }
-    float hn = 0.f, tn = 0.f;
-    if (nf) {
-        hn = vnormalize<kFm>(hh, hh);
-        vnormalize<kFm>(rh, rh);
-        tn = vnormalize<kFm>(th, th);
-    }
-#pragma unroll
-    for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
-    const float ps = vpnorm<kFm>(vpos, p);
-    Vec aH, aT, aR, aW;
-    vzero(aH); vzero(aT); vzero(aR); vzero(aW);
-    float csum = 0.f, lsum = 0.f;
-    const float m = P.margin, inv = P.inv_count;
-    for (int64_t k = 0; k < neg; ++k) {
-        if (k > 0) {
-            get_neg(k, e, tail_side);
-            vload(X, P.ent + e * D, D, lane);
-        }
-        Vec xs, xh, vk;
-        const float ed = vdot(X, nW);
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) xs.x[i] = X.x[i] - ed * nW.x[i];
-        float en = 0.f;
-        if (nf) en = vnormalize<kFm>(xs, xh); else xh = xs;
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i)
-            vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - xh.x[i] : (xh.x[i] + rh.x[i]) - th.x[i];
-        const float ns = vpnorm<kFm>(vk, p);
-        const float a = ps - ns;
-        lsum += a > -m ? a : -m;
-        const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
-        if (c == 0.f) continue;
-        csum += c;
-        vpnorm_bwd<kFm>(vk, ns, p, -c, vk);   // vk := d loss / d v_k
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            aR.x[i] += vk.x[i];
-            if (tail_side) aH.x[i] += vk.x[i]; else aT.x[i] -= vk.x[i];
-            xh.x[i] = tail_side ? -vk.x[i] : vk.x[i];   // d / d(normalized projected corrupted row)
-        }
-        Vec gp;
-        if (nf) vnormalize_bwd<kFm>(xs, en, xh, gp); else gp = xh;
-        const float ng = vdot(nW, gp);
-        Vec gw;
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            xh.x[i] = gp.x[i] - nW.x[i] * ng;
-            gw.x[i] = -(ed * gp.x[i] + ng * X.x[i]);
-        }
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) aW.x[i] += gw.x[i];
-        sink.ent(e, xh, D, lane);
-    }
-    if (csum != 0.f) {
-        vpnorm_bwd<kFm>(vpos, ps, p, csum, vpos);
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            aH.x[i] += vpos.x[i];
-            aR.x[i] += vpos.x[i];
-            aT.x[i] -= vpos.x[i];
-        }
-    }
-    if (vnonzero(aR)) sink.rel(rp, aR, D, lane);
-    // the positive's two entity rows (a lambda over explicit operands, not a loop selecting arrays by
-    // index: that would take their addresses and move them to scratch)
-    auto finish = [&](const Vec &acc, const Vec &E, float edot, float en, int64_t row) {
-        if (!vnonzero(acc)) return;
-        Vec es, gp;
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) es.x[i] = E.x[i] - edot * nW.x[i];
-        if (nf) vnormalize_bwd<kFm>(es, en, acc, gp); else gp = acc;
-        const float ng = vdot(nW, gp);
-#pragma unroll
-        for (int i = 0; i < Vec::N; ++i) {
-            es.x[i] = gp.x[i] - nW.x[i] * ng;
-            aW.x[i] -= edot * gp.x[i] + ng * E.x[i];
-        }
-        sink.ent(row, es, D, lane);
-    };
-    finish(aH, H, hdot, hn, hp);
-    finish(aT, T, tdot, tn, tp);
-    if (vnonzero(aW)) sink.norm(rp, aW, D, lane);
-    return lsum;
-}
-
-// Dynamic LDS layout (int32 units; the host sizes it for the largest universe of the launch):
-//   list[list_cap] | flags[E + 2R] or [2R] | head[E] + next[ccap] (contrib) |
-//   batch h, r, t [3][pchunk * bs * (1 + neg)] (pchunk > 0) | rel (+ norm) gradient rows [R][D] floats
-// LDS state of a universe workgroup that is not in the dynamic area (declared once by the kernel)
-struct UniShared {
-    int32_t *dyn;
-    uint64_t *states;   // [64]
-    int *count, *ccount;
-    float *loss;
-};
-
-// One universe's whole training run (all epochs x nbatches steps) by the calling workgroup.
-template <int MODEL, int G, int VEC, int KCH, int NT>
-__device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, int norm_flag, int opt, int64_t neg,
-                                             int bern, int filter, const UniverseLaunch &cfg, const UniShared &S) {
-    using Vec = V<G, VEC, KCH>;
-    constexpr int GPB = NT / G;
-    int32_t *s_dyn = S.dyn;
-    uint64_t *s_states = S.states;
-    int &s_count = *S.count;
-    int &s_ccount = *S.ccount;
-    float &s_loss = *S.loss;
-    const int tid = threadIdx.x, lane = tid % G, grp = tid / G;
-    const int64_t bs = U.bs, threads = U.threads, D = U.dim;
-    const int64_t E = U.g.ent_total, R = U.g.rel_total;
-    const bool contrib = cfg.contrib && U.contrib;
-    const int64_t seq = bs * (1 + neg);
-    const int64_t pchunk = cfg.pchunk < U.nbatches ? cfg.pchunk : U.nbatches;
-    // carve the LDS
-    const bool rel_list = contrib && cfg.rel_list;
-    const int64_t ccap = bs * ((rel_list ? 4 : 2) + neg);
-    int32_t *p = s_dyn;
-    int32_t *s_list = p;
-    p += cfg.list_cap;
-    int32_t *s_flags = p;   // [E (entity atomics only)][R][R] (relation rows not in lists)
-    const int64_t nflags = cfg.lds_flags ? ((contrib ? 0 : E) + (rel_list ? 0 : 2 * R)) : 0;
-    p += (nflags + 3) & ~int64_t(3);
-    int32_t *s_head = p;
-    const int64_t nheads = contrib ? E + 2 * R : 0;
-    int32_t *s_next = p + ((nheads + 3) & ~int64_t(3));
-    if (contrib) p += ((nheads + 3) & ~int64_t(3)) + ((ccap + 3) & ~int64_t(3));
-    int32_t *s_bh = p, *s_br = p + pchunk * seq, *s_bt = p + 2 * pchunk * seq;
-    p += 3 * pchunk * seq;
-    float *s_grel = reinterpret_cast<float *>(p);
-    const int64_t nrelg = cfg.lds_relgrad && !rel_list ? R * D * (MODEL == 1 ? 2 : 1) : 0;
-
-    if (tid < threads) s_states[tid] = U.states[tid];
-    for (int64_t i = tid; i < nflags; i += NT) s_flags[i] = 0;
-    for (int64_t i = tid; i < nheads; i += NT) s_head[i] = -1;
-    for (int64_t i = tid; i < nrelg; i += NT) s_grel[i] = 0.f;
-    StepParams P{};
-    P.model = MODEL; P.p_norm = p_norm; P.norm_flag = norm_flag; P.opt = opt;
-    P.lr = U.lr; P.margin = U.margin;
-    P.ent_total = E; P.rel_total = R; P.dim = D;
-    P.ent = U.ent; P.rel = U.rel; P.normv = U.normv;
-    P.ent_acc = U.ent_acc; P.rel_acc = U.rel_acc; P.norm_acc = U.norm_acc;
-    P.batch_size = bs; P.neg = neg;
-    P.inv_count = 1.0f / (float)(bs * neg);
-    UniverseSink sink{U.gent, U.grel, U.gnorm, U.fent, U.frel, U.fnorm, s_list, &s_count,
-                      contrib ? U.contrib : nullptr, s_head, s_next, &s_ccount, E, R, rel_list};
-    if (cfg.lds_flags) {
-        int32_t *f = s_flags;
-        if (!contrib) {
-            sink.fent = f;
-            f += E;
-        }
-        if (!rel_list) {
-            sink.frel = f;
-            sink.fnorm = f + R;
-        }
-    }
-    if (nrelg) {
-        sink.grel = s_grel;
-        sink.gnorm = s_grel + R * D;
-    }
-    const int64_t dpp = 1 + 2 * neg;
-    const DeviceGraph &g = U.g;
-    const int64_t per = bs % threads == 0 ? bs / threads : bs / threads + 1;
-    float epoch_loss = 0.f;
-    uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0;
-    __syncthreads();
-    for (int64_t epoch = 0; epoch < U.epochs; ++epoch) {
-        for (int64_t step = 0; step < U.nbatches; ++step) {
-            if (U.prof) t0 = clock64();
-            const int64_t cs = pchunk > 0 ? step % pchunk : 0;
-            if (pchunk > 0 && cs == 0) {
-                // the next min(pchunk, left) batches drawn at once into LDS: batch j of the chunk is
-                // sampler call j after the chunk-start stream states
-                const int64_t nb = U.nbatches - step < pchunk ? U.nbatches - step : pchunk;
-                for (int64_t q = tid; q < nb * bs; q += NT) {
-                    const int64_t s = q / bs, b = q - s * bs;
-                    const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp, s);
-                    int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
-                    bh[b] = (int32_t)pd.h; br[b] = (int32_t)pd.r; bt[b] = (int32_t)pd.t;
-                    for (int64_t k = 0; k < neg; ++k) {
-                        int side;
-                        const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
-                        const int64_t o = (k + 1) * bs + b;
-                        bh[o] = (int32_t)(side ? pd.h : e);
-                        bt[o] = (int32_t)(side ? e : pd.t);
-                        br[o] = (int32_t)pd.r;
-                    }
-                }
-                __syncthreads();
-                if (tid < threads) {   // the chunk consumed nb calls of the streams
-                    int64_t len = bs - tid * per;
-                    len = len < 0 ? 0 : (len > per ? per : len);
-                    s_states[tid] = lcg_jump(s_states[tid], (uint64_t)(len * dpp * nb));
-                }
-            }
-            if (tid == 0) {
-                s_count = 0;
-                s_ccount = 0;
-                s_loss = 0.f;
-            }
-            phase_barrier(cfg.agent_fence);
-            if (U.prof) {
-                const uint64_t t1 = clock64();
-                t_pre += t1 - t0;
-                t0 = t1;
-            }
-            // ---- phase A: forward + backward of the step's positives
-            for (int64_t b = grp; b < bs; b += GPB) {
-                float lsum;
-                sink.slot = (int)(b * ((rel_list ? 4 : 2) + neg));
-                if (pchunk > 0) {
-                    const int32_t *bh = s_bh + cs * seq, *br = s_br + cs * seq, *bt = s_bt + cs * seq;
-                    const int64_t hp = bh[b], rp = br[b], tp = bt[b];
-                    if constexpr (MODEL == 0) {
-                        // a negative shares one side with its positive: the head when the tail was
-                        // corrupted (if both sides match, the negative equals the positive and either
-                        // reading gives the same gradients)
-                        lsum = transe_step<G, VEC, KCH>(
-                            P, hp, rp, tp, neg,
-                            [&](int64_t k, int64_t &e, bool &tail_side) {
-                                const int64_t o = (k + 1) * bs + b;
-                                tail_side = bh[o] == hp;
-                                e = tail_side ? bt[o] : bh[o];
-                            },
-                            sink, lane);
-                    } else {
-                        lsum = transh_step<G, VEC, KCH>(
-                            P, hp, rp, tp, neg,
-                            [&](int64_t k, int64_t &e, bool &tail_side) {
-                                const int64_t o = (k + 1) * bs + b;
-                                tail_side = bh[o] == hp;
-                                e = tail_side ? bt[o] : bh[o];
-                            },
-                            sink, lane);
-                    }
-                } else {
-                    const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp);
-                    if constexpr (MODEL == 0) {
-                        lsum = transe_step<G, VEC, KCH>(
-                            P, pd.h, pd.r, pd.t, neg,
-                            [&](int64_t k, int64_t &e, bool &tail_side) {
-                                int side;
-                                e = draw_negative(g, pd, k, bern, filter, &side);
-                                tail_side = side != 0;
-                            },
-                            sink, lane);
-                    } else {
-                        lsum = transh_step<G, VEC, KCH>(
-                            P, pd.h, pd.r, pd.t, neg,
-                            [&](int64_t k, int64_t &e, bool &tail_side) {
-                                int side;
-                                e = draw_negative(g, pd, k, bern, filter, &side);
-                                tail_side = side != 0;
-                            },
-                            sink, lane);
-                    }
-                }
-                if (lane == 0) atomicAdd(&s_loss, lsum);
-            }
-            phase_barrier(cfg.agent_fence);
-            if (U.prof) {
-                const uint64_t t1 = clock64();
-                t_a += t1 - t0;
-                t0 = t1;
-            }
-            // ---- phase B: row updates of the touched rows, RB rows per lane group at a time (all their
-            // loads in flight together: the pass is a chain of dependent memory round trips otherwise)
-            const int n = s_count;
-            // (TransH: 2 rows of 8 floats per lane in flight spill its step's registers; TransE keeps 2)
-            constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? (MODEL == 1 ? 1 : 2) : 4);
-            constexpr bool kFastUpd = kUF && VEC * KCH <= 8;
-            // (guards, not breaks, inside the unrolled loops: the row arrays must stay in registers)
-            for (int i0 = grp * RB; i0 < n; i0 += GPB * RB) {
-                Vec x[RB], gs[RB], a[RB], y[RB];
-                int32_t code[RB], c1[RB];
-#pragma unroll
-                for (int u = 0; u < RB; ++u) {
-                    code[u] = i0 + u < n ? s_list[i0 + u] : -1;
-                    c1[u] = -1;
-                    if (code[u] >= 0) {
-                        const int table = code[u] & 3;
-                        const int64_t row = code[u] >> 2;
-                        const float *wp = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
-                        const float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
-                        vload(x[u], wp, (int)D, lane);
-                        if (opt != 0) vload(a[u], ap, (int)D, lane);
-                        if ((table == 0 && contrib) || (table > 0 && rel_list)) {
-                            // the row's contributions (linked in LDS): the first two loads issued with the
-                            // row's own, the rest walked below; summed in list order
-                            const int32_t c0 = s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row];
-                            vload(gs[u], U.contrib + (int64_t)c0 * D, (int)D, lane);
-                            c1[u] = s_next[c0];
-                            if (c1[u] >= 0) vload(y[u], U.contrib + (int64_t)c1[u] * D, (int)D, lane);
-                        } else {
-                            vload(gs[u], (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D,
-                                  (int)D, lane);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < RB; ++u) {
-                    if (code[u] >= 0 && c1[u] >= 0) {
-#pragma unroll
-                        for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
-                        for (int32_t c = s_next[c1[u]]; c >= 0; c = s_next[c]) {
-                            vload(y[u], U.contrib + (int64_t)c * D, (int)D, lane);
-#pragma unroll
-                            for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < RB; ++u) {
-                    if (code[u] < 0) continue;
-                    const int table = code[u] & 3;
-                    const int64_t row = code[u] >> 2;
-                    float *wp = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
-                    float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
-                    // ent rows of TransE and every rel / norm_vector row carry normalized-space gradients
-                    const bool jac = table == 0 ? (MODEL == 0 && norm_flag) : (table == 1 ? norm_flag != 0 : true);
-                    Vec gg;
-                    if (jac) {
-                        const float nx = fsqrt<kFastUpd>(vdot(x[u], x[u]));
-                        vnormalize_bwd<kFastUpd>(x[u], nx, gs[u], gg);
-                    } else {
-                        gg = gs[u];
-                    }
-                    if (opt == 0) {
-#pragma unroll
-                        for (int j = 0; j < Vec::N; ++j) x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j];
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < Vec::N; ++j) {
-                            a[u].x[j] = a[u].x[j] + gg.x[j] * gg.x[j];
-                            if constexpr (kFastUpd)
-                                x[u].x[j] = x[u].x[j] + (-U.lr) * (gg.x[j] * frcp<true>(fsqrt<true>(a[u].x[j]) + 1e-10f));
-                            else
-                                x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j] / (sqrtf(a[u].x[j]) + 1e-10f);
-                        }
-                        vstore(a[u], ap, (int)D, lane);
-                    }
-                    vstore(x[u], wp, (int)D, lane);
-                    if ((table == 0 && contrib) || (table > 0 && rel_list)) {
-                        if (lane == 0) s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row] = -1;
-                    } else {
-                        Vec z;
-                        vzero(z);
-                        vstore(z, (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D, (int)D,
-                               lane);
-                        if (lane == 0) (table == 0 ? sink.fent : (table == 1 ? sink.frel : sink.fnorm))[row] = 0;
-                    }
-                }
-            }
-            if (pchunk == 0 && tid < threads) {   // the step consumed bs positives x dpp draws
-                int64_t len = bs - tid * per;
-                len = len < 0 ? 0 : (len > per ? per : len);
-                s_states[tid] = lcg_jump(s_states[tid], (uint64_t)(len * dpp));
-            }
-            if (tid == 0) epoch_loss += s_loss * P.inv_count + U.margin;
-            if (U.prof) {
-                const uint64_t t1 = clock64();
-                t_b += t1 - t0;
-            }
-        }
-        if (tid == 0 && U.losses) U.losses[epoch] = epoch_loss;
-        epoch_loss = 0.f;
-    }
-    phase_barrier(cfg.agent_fence);
-    if (U.prof && tid == 0) {
-        U.prof[0] = t_pre;
-        U.prof[1] = t_a;
-        U.prof[2] = t_b;
-        U.prof[3] = (uint64_t)U.epochs * U.nbatches;
-        U.prof[4] = (uint64_t)bs;
-        U.prof[5] = (uint64_t)D;
-        U.prof[6] = (uint64_t)E;
-    }
-    if (tid < threads) U.states[tid] = s_states[tid];
-}
-
-// row shapes of the universe kernel: narrower lane groups than the single-model kernels (2 x VEC=4
-// or 4 x VEC=1 chunks per lane) so a step's ~25-100 positives and ~100-300 touched rows take few rounds
-#define PT_USHAPES(X)                                                                                  \
-    X(0, 2, 4, 1) X(1, 2, 4, 2) X(2, 4, 4, 2) X(3, 8, 4, 2) X(4, 16, 4, 2) X(5, 32, 4, 2) X(6, 64, 4, 2) \
-    X(7, 2, 1, 1) X(8, 2, 1, 2) X(9, 2, 1, 4) X(10, 4, 1, 4) X(11, 8, 1, 4) X(12, 16, 1, 4)              \
-    X(13, 32, 1, 4) X(14, 64, 1, 4) X(15, 64, 1, 8)                                                      \
-    X(16, 2, 4, 4) X(17, 4, 4, 4) X(18, 8, 4, 4) X(19, 16, 4, 4) X(20, 32, 4, 4) X(21, 64, 4, 4)        \
-    X(22, 2, 1, 8) X(23, 4, 1, 8) X(24, 8, 1, 8) X(25, 16, 1, 8) X(26, 32, 1, 8)
-
-// shape class (one kernel each): 0 = at most 4 floats per lane, 1 = 8, 2 = 16 (TransE's wide shapes)
-#define PT_UCLASS(V_, K_) ((V_) * (K_) <= 4 ? 0 : ((V_) * (K_) <= 8 ? 1 : 2))
-
-// Persistent work-queue kernel of one shape CLASS (rows of <= 4 floats per lane, or wider): a workgroup
-// takes universes (all of this class, in the host's longest-first order) from an atomic counter until
-// the queue is empty - greedy longest-processing-time list scheduling over the launch's workgroups -
-// and runs each with its shape's code path. Two classes instead of one kernel for every shape: each
-// kernel is register-allocated for its own widest shape (one kernel over all shapes spills the narrow
-// ones' state too), and two launches still run concurrently (a launch per shape would need more
-// hardware queues than a process gets).
-template <int MODEL, int NT, int WPE, int CLS>
-__global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__restrict__ us, int64_t n,
-                                                       int *__restrict__ next_universe, int p_norm, int norm_flag,
-                                                       int opt, int64_t neg, int bern, int filter,
-                                                       UniverseLaunch cfg) {
-    extern __shared__ int32_t s_dyn[];
-    __shared__ uint64_t s_states[64];
-    __shared__ int s_count, s_ccount, s_u;
-    __shared__ float s_loss;
-    const UniShared S{s_dyn, s_states, &s_count, &s_ccount, &s_loss};
-    for (;;) {
-        if (threadIdx.x == 0) s_u = atomicAdd(next_universe, 1);
-        __syncthreads();
-        // uniform: readfirstlane makes the descriptor loads below scalar (its fields live in SGPRs, not in
-        // the VGPRs the step's rows need)
-        const int64_t u = __builtin_amdgcn_readfirstlane(s_u);
-        __syncthreads();
-        if (u >= n) break;   // every wave of the workgroup reads the same u: the whole group exits
-        // the 16-float class reads the descriptor's fields where they are used (fewer live scalars: C4 113 ->
-        // 104 ms); the narrower classes keep a register copy (C3 65 vs 68 ms)
-        const UniverseDev Uc = CLS == 2 ? UniverseDev{} : us[u];
-        const UniverseDev &U = CLS == 2 ? us[u] : Uc;
-        switch (U.shape) {
-#define PT_URUN(ID_, G_, V_, K_)                                                                       \
-    case ID_:                                                                                          \
-        if constexpr (PT_UCLASS(V_, K_) == CLS && (MODEL == 0 || ID_ < 16)) /* TransH: narrow shapes */  \
-            universe_run<MODEL, G_, V_, K_, NT>(U, p_norm, norm_flag, opt, neg, bern, filter, cfg, S); \
-        break;
-            PT_USHAPES(PT_URUN)
-#undef PT_URUN
-            default:
-                break;
-        }
-        __syncthreads();
-    }
-}
-
-}  // namespace dev
 
 Shape pick_universe_shape(int64_t D, bool wide) {
     const int VEC = D % 4 == 0 ? 4 : 1;
@@ -704,33 +33,6 @@ int universe_shape_id(int64_t D, int model) {
 
 bool universe_shape_supported(int64_t D, int model) { return universe_shape_id(D, model) >= 0; }
 
-namespace {
-template <int MODEL, int WPE, int CLS>
-hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int64_t cus, int p_norm, int norm_flag, int opt,
-                    int64_t neg, int bern, int filter, const UniverseLaunch &cfg, hipStream_t st) {
-    constexpr int NT = 512;
-    auto kern = dev::k_universes<MODEL, NT, WPE, CLS>;
-    if (cfg.lds_bytes > (64 << 10)) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)cfg.lds_bytes);
-        if (e != hipSuccess) return e;
-    }
-    int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kern), NT,
-                                                                (size_t)cfg.lds_bytes);
-    if (e != hipSuccess) return e;
-    if (per_cu < 1) per_cu = 1;
-    int64_t grid = cus * per_cu;
-    if (grid > n) grid = n;
-    if (grid < 1) grid = 1;
-    e = hipMemsetAsync(counter, 0, sizeof(int), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), (size_t)cfg.lds_bytes, st, d_us, n, counter, p_norm,
-                       norm_flag, opt, neg, bern, filter, cfg);
-    return hipGetLastError();
-}
-}  // namespace
-
 // shape class of a row shape (one kernel per class)
 int universe_shape_class(int shape) {
 #define PT_UCLS(ID_, G_, V_, K_) \
@@ -749,19 +51,29 @@ int universe_shape_groups(int shape) {
     return 1;
 }
 
+// the LDS plan the launch configuration amounts to (universe_run's PLAN): 1 and 2 are compiled apart with
+// their choices fixed, anything else takes the general kernel
+static int universe_plan(const UniverseLaunch &cfg) {
+    if (!cfg.contrib || cfg.pchunk <= 0 || cfg.agent_fence) return 0;
+    if (cfg.rel_list) return 2;
+    return cfg.lds_relgrad && cfg.lds_flags ? 1 : 0;
+}
+
 hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, int cls, int64_t cus, int model,
                             int p_norm, int norm_flag, int opt, int64_t neg, int bern, int filter,
                             const UniverseLaunch &cfg, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    if (cls == 0)
-        return model == 0 ? launch_q<0, 2, 0>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
-                          : launch_q<1, 2, 0>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
-    if (cls == 1)
-        return model == 0 ? launch_q<0, 2, 1>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
-                          : launch_q<1, 2, 1>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
-    if (model == 0)
-        return launch_q<0, 2, 2>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
-    return hipErrorInvalidValue;   // TransH universes use the narrow shapes
+    switch (universe_plan(cfg)) {
+        case 1:
+            return launch_universes_plan<1>(d_us, n, counter, cls, cus, model, p_norm, norm_flag, opt, neg, bern, filter,
+                                            cfg, st);
+        case 2:
+            return launch_universes_plan<2>(d_us, n, counter, cls, cus, model, p_norm, norm_flag, opt, neg, bern, filter,
+                                            cfg, st);
+        default:
+            return launch_universes_plan<0>(d_us, n, counter, cls, cus, model, p_norm, norm_flag, opt, neg, bern, filter,
+                                            cfg, st);
+    }
 }
 
 }  // namespace pt
