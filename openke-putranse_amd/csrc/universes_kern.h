@@ -78,20 +78,20 @@ struct UniverseSink {
     int32_t *head;       // [E + 2R] LDS list heads (entity rows, then relation rows, then norm_vector rows)
     int32_t *next;       // [ccap] LDS
     int *ccount;         // LDS counter of contribution slots
-    int64_t E, R;
+    int E, R;
     bool rel_list;       // relation / norm_vector rows as contribution lists too
     // next contribution slot of the lane group's current positive: positive b owns the static slots
     // [b * per_pos, (b + 1) * per_pos), per_pos = neg + 2 (+2 with relation lists) >= its links
     mutable int slot = 0;
-    __device__ __forceinline__ void touch(int32_t *flag, int64_t row, int table) const {
+    __device__ __forceinline__ void touch(int32_t *flag, int row, int table) const {
         if (atomicExch(flag + row, 1) == 0) list[atomicAdd(count, 1)] = (int32_t)(row << 2) | table;
     }
     // plain store of the row gradient into a fresh contribution slot, linked into the row's list
     template <int G, int VEC, int KCH>
-    __device__ __forceinline__ void link(int32_t *h, int64_t row, int table, const V<G, VEC, KCH> &g, int D,
+    __device__ __forceinline__ void link(int32_t *h, int row, int table, const V<G, VEC, KCH> &g, int D,
                                          int lane) const {
         const int c = slot++;   // group-uniform: every lane of the group makes the same calls
-        vstore(g, contrib + (int64_t)c * D, D, lane);
+        vstore(g, contrib + c * D, D, lane);
         if (lane == 0) {
             const int32_t prev = atomicExch(h + row, c);
             next[c] = prev;
@@ -99,7 +99,7 @@ struct UniverseSink {
         }
     }
     template <int G, int VEC, int KCH>
-    __device__ __forceinline__ void ent(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
+    __device__ __forceinline__ void ent(int row, const V<G, VEC, KCH> &g, int D, int lane) const {
         if (PLAN != 0 || contrib) {
             link(head, row, 0, g, D, lane);
         } else {
@@ -108,7 +108,7 @@ struct UniverseSink {
         }
     }
     template <int G, int VEC, int KCH>
-    __device__ __forceinline__ void rel(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
+    __device__ __forceinline__ void rel(int row, const V<G, VEC, KCH> &g, int D, int lane) const {
         if (PLAN == 2 || (PLAN == 0 && rel_list)) {
             link(head + E, row, 1, g, D, lane);
         } else {
@@ -117,7 +117,7 @@ struct UniverseSink {
         }
     }
     template <int G, int VEC, int KCH>
-    __device__ __forceinline__ void norm(int64_t row, const V<G, VEC, KCH> &g, int D, int lane) const {
+    __device__ __forceinline__ void norm(int row, const V<G, VEC, KCH> &g, int D, int lane) const {
         if (PLAN == 2 || (PLAN == 0 && rel_list)) {
             link(head + E + R, row, 2, g, D, lane);
         } else {
@@ -135,15 +135,15 @@ struct UniverseSink {
 // group_step for TransE; a corrupted row equal to a positive row is simply a separate contribution.
 // Positive q's gradient rows go to sink sk[q] (its own contribution slots). Returns the summed losses.
 template <int NP, int G, int VEC, int KCH, typename Sink, typename NegFn>
-__device__ __forceinline__ float transe_step(const StepParams &P, const int64_t (&hp)[NP], const int64_t (&rp)[NP],
-                                             const int64_t (&tp)[NP], int64_t neg, NegFn get_neg, const Sink (&sk)[NP],
+__device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp)[NP], const int (&rp)[NP],
+                                             const int (&tp)[NP], int neg, NegFn get_neg, const Sink (&sk)[NP],
                                              int lane) {
     using Vec = V<G, VEC, KCH>;
     constexpr bool kFm = kUF && VEC * KCH <= 8;   // hardware sqrt / rcp (see kUF)
     const int D = (int)P.dim;
     const int p = P.p_norm;
     const bool nf = P.norm_flag != 0;
-    Vec hh[NP], th[NP], rh[NP], vpos[NP];
+    Vec hh[NP], th[NP], rh[NP];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
         vload(hh[q], P.ent + hp[q] * D, D, lane);
@@ -154,7 +154,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int64_t 
     // with the positive's, the rest one at a time in the loop (measured: C4, D = 200, 129 -> 108 ms; for
     // the short rows of C3 the extra live row costs more than the round trip it hides, 66 -> 74 ms)
     constexpr bool kPrefetch = VEC * KCH >= 16 && G >= 16;
-    int64_t e[NP];
+    int e[NP];
     bool tail_side[NP];
     Vec x[NP];
 #pragma unroll
@@ -174,18 +174,22 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int64_t 
             vnormalize<kFm>(rh[q], rh[q]);
             vnormalize<kFm>(th[q], th[q]);
         }
+        Vec vpos;
 #pragma unroll
-        for (int i = 0; i < Vec::N; ++i) vpos[q].x[i] = (hh[q].x[i] + rh[q].x[i]) - th[q].x[i];
-        ps[q] = vpnorm<kFm>(vpos[q], p);
+        for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh[q].x[i] + rh[q].x[i]) - th[q].x[i];
+        ps[q] = vpnorm<kFm>(vpos, p);
         csum[q] = lsum[q] = 0.f;
     }
-    Vec aH[NP], aT[NP], aR[NP];
+    // on-chip accumulators of the positive's rows: aH over the tail-corrupted negatives' dL/dv, aT minus the
+    // head-corrupted ones'; the relation's is their difference (with one negative per positive, as in
+    // PuTransE, exactly the same sum; not kept live: the 16-float rows spilled with it)
+    Vec aH[NP], aT[NP];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
-        vzero(aH[q]); vzero(aT[q]); vzero(aR[q]);
+        vzero(aH[q]); vzero(aT[q]);
     }
     const float m = P.margin, inv = P.inv_count;
-    for (int64_t k = 0; k < neg; ++k) {
+    for (int k = 0; k < neg; ++k) {
         if (!kPrefetch || k > 0) {
 #pragma unroll
             for (int q = 0; q < NP; ++q) {
@@ -208,7 +212,6 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int64_t 
                 vpnorm_bwd<kFm>(x[q], ns, p, -c, x[q]);   // x := d loss / d v_k
 #pragma unroll
                 for (int i = 0; i < Vec::N; ++i) {
-                    aR[q].x[i] += x[q].x[i];
                     if (tail_side[q]) aH[q].x[i] += x[q].x[i]; else aT[q].x[i] -= x[q].x[i];
                 }
                 if (tail_side[q]) {
@@ -222,16 +225,22 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int64_t 
     float loss = 0.f;
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
+        Vec aR;
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) aR.x[i] = aH[q].x[i] - aT[q].x[i];
         if (csum[q] != 0.f) {
-            vpnorm_bwd<kFm>(vpos[q], ps[q], p, csum[q], vpos[q]);
+            Vec g;   // the positive's dL/dv, v+ re-formed (same expression as the forward)
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i) g.x[i] = (hh[q].x[i] + rh[q].x[i]) - th[q].x[i];
+            vpnorm_bwd<kFm>(g, ps[q], p, csum[q], g);
 #pragma unroll
             for (int i = 0; i < Vec::N; ++i) {
-                aH[q].x[i] += vpos[q].x[i];
-                aR[q].x[i] += vpos[q].x[i];
-                aT[q].x[i] -= vpos[q].x[i];
+                aH[q].x[i] += g.x[i];
+                aR.x[i] += g.x[i];
+                aT[q].x[i] -= g.x[i];
             }
         }
-        if (vnonzero(aR[q])) sk[q].rel(rp[q], aR[q], D, lane);
+        if (vnonzero(aR)) sk[q].rel(rp[q], aR, D, lane);
         if (vnonzero(aH[q])) sk[q].ent(hp[q], aH[q], D, lane);
         if (vnonzero(aT[q])) sk[q].ent(tp[q], aT[q], D, lane);
         loss += lsum[q];
@@ -245,7 +254,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int64_t 
 // universe kernel's register budget). Entity gradients leave raw (projection and normalize Jacobians
 // applied here, they depend on the relation), rel in normalized space, norm_vector in n-hat space.
 template <int G, int VEC, int KCH, typename Sink, typename NegFn>
-__device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, int64_t rp, int64_t tp, int64_t neg,
+__device__ __forceinline__ float transh_step(const StepParams &P, int hp, int rp, int tp, int neg,
                                              NegFn get_neg, const Sink &sink, int lane) {
     using Vec = V<G, VEC, KCH>;
     constexpr bool kFm = kUF && VEC * KCH <= 8;   // hardware sqrt / rcp (see kUF)
@@ -257,7 +266,7 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
     vload(T, P.ent + tp * D, D, lane);
     vload(rh, P.rel + rp * D, D, lane);
     vload(nW, P.normv + rp * D, D, lane);
-    int64_t e = 0;   // the first negative's row loads with the positive's
+    int e = 0;   // the first negative's row loads with the positive's
     bool tail_side = false;
     Vec X;
     if (neg > 0) {
@@ -284,7 +293,7 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
     vzero(aH); vzero(aT); vzero(aR); vzero(aW);
     float csum = 0.f, lsum = 0.f;
     const float m = P.margin, inv = P.inv_count;
-    for (int64_t k = 0; k < neg; ++k) {
+    for (int k = 0; k < neg; ++k) {
         if (k > 0) {
             get_neg(k, e, tail_side);
             vload(X, P.ent + e * D, D, lane);
@@ -336,7 +345,7 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int64_t hp, in
     if (vnonzero(aR)) sink.rel(rp, aR, D, lane);
     // the positive's two entity rows (a lambda over explicit operands, not a loop selecting arrays by
     // index: that would take their addresses and move them to scratch)
-    auto finish = [&](const Vec &acc, const Vec &E, float edot, float en, int64_t row) {
+    auto finish = [&](const Vec &acc, const Vec &E, float edot, float en, int row) {
         if (!vnonzero(acc)) return;
         Vec es, gp;
 #pragma unroll
@@ -377,7 +386,7 @@ struct UniShared {
 //   0 = the launch configuration's choices at run time (fallbacks: global float atomics, global flags,
 //       per-step sampling).
 template <int MODEL, int G, int VEC, int KCH, int NT, int PLAN>
-__device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, int norm_flag, int opt, int64_t neg,
+__device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, int norm_flag, int opt, int neg,
                                              int bern, int filter, const UniverseLaunch &cfg, const UniShared &S) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = NT / G;
@@ -387,36 +396,39 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     int &s_ccount = *S.ccount;
     float &s_loss = *S.loss;
     const int tid = threadIdx.x, lane = tid % G, grp = tid / G;
-    const int64_t bs = U.bs, threads = U.threads, D = U.dim;
-    const int64_t E = U.g.ent_total, R = U.g.rel_total;
+    // 32-bit sizes and indices (a universe is small): half the scalar registers of 64-bit ones, which the
+    // kernels spill into VGPR lanes
+    const int bs = (int)U.bs, threads = (int)U.threads, D = (int)U.dim;
+    const int E = (int)U.g.ent_total, R = (int)U.g.rel_total;
     const bool contrib = PLAN != 0 || (cfg.contrib && U.contrib);
-    const int64_t seq = bs * (1 + neg);
-    const int64_t pchunk = cfg.pchunk < U.nbatches ? cfg.pchunk : U.nbatches;
+    const int seq = bs * (1 + neg);
+    const int nbatches = (int)U.nbatches, epochs = (int)U.epochs;
+    const int pchunk = (int)(cfg.pchunk < U.nbatches ? cfg.pchunk : U.nbatches);
     const bool presampled = PLAN != 0 || pchunk > 0;
     const bool agent_fence = PLAN == 0 && cfg.agent_fence;
     const bool lds_flags = PLAN == 1 || (PLAN == 0 && cfg.lds_flags);
     // carve the LDS
     const bool rel_list = PLAN == 2 || (PLAN == 0 && contrib && cfg.rel_list);
-    const int64_t ccap = bs * ((rel_list ? 4 : 2) + neg);
+    const int ccap = bs * ((rel_list ? 4 : 2) + neg);
     int32_t *p = s_dyn;
     int32_t *s_list = p;
     p += cfg.list_cap;
     int32_t *s_flags = p;   // [E (entity atomics only)][R][R] (relation rows not in lists)
-    const int64_t nflags = lds_flags ? ((contrib ? 0 : E) + (rel_list ? 0 : 2 * R)) : 0;
-    p += (nflags + 3) & ~int64_t(3);
+    const int nflags = lds_flags ? ((contrib ? 0 : E) + (rel_list ? 0 : 2 * R)) : 0;
+    p += (nflags + 3) & ~3;
     int32_t *s_head = p;
-    const int64_t nheads = contrib ? E + 2 * R : 0;
-    int32_t *s_next = p + ((nheads + 3) & ~int64_t(3));
-    if (contrib) p += ((nheads + 3) & ~int64_t(3)) + ((ccap + 3) & ~int64_t(3));
+    const int nheads = contrib ? E + 2 * R : 0;
+    int32_t *s_next = p + ((nheads + 3) & ~3);
+    if (contrib) p += ((nheads + 3) & ~3) + ((ccap + 3) & ~3);
     int32_t *s_bh = p, *s_br = p + pchunk * seq, *s_bt = p + 2 * pchunk * seq;
     p += 3 * pchunk * seq;
     float *s_grel = reinterpret_cast<float *>(p);
-    const int64_t nrelg = (PLAN == 1 || (PLAN == 0 && cfg.lds_relgrad)) && !rel_list ? R * D * (MODEL == 1 ? 2 : 1) : 0;
+    const int nrelg = (PLAN == 1 || (PLAN == 0 && cfg.lds_relgrad)) && !rel_list ? R * D * (MODEL == 1 ? 2 : 1) : 0;
 
     if (tid < threads) s_states[tid] = U.states[tid];
-    for (int64_t i = tid; i < nflags; i += NT) s_flags[i] = 0;
-    for (int64_t i = tid; i < nheads; i += NT) s_head[i] = -1;
-    for (int64_t i = tid; i < nrelg; i += NT) s_grel[i] = 0.f;
+    for (int i = tid; i < nflags; i += NT) s_flags[i] = 0;
+    for (int i = tid; i < nheads; i += NT) s_head[i] = -1;
+    for (int i = tid; i < nrelg; i += NT) s_grel[i] = 0.f;
     StepParams P{};
     P.model = MODEL; P.p_norm = p_norm; P.norm_flag = norm_flag; P.opt = opt;
     P.lr = U.lr; P.margin = U.margin;
@@ -442,29 +454,29 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
         sink.grel = s_grel;
         sink.gnorm = s_grel + R * D;
     }
-    const int64_t dpp = 1 + 2 * neg;
+    const int dpp = 1 + 2 * neg;
     const DeviceGraph &g = U.g;
-    const int64_t per = bs % threads == 0 ? bs / threads : bs / threads + 1;
+    const int per = bs % threads == 0 ? bs / threads : bs / threads + 1;
     float epoch_loss = 0.f;
     uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0;
     __syncthreads();
-    for (int64_t epoch = 0; epoch < U.epochs; ++epoch) {
-        for (int64_t step = 0; step < U.nbatches; ++step) {
+    for (int epoch = 0; epoch < epochs; ++epoch) {
+        for (int step = 0; step < nbatches; ++step) {
             if (U.prof) t0 = clock64();
-            const int64_t cs = pchunk > 0 ? step % pchunk : 0;
+            const int cs = pchunk > 0 ? step % pchunk : 0;
             if (presampled && cs == 0) {
                 // the next min(pchunk, left) batches drawn at once into LDS: batch j of the chunk is
                 // sampler call j after the chunk-start stream states
-                const int64_t nb = U.nbatches - step < pchunk ? U.nbatches - step : pchunk;
-                for (int64_t q = tid; q < nb * bs; q += NT) {
-                    const int64_t s = q / bs, b = q - s * bs;
+                const int nb = nbatches - step < pchunk ? nbatches - step : pchunk;
+                for (int q = tid; q < nb * bs; q += NT) {
+                    const int s = q / bs, b = q - s * bs;
                     const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp, s);
                     int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
                     bh[b] = (int32_t)pd.h; br[b] = (int32_t)pd.r; bt[b] = (int32_t)pd.t;
-                    for (int64_t k = 0; k < neg; ++k) {
+                    for (int k = 0; k < neg; ++k) {
                         int side;
-                        const int64_t e = draw_negative(g, pd, k, bern, filter, &side);
-                        const int64_t o = (k + 1) * bs + b;
+                        const int e = (int)draw_negative(g, pd, k, bern, filter, &side);
+                        const int o = (k + 1) * bs + b;
                         bh[o] = (int32_t)(side ? pd.h : e);
                         bt[o] = (int32_t)(side ? e : pd.t);
                         br[o] = (int32_t)pd.r;
@@ -472,9 +484,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                 }
                 __syncthreads();
                 if (tid < threads) {   // the chunk consumed nb calls of the streams
-                    int64_t len = bs - tid * per;
+                    int len = bs - tid * per;
                     len = len < 0 ? 0 : (len > per ? per : len);
-                    s_states[tid] = lcg_jump(s_states[tid], (uint64_t)(len * dpp * nb));
+                    s_states[tid] = lcg_jump(s_states[tid], (uint64_t)len * (uint64_t)dpp * (uint64_t)nb);
                 }
             }
             if (tid == 0) {
@@ -489,22 +501,22 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                 t0 = t1;
             }
             // ---- phase A: forward + backward of the step's positives
-            for (int64_t b = grp; b < bs; b += GPB) {
+            for (int b = grp; b < bs; b += GPB) {
                 float lsum;
                 sink.slot = (int)(b * ((rel_list ? 4 : 2) + neg));
                 if (presampled) {
                     const int32_t *bh = s_bh + cs * seq, *br = s_br + cs * seq, *bt = s_bt + cs * seq;
-                    const int64_t hp = bh[b], rp = br[b], tp = bt[b];
+                    const int hp = bh[b], rp = br[b], tp = bt[b];
                     if constexpr (MODEL == 0) {
                         // a negative shares one side with its positive: the head when the tail was
                         // corrupted (if both sides match, the negative equals the positive and either
                         // reading gives the same gradients)
-                        const int64_t hq[1] = {hp}, rq[1] = {rp}, tq[1] = {tp};
+                        const int hq[1] = {hp}, rq[1] = {rp}, tq[1] = {tp};
                         const UniverseSink<PLAN> sk[1] = {sink};
                         lsum = transe_step<1, G, VEC, KCH>(
                             P, hq, rq, tq, neg,
-                            [&](int, int64_t k, int64_t &e, bool &tail_side) {
-                                const int64_t o = (k + 1) * bs + b;
+                            [&](int, int k, int &e, bool &tail_side) {
+                                const int o = (k + 1) * bs + b;
                                 tail_side = bh[o] == hp;
                                 e = tail_side ? bt[o] : bh[o];
                             },
@@ -512,8 +524,8 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     } else {
                         lsum = transh_step<G, VEC, KCH>(
                             P, hp, rp, tp, neg,
-                            [&](int64_t k, int64_t &e, bool &tail_side) {
-                                const int64_t o = (k + 1) * bs + b;
+                            [&](int k, int &e, bool &tail_side) {
+                                const int o = (k + 1) * bs + b;
                                 tail_side = bh[o] == hp;
                                 e = tail_side ? bt[o] : bh[o];
                             },
@@ -522,22 +534,22 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                 } else {
                     const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp);
                     if constexpr (MODEL == 0) {
-                        const int64_t hq[1] = {pd.h}, rq[1] = {pd.r}, tq[1] = {pd.t};
+                        const int hq[1] = {(int)pd.h}, rq[1] = {(int)pd.r}, tq[1] = {(int)pd.t};
                         const UniverseSink<PLAN> sk[1] = {sink};
                         lsum = transe_step<1, G, VEC, KCH>(
                             P, hq, rq, tq, neg,
-                            [&](int, int64_t k, int64_t &e, bool &tail_side) {
+                            [&](int, int k, int &e, bool &tail_side) {
                                 int side;
-                                e = draw_negative(g, pd, k, bern, filter, &side);
+                                e = (int)draw_negative(g, pd, k, bern, filter, &side);
                                 tail_side = side != 0;
                             },
                             sk, lane);
                     } else {
                         lsum = transh_step<G, VEC, KCH>(
-                            P, pd.h, pd.r, pd.t, neg,
-                            [&](int64_t k, int64_t &e, bool &tail_side) {
+                            P, (int)pd.h, (int)pd.r, (int)pd.t, neg,
+                            [&](int k, int &e, bool &tail_side) {
                                 int side;
-                                e = draw_negative(g, pd, k, bern, filter, &side);
+                                e = (int)draw_negative(g, pd, k, bern, filter, &side);
                                 tail_side = side != 0;
                             },
                             sink, lane);
@@ -567,7 +579,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     c1[u] = -1;
                     if (code[u] >= 0) {
                         const int table = code[u] & 3;
-                        const int64_t row = code[u] >> 2;
+                        const int row = code[u] >> 2;
                         const float *wp = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
                         const float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
                         vload(x[u], wp, (int)D, lane);
@@ -576,9 +588,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                             // the row's contributions (linked in LDS): the first two loads issued with the
                             // row's own, the rest walked below; summed in list order
                             const int32_t c0 = s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row];
-                            vload(gs[u], U.contrib + (int64_t)c0 * D, (int)D, lane);
+                            vload(gs[u], U.contrib + c0 * D, (int)D, lane);
                             c1[u] = s_next[c0];
-                            if (c1[u] >= 0) vload(y[u], U.contrib + (int64_t)c1[u] * D, (int)D, lane);
+                            if (c1[u] >= 0) vload(y[u], U.contrib + c1[u] * D, (int)D, lane);
                         } else {
                             vload(gs[u], (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D,
                                   (int)D, lane);
@@ -591,7 +603,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
 #pragma unroll
                         for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
                         for (int32_t c = s_next[c1[u]]; c >= 0; c = s_next[c]) {
-                            vload(y[u], U.contrib + (int64_t)c * D, (int)D, lane);
+                            vload(y[u], U.contrib + c * D, (int)D, lane);
 #pragma unroll
                             for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
                         }
@@ -601,7 +613,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                 for (int u = 0; u < RB; ++u) {
                     if (code[u] < 0) continue;
                     const int table = code[u] & 3;
-                    const int64_t row = code[u] >> 2;
+                    const int row = code[u] >> 2;
                     float *wp = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
                     float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
                     // ent rows of TransE and every rel / norm_vector row carry normalized-space gradients
@@ -640,9 +652,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                 }
             }
             if (!presampled && tid < threads) {   // the step consumed bs positives x dpp draws
-                int64_t len = bs - tid * per;
+                int len = bs - tid * per;
                 len = len < 0 ? 0 : (len > per ? per : len);
-                s_states[tid] = lcg_jump(s_states[tid], (uint64_t)(len * dpp));
+                s_states[tid] = lcg_jump(s_states[tid], (uint64_t)len * (uint64_t)dpp);
             }
             if (tid == 0) epoch_loss += s_loss * P.inv_count + U.margin;
             if (U.prof) {
@@ -678,6 +690,16 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
 // shape class (one kernel each): 0 = at most 4 floats per lane, 1 = 8, 2 = 16 (TransE's wide shapes)
 #define PT_UCLASS(V_, K_) ((V_) * (K_) <= 4 ? 0 : ((V_) * (K_) <= 8 ? 1 : 2))
 
+// whether pick_universe_shape can return (G, VEC, KCH) for the model (TransE: wide shapes, TransH: narrow):
+// with p chunks per lane, a group of more than 2 and fewer than 64 lanes holds exactly p, the 2-lane group
+// up to p and the 64-lane group p or more. Each class kernel compiles only these shapes (fewer paths, a
+// register allocation for fewer of them); TransH rows above 512 floats (class 2) are not supported.
+constexpr bool shape_reachable(int model, int G, int VEC, int KCH) {
+    const int p = (VEC == 4 ? 2 : 4) * (model == 0 ? 2 : 1);
+    if (model == 1 && VEC * KCH > 8) return false;
+    return G == 2 ? KCH <= p : (G == 64 ? KCH >= p : KCH == p);
+}
+
 // Persistent work-queue kernel of one shape CLASS (rows of <= 4 floats per lane, or wider): a workgroup
 // takes universes (all of this class, in the host's longest-first order) from an atomic counter until
 // the queue is empty - greedy longest-processing-time list scheduling over the launch's workgroups -
@@ -710,8 +732,8 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
         switch (U.shape) {
 #define PT_URUN(ID_, G_, V_, K_)                                                                       \
     case ID_:                                                                                          \
-        if constexpr (PT_UCLASS(V_, K_) == CLS && (MODEL == 0 || ID_ < 16)) /* TransH: narrow shapes */  \
-            universe_run<MODEL, G_, V_, K_, NT, PLAN>(U, p_norm, norm_flag, opt, neg, bern, filter, cfg, S); \
+        if constexpr (PT_UCLASS(V_, K_) == CLS && shape_reachable(MODEL, G_, V_, K_))                   \
+            universe_run<MODEL, G_, V_, K_, NT, PLAN>(U, p_norm, norm_flag, opt, (int)neg, bern, filter, cfg, S); \
         break;
             PT_USHAPES(PT_URUN)
 #undef PT_URUN
