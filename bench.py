@@ -252,15 +252,25 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
     slots_all, bytes_all = float(tot[1].item()), float(tot[2].item())
     assert torch.isfinite(losses).all(), "non-finite universe loss"
     if os.environ.get("PT_UNI_PROF") == "1":
-        prof = np.zeros(8 * max(len(jobs), 1), dtype=np.uint64)
+        prof = np.zeros(64 * max(len(jobs), 1), dtype=np.uint64)
         _native.check(L.pt_universe_set_profile(uset, prof.ctypes.data))
-        prof = prof.reshape(-1, 8).astype(np.float64)
+        prof = prof.reshape(-1, 64).astype(np.float64)
         span = prof[:, :3].sum(axis=1)
         for i in np.argsort(-span)[:6]:   # the longest universes (cycles of the last run)
             steps = max(prof[i, 3], 1)
             print("universe-prof span %.1f Mcyc steps %d bs %d D %d E %d  cycles/step: presample %.0f"
                   "  A %.0f  B %.0f" % (span[i] / 1e6, steps, prof[i, 4], prof[i, 5], prof[i, 6],
                                        prof[i, 0] / steps, prof[i, 1] / steps, prof[i, 2] / steps), file=sys.stderr)
+        lu = int(np.argmax(span))
+        st = prof[lu, 8:]
+        if st.any():   # measurement build: stamps of one step of the longest universe (lane group 0)
+            base = st[38]
+            rel = lambda v: "%.0f" % (v - base) if v else "-"
+            print("universe-trace A rounds [start pos-fwd neg-fwd neg-sink end]: " +
+                  " | ".join(" ".join(rel(v) for v in st[6 * r:6 * r + 5]) for r in range(6) if st[6 * r]),
+                  file=sys.stderr)
+            print("universe-trace B start %s rounds %s end %s" % (rel(st[39]), " ".join(rel(v) for v in st[40:54] if v),
+                                                                  rel(st[55])), file=sys.stderr)
         tot_p = prof[:, :3].sum(axis=0) / max(prof[:, 3].sum(), 1)
         print("universe-prof all: cycles/step presample %.0f A %.0f B %.0f" % tuple(tot_p), file=sys.stderr)
         print("universe-prof longest universe: %.1f Mcycles (%.1f ms at 2.4 GHz); run %.1f ms" %

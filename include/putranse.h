@@ -206,9 +206,10 @@ int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, int32_t model
  * [sum of epochs] floats, job-order concatenation of Trainer.run's per-epoch loss sums */
 int pt_universe_set_train(pt_universe_set *s, float *d_losses, void *stream);
 int pt_universe_set_free(pt_universe_set *s);
-/* per-universe cycle counters of the fast kernel (on = 1; off by default) and their readout: out[n][8], per
+/* per-universe cycle counters of the fast kernel (on = 1; off by default) and their readout: out[n][64], per
  * universe (in the set's launch order) shader-clock cycles spent in epoch presampling, phase A, phase B, the
- * step count, batch size, dim and entity count (last train call; out[.][7] unused) */
+ * step count, batch size, dim and entity count (last train call; out[.][7] unused); out[.][8..63]: phase stamps
+ * of one step of lane group 0 in the measurement build (make TUNING=1), zero otherwise */
 int pt_universe_set_profiling(pt_universe_set *s, int32_t on);
 int pt_universe_set_profile(pt_universe_set *s, uint64_t *out);
 /* the current LCG states of job `job` (input order) of a set: `threads` values (host copy; synchronizes) */

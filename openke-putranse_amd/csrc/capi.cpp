@@ -984,7 +984,7 @@ struct pt_universe_set {
     std::vector<pt::UniverseDev> host;    // same order; loss pointers patched per train call
     std::vector<int64_t> host_loss_off;
     std::vector<int64_t> host_of_job;     // job index -> index in host / d_us
-    uint64_t *prof = nullptr;             // PT_UNI_PROF=1: [n][8] cycle counters + shape (device)
+    uint64_t *prof = nullptr;             // PT_UNI_PROF=1: [n][64] cycle counters + shape (+ stamps) (device)
     // reference-order (deterministic) mode (pt_universe_set_deterministic): ordered.hip's universe kernel
     bool ordered = false;
     void *ord_arena = nullptr;            // per universe [4][seq][dim] gradient rows
@@ -1304,20 +1304,20 @@ extern "C" int pt_universe_set_states(pt_universe_set *set, int64_t job, uint64_
 extern "C" int pt_universe_set_profiling(pt_universe_set *set, int32_t on) {
     PT_CHECK(set, PT_EINVAL, "null universe set");
     if (on && !set->prof && !set->host.empty()) {
-        PT_HIP(hipMalloc((void **)&set->prof, 64 * set->host.size()));
-        PT_HIP(hipMemset(set->prof, 0, 64 * set->host.size()));
+        PT_HIP(hipMalloc((void **)&set->prof, 512 * set->host.size()));
+        PT_HIP(hipMemset(set->prof, 0, 512 * set->host.size()));
     }
-    for (size_t i = 0; i < set->host.size(); ++i) set->host[i].prof = on && set->prof ? set->prof + 8 * i : nullptr;
+    for (size_t i = 0; i < set->host.size(); ++i) set->host[i].prof = on && set->prof ? set->prof + 64 * i : nullptr;
     return PT_OK;
 }
 
-// diagnostics: per universe (set order) cycles in presampling / phase A / phase B, steps, batch size, dim and
-// entities of the last train call with profiling on
+// diagnostics: per universe (set order) 64 words: cycles in presampling / phase A / phase B, steps, batch size,
+// dim and entities of the last train call with profiling on; words 8-63 phase stamps of one step (tuning build)
 extern "C" int pt_universe_set_profile(pt_universe_set *set, uint64_t *out) {
     PT_CHECK(set && out, PT_EINVAL, "null argument");
     PT_CHECK(set->prof, PT_ESTATE, "profiling not enabled (pt_universe_set_profiling)");
     PT_HIP(hipDeviceSynchronize());
-    PT_HIP(hipMemcpy(out, set->prof, 64 * set->host.size(), hipMemcpyDeviceToHost));
+    PT_HIP(hipMemcpy(out, set->prof, 512 * set->host.size(), hipMemcpyDeviceToHost));
     return PT_OK;
 }
 

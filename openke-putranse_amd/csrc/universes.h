@@ -20,7 +20,7 @@ struct UniverseDev {
     float *contrib;                                 // [bs*(4+neg)][dim] gradient-row contributions
     float *ord;                                     // reference-order mode: [4][seq][dim] per-slot gradient rows
     float *losses;                                  // [epochs] Trainer.run's per-epoch loss sum (or null)
-    uint64_t *prof;                                 // null, or [8]: cycles (presample, A, B), steps, bs, dim, E, 0
+    uint64_t *prof;                                 // null, or [64]: cycles (presample, A, B), steps, bs, dim, E, 0, stamps
     int64_t threads, bs, nbatches, epochs, dim;
     float lr, margin;
     int32_t shape;                                  // universe_shape_id(dim)

@@ -28,6 +28,13 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// Tuning build only: s_memtime stamps of one step's rounds (lane group 0) into the profiling record
+#ifdef PT_TUNING
+#define PT_USTAMP(ptr, i) do { if ((ptr) && lane == 0) (ptr)[i] = clock64(); } while (0)
+#else
+#define PT_USTAMP(ptr, i) do { } while (0)
+#endif
+
 #include <cstdint>
 #include <cstdlib>
 
@@ -83,6 +90,7 @@ struct UniverseSink {
     // next contribution slot of the lane group's current positive: positive b owns the static slots
     // [b * per_pos, (b + 1) * per_pos), per_pos = neg + 2 (+2 with relation lists) >= its links
     mutable int slot = 0;
+    uint64_t *trace = nullptr;   // tuning build: phase stamps of this positive (null: none)
     __device__ __forceinline__ void touch(int32_t *flag, int row, int table) const {
         if (atomicExch(flag + row, 1) == 0) list[atomicAdd(count, 1)] = (int32_t)(row << 2) | table;
     }
@@ -143,6 +151,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     const int D = (int)P.dim;
     const int p = P.p_norm;
     const bool nf = P.norm_flag != 0;
+    PT_USTAMP(sk[0].trace, 0);
     Vec hh[NP], th[NP], rh[NP];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
@@ -180,6 +189,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
         ps[q] = vpnorm<kFm>(vpos, p);
         csum[q] = lsum[q] = 0.f;
     }
+    PT_USTAMP(sk[0].trace, 1);
     // on-chip accumulators of the positive's rows: aH over the tail-corrupted negatives' dL/dv, aT minus the
     // head-corrupted ones'; the relation's is their difference (with one negative per positive, as in
     // PuTransE, exactly the same sum; not kept live: the 16-float rows spilled with it)
@@ -204,6 +214,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
             for (int i = 0; i < Vec::N; ++i)
                 x[q].x[i] = tail_side[q] ? (hh[q].x[i] + rh[q].x[i]) - x[q].x[i] : (x[q].x[i] + rh[q].x[i]) - th[q].x[i];
             const float ns = vpnorm<kFm>(x[q], p);
+            PT_USTAMP(sk[0].trace, 2);
             const float a = ps[q] - ns;
             lsum[q] += a > -m ? a : -m;
             const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
@@ -219,6 +230,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
                     for (int i = 0; i < Vec::N; ++i) x[q].x[i] = -x[q].x[i];
                 }
                 sk[q].ent(e[q], x[q], D, lane);   // corrupted tail gets -g, corrupted head +g
+                PT_USTAMP(sk[0].trace, 3);
             }
         }
     }
@@ -245,6 +257,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
         if (vnonzero(aT[q])) sk[q].ent(tp[q], aT[q], D, lane);
         loss += lsum[q];
     }
+    PT_USTAMP(sk[0].trace, 4);
     return loss;
 }
 
@@ -463,6 +476,8 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     for (int epoch = 0; epoch < epochs; ++epoch) {
         for (int step = 0; step < nbatches; ++step) {
             if (U.prof) t0 = clock64();
+            // tuning build: stamps of step 5 of epoch 1 (phase A rounds [8 + 6r, +5), phase B rounds [48 + r])
+            uint64_t *const tr = U.prof && epoch == 1 && step == 5 && grp == 0 ? U.prof : nullptr;
             const int cs = pchunk > 0 ? step % pchunk : 0;
             if (presampled && cs == 0) {
                 // the next min(pchunk, left) batches drawn at once into LDS: batch j of the chunk is
@@ -500,10 +515,12 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                 t_pre += t1 - t0;
                 t0 = t1;
             }
+            PT_USTAMP(tr, 46);
             // ---- phase A: forward + backward of the step's positives
             for (int b = grp; b < bs; b += GPB) {
                 float lsum;
                 sink.slot = (int)(b * ((rel_list ? 4 : 2) + neg));
+                sink.trace = tr && b / GPB < 6 ? tr + 8 + 6 * (b / GPB) : nullptr;
                 if (presampled) {
                     const int32_t *bh = s_bh + cs * seq, *br = s_br + cs * seq, *bt = s_bt + cs * seq;
                     const int hp = bh[b], rp = br[b], tp = bt[b];
@@ -570,7 +587,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? (MODEL == 1 ? 1 : 2) : 4);
             constexpr bool kFastUpd = kUF && VEC * KCH <= 8;
             // (guards, not breaks, inside the unrolled loops: the row arrays must stay in registers)
+            PT_USTAMP(tr, 47);
             for (int i0 = grp * RB; i0 < n; i0 += GPB * RB) {
+                if (i0 / (GPB * RB) < 14) PT_USTAMP(tr, 48 + i0 / (GPB * RB));
                 Vec x[RB], gs[RB], a[RB], y[RB];
                 int32_t code[RB], c1[RB];
 #pragma unroll
@@ -660,6 +679,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             if (U.prof) {
                 const uint64_t t1 = clock64();
                 t_b += t1 - t0;
+                PT_USTAMP(tr, 63);
             }
         }
         if (tid == 0 && U.losses) U.losses[epoch] = epoch_loss;
