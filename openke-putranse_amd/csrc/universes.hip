@@ -12,6 +12,7 @@ Shape pick_universe_shape(int64_t D, bool wide) {
     while (G < 64 && (int64_t)G * per_lane < chunks) G <<= 1;
     int KCH = 1;
     while ((int64_t)G * KCH < chunks) KCH <<= 1;
+    if (dev::exact_kch_shape(G, VEC)) KCH = (int)((chunks + G - 1) / G);   // no power-of-two padding (universes_kern.h)
     return Shape{G, VEC, KCH};
 }
 

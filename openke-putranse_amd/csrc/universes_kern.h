@@ -252,12 +252,15 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
                 aT[q].x[i] -= g.x[i];
             }
         }
+        PT_USTAMP(sk[0].trace, 4);
         if (vnonzero(aR)) sk[q].rel(rp[q], aR, D, lane);
+        PT_USTAMP(sk[0].trace, 5);
         if (vnonzero(aH[q])) sk[q].ent(hp[q], aH[q], D, lane);
+        PT_USTAMP(sk[0].trace, 6);
         if (vnonzero(aT[q])) sk[q].ent(tp[q], aT[q], D, lane);
         loss += lsum[q];
     }
-    PT_USTAMP(sk[0].trace, 4);
+    PT_USTAMP(sk[0].trace, 7);
     return loss;
 }
 
@@ -476,7 +479,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     for (int epoch = 0; epoch < epochs; ++epoch) {
         for (int step = 0; step < nbatches; ++step) {
             if (U.prof) t0 = clock64();
-            // tuning build: stamps of step 5 of epoch 1 (phase A rounds [8 + 6r, +5), phase B rounds [48 + r])
+            // tuning build: stamps of step 5 of epoch 1 (phase A rounds [8 + 8r, +8), phase B rounds [48 + r])
             uint64_t *const tr = U.prof && epoch == 1 && step == 5 && grp == 0 ? U.prof : nullptr;
             const int cs = pchunk > 0 ? step % pchunk : 0;
             if (presampled && cs == 0) {
@@ -520,7 +523,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             for (int b = grp; b < bs; b += GPB) {
                 float lsum;
                 sink.slot = (int)(b * ((rel_list ? 4 : 2) + neg));
-                sink.trace = tr && b / GPB < 6 ? tr + 8 + 6 * (b / GPB) : nullptr;
+                sink.trace = tr && b / GPB < 4 ? tr + 8 + 8 * (b / GPB) : nullptr;
                 if (presampled) {
                     const int32_t *bh = s_bh + cs * seq, *br = s_br + cs * seq, *bt = s_bt + cs * seq;
                     const int hp = bh[b], rp = br[b], tp = bt[b];
@@ -705,18 +708,28 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     X(7, 2, 1, 1) X(8, 2, 1, 2) X(9, 2, 1, 4) X(10, 4, 1, 4) X(11, 8, 1, 4) X(12, 16, 1, 4)              \
     X(13, 32, 1, 4) X(14, 64, 1, 4) X(15, 64, 1, 8)                                                      \
     X(16, 2, 4, 4) X(17, 4, 4, 4) X(18, 8, 4, 4) X(19, 16, 4, 4) X(20, 32, 4, 4) X(21, 64, 4, 4)        \
-    X(22, 2, 1, 8) X(23, 4, 1, 8) X(24, 8, 1, 8) X(25, 16, 1, 8) X(26, 32, 1, 8)
+    X(22, 2, 1, 8) X(23, 4, 1, 8) X(24, 8, 1, 8) X(25, 16, 1, 8) X(26, 32, 1, 8)                       \
+    X(27, 16, 1, 5) X(28, 16, 1, 6) X(29, 16, 1, 7) X(30, 8, 1, 5) X(31, 8, 1, 6) X(32, 8, 1, 7)        \
+    X(33, 4, 1, 5) X(34, 4, 1, 6) X(35, 4, 1, 7) X(36, 2, 4, 3) X(37, 4, 4, 3) X(38, 8, 4, 3)           \
+    X(39, 4, 1, 3) X(40, 8, 1, 3) X(41, 16, 1, 3)
 
 // shape class (one kernel each): 0 = at most 4 floats per lane, 1 = 8, 2 = 16 (TransE's wide shapes)
 #define PT_UCLASS(V_, K_) ((V_) * (K_) <= 4 ? 0 : ((V_) * (K_) <= 8 ? 1 : 2))
 
+// Rows of up to 128 floats (16 lanes or fewer) take KCH = ceil(chunks / G) chunks per lane instead of the next
+// power of two: e.g. D = 69 on 16 lanes holds 5 floats per lane, not 8 (C3 48.3 -> 43.3 ms, the longest
+// universe's phase A 21.1k -> 19.2k cycles/step); G = 2 rows and longer rows keep power-of-two chunk counts
+// (2-lane groups: any KCH <= p is already exact; G = 32 / 64: fewer shapes per class kernel)
+constexpr bool exact_kch_shape(int G, int VEC) { return G >= (VEC == 4 ? 2 : 4) && G <= (VEC == 4 ? 8 : 16); }
 // whether pick_universe_shape can return (G, VEC, KCH) for the model (TransE: wide shapes, TransH: narrow):
 // with p chunks per lane, a group of more than 2 and fewer than 64 lanes holds exactly p, the 2-lane group
 // up to p and the 64-lane group p or more. Each class kernel compiles only these shapes (fewer paths, a
 // register allocation for fewer of them); TransH rows above 512 floats (class 2) are not supported.
 constexpr bool shape_reachable(int model, int G, int VEC, int KCH) {
+    // (exact_kch_shape: G in (2, 64), so the 2-lane VEC=4 exact shape is the KCH <= p case below)
     const int p = (VEC == 4 ? 2 : 4) * (model == 0 ? 2 : 1);
     if (model == 1 && VEC * KCH > 8) return false;
+    if (G > 2 && G < 64 && KCH > p / 2 && KCH < p) return exact_kch_shape(G, VEC);   // see pick_universe_shape
     return G == 2 ? KCH <= p : (G == 64 ? KCH >= p : KCH == p);
 }
 
