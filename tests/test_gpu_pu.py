@@ -307,7 +307,7 @@ def test_pu_null_vector_ranks_match_oracle(path, tmp_path):
     _assert_ranks_match(pu.last_ranks, ranks, con_h, con_t)
 
 
-UNIVERSE_DIMS = [8, 20, 50, 100, 20, 64, 69, 23]   # every row-shape class, the odd (scalar-chunk) shapes included
+UNIVERSE_DIMS = [8, 20, 50, 100, 20, 64, 69, 23, 44, 85]   # every row-shape class, odd (scalar-chunk) and non-power-of-two chunk counts included
 
 
 @pytest.mark.parametrize("model,p,neg,bern,filt,opt", [
