@@ -266,8 +266,8 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
         if st.any():   # measurement build: stamps of one step of the longest universe (lane group 0)
             base = st[38]
             rel = lambda v: "%.0f" % (v - base) if v else "-"
-            print("universe-trace A rounds [start pos-fwd neg-fwd neg-sink end]: " +
-                  " | ".join(" ".join(rel(v) for v in st[6 * r:6 * r + 5]) for r in range(6) if st[6 * r]),
+            print("universe-trace A rounds [start pos-fwd neg-fwd neg-sink bwd rel-sink h-sink end]: " +
+                  " | ".join(" ".join(rel(v) for v in st[8 * r:8 * r + 8]) for r in range(4) if st[8 * r]),
                   file=sys.stderr)
             print("universe-trace B start %s rounds %s end %s" % (rel(st[39]), " ".join(rel(v) for v in st[40:54] if v),
                                                                   rel(st[55])), file=sys.stderr)
