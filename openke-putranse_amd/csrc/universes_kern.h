@@ -162,7 +162,10 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     // long wide rows (16 floats per lane over >= 16 lanes, D > 128): the first negative's row loads
     // with the positive's, the rest one at a time in the loop (measured: C4, D = 200, 129 -> 108 ms; for
     // the short rows of C3 the extra live row costs more than the round trip it hides, 66 -> 74 ms)
-    constexpr bool kPrefetch = VEC * KCH >= 16 && G >= 16;
+#ifndef PT_UNI_PREFETCH_ALL
+#define PT_UNI_PREFETCH_ALL 0
+#endif
+    constexpr bool kPrefetch = PT_UNI_PREFETCH_ALL || (VEC * KCH >= 16 && G >= 16);
     int e[NP];
     bool tail_side[NP];
     Vec x[NP];
@@ -253,11 +256,16 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
             }
         }
         PT_USTAMP(sk[0].trace, 4);
-        if (vnonzero(aR)) sk[q].rel(rp[q], aR, D, lane);
-        PT_USTAMP(sk[0].trace, 5);
-        if (vnonzero(aH[q])) sk[q].ent(hp[q], aH[q], D, lane);
-        PT_USTAMP(sk[0].trace, 6);
-        if (vnonzero(aT[q])) sk[q].ent(tp[q], aT[q], D, lane);
+        // no active pair: every accumulator is zero, nothing to route. Otherwise the three rows go out
+        // without a zero test (three lane-group reductions per positive): a row whose sum cancelled to zero
+        // is a zero contribution, and a zero gradient leaves a row and its Adagrad state unchanged
+        if (csum[q] != 0.f) {
+            sk[q].rel(rp[q], aR, D, lane);
+            PT_USTAMP(sk[0].trace, 5);
+            sk[q].ent(hp[q], aH[q], D, lane);
+            PT_USTAMP(sk[0].trace, 6);
+            sk[q].ent(tp[q], aT[q], D, lane);
+        }
         loss += lsum[q];
     }
     PT_USTAMP(sk[0].trace, 7);
@@ -358,11 +366,11 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int hp, int rp
             aT.x[i] -= vpos.x[i];
         }
     }
-    if (vnonzero(aR)) sink.rel(rp, aR, D, lane);
+    if (csum == 0.f) return lsum;   // no active pair: every accumulator is zero (see transe_step)
+    sink.rel(rp, aR, D, lane);
     // the positive's two entity rows (a lambda over explicit operands, not a loop selecting arrays by
     // index: that would take their addresses and move them to scratch)
     auto finish = [&](const Vec &acc, const Vec &E, float edot, float en, int row) {
-        if (!vnonzero(acc)) return;
         Vec es, gp;
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) es.x[i] = E.x[i] - edot * nW.x[i];
@@ -377,7 +385,7 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int hp, int rp
     };
     finish(aH, H, hdot, hn, hp);
     finish(aT, T, tdot, tn, tp);
-    if (vnonzero(aW)) sink.norm(rp, aW, D, lane);
+    sink.norm(rp, aW, D, lane);
     return lsum;
 }
 
