@@ -162,10 +162,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     // long wide rows (16 floats per lane over >= 16 lanes, D > 128): the first negative's row loads
     // with the positive's, the rest one at a time in the loop (measured: C4, D = 200, 129 -> 108 ms; for
     // the short rows of C3 the extra live row costs more than the round trip it hides, 66 -> 74 ms)
-#ifndef PT_UNI_PREFETCH_ALL
-#define PT_UNI_PREFETCH_ALL 0
-#endif
-    constexpr bool kPrefetch = PT_UNI_PREFETCH_ALL || (VEC * KCH >= 16 && G >= 16);
+    constexpr bool kPrefetch = VEC * KCH >= 16 && G >= 16;   // (for every shape: C3 / C4 / C5 unchanged, r03)
     int e[NP];
     bool tail_side[NP];
     Vec x[NP];
