@@ -71,6 +71,18 @@ __device__ __forceinline__ void phase_barrier(bool agent) {
 // keeps IEEE forms throughout.
 constexpr bool kUF = true;
 
+// backward of F.normalize (vnormalize_bwd) without a branch on the norm: the rows of a wave's lane groups
+// take the (g - x (x.g)/n^2) / n form or the clamp's g / eps form by selects, not by divergent paths
+template <bool FAST, int G, int VEC, int KCH>
+__device__ __forceinline__ void unormalize_bwd(const V<G, VEC, KCH> &x, float n, const V<G, VEC, KCH> &g,
+                                               V<G, VEC, KCH> &out) {
+    const bool big = n > kEps;
+    const float inv = big ? frcp<FAST>(n) : 1.0f / kEps;
+    const float c = big ? vdot(g, x) * (inv * inv) : 0.f;
+#pragma unroll
+    for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = (g.x[i] - x.x[i] * c) * inv;
+}
+
 // Gradient sink of one universe.
 //   contrib != null: entity rows go to contribution slots (plain stores) linked per row in LDS
 //   (head[row] -> c -> next[c] -> ... -> -1); otherwise float atomics into gent.
@@ -342,7 +354,7 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int hp, int rp
             xh.x[i] = tail_side ? -vk.x[i] : vk.x[i];   // d / d(normalized projected corrupted row)
         }
         Vec gp;
-        if (nf) vnormalize_bwd<kFm>(xs, en, xh, gp); else gp = xh;
+        if (nf) unormalize_bwd<kFm>(xs, en, xh, gp); else gp = xh;
         const float ng = vdot(nW, gp);
         Vec gw;
 #pragma unroll
@@ -371,7 +383,7 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int hp, int rp
         Vec es, gp;
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) es.x[i] = E.x[i] - edot * nW.x[i];
-        if (nf) vnormalize_bwd<kFm>(es, en, acc, gp); else gp = acc;
+        if (nf) unormalize_bwd<kFm>(es, en, acc, gp); else gp = acc;
         const float ng = vdot(nW, gp);
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) {
@@ -525,6 +537,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             }
             PT_USTAMP(tr, 46);
             // ---- phase A: forward + backward of the step's positives
+            float lacc = 0.f;   // this lane group's positives' loss, one LDS add per step
             for (int b = grp; b < bs; b += GPB) {
                 float lsum;
                 sink.slot = (int)(b * ((rel_list ? 4 : 2) + neg));
@@ -580,8 +593,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                             sink, lane);
                     }
                 }
-                if (lane == 0) atomicAdd(&s_loss, lsum);
+                lacc += lsum;
             }
+            if (lane == 0 && grp < bs) atomicAdd(&s_loss, lacc);
             phase_barrier(agent_fence);
             if (U.prof) {
                 const uint64_t t1 = clock64();
@@ -648,7 +662,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     Vec gg;
                     if (jac) {
                         const float nx = fsqrt<kFastUpd>(vdot(x[u], x[u]));
-                        vnormalize_bwd<kFastUpd>(x[u], nx, gs[u], gg);
+                        unormalize_bwd<kFastUpd>(x[u], nx, gs[u], gg);
                     } else {
                         gg = gs[u];
                     }
