@@ -218,30 +218,61 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
         em = np.zeros(max(E, 1), dtype=np.int64)
         rm = np.zeros(max(R, 1), dtype=np.int64)
         _native.check(L.pt_universe_remaps(h, em.ctypes.data, rm.ctypes.data))
-        unis.append({"ent": ent, "rel": rel, "nv": nv, "em": em[:E], "rm": rm[:R], "dim": D})
+        unis.append({"ent": ent, "rel": rel, "nv": nv, "em": em[:E], "rm": rm[:R], "dim": D,
+                     "init": tuple(x.clone() if x is not None else None for x in (ent, rel, nv))})
         slots = epochs * 20 * bs * 2
         slots_step += slots
         bytes_step += slots * algorithmic_bytes_per_slot(model, "adagrad", D)
-    arr = (_native.UniverseJob * max(len(jobs), 1))(*jobs)
-    uset = ctypes.c_void_p()
-    _native.check(L.pt_universe_set_create(arr, len(jobs), mid, p_norm, 1, _native.PT_ADAGRAD, 0, 0,
-                                           ctypes.byref(uset)))
-    if os.environ.get("PT_UNI_PROF") == "1":
-        _native.check(L.pt_universe_set_profiling(uset, 1))
-    total_epochs = sum(int(j.epochs) for j in jobs)
-    losses = torch.zeros(max(total_epochs, 1), device=dev)
-    stream = _native.stream()
-    for _ in range(args.c3_warmup):
-        _native.check(L.pt_universe_set_train(uset, _native.ptr(losses), stream))
-    torch.cuda.synchronize()
-    barrier(ws)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.c3_steps):
-        _native.check(L.pt_universe_set_train(uset, _native.ptr(losses), stream))
-    torch.cuda.synchronize()
-    barrier(ws)
-    el = time.perf_counter() - t0
+    prof_on = os.environ.get("PT_UNI_PROF") == "1"
+    has_reset = hasattr(L, "pt_universe_set_reset")
+
+    def make_set(idx):
+        """A universe set of jobs[idx]; returns (set handle, reset function restoring every table, Adagrad
+        state and sampler stream to its initial value - each timed run trains from the same start)."""
+        arr = (_native.UniverseJob * max(len(idx), 1))(*[jobs[i] for i in idx])
+        us = ctypes.c_void_p()
+        _native.check(L.pt_universe_set_create(arr, len(idx), mid, p_norm, 1, _native.PT_ADAGRAD, 0, 0,
+                                               ctypes.byref(us)))
+        if prof_on:
+            _native.check(L.pt_universe_set_profiling(us, 1))
+
+        def reset():
+            for i in idx:
+                u = unis[i]
+                for live, init in zip((u["ent"], u["rel"], u["nv"]), u["init"]):
+                    if live is not None:
+                        live.copy_(init)
+                for a in keep[i][1]:
+                    if a is not None:
+                        a.zero_()
+            if has_reset:   # (an older build under A/B lacks it: its streams continue instead)
+                _native.check(L.pt_universe_set_reset(us))
+        return us, reset
+
+    def time_set(us, reset, idx, steps, warmup):
+        """Seconds of `steps` trainings of the set (after `warmup` untimed ones), each from the initial state:
+        the reset outside the timed region, barrier + synchronize on both sides of every timed training."""
+        total_epochs = sum(int(jobs[i].epochs) for i in idx)
+        losses = torch.zeros(max(total_epochs, 1), device=dev)
+        stream = _native.stream()
+        el = 0.0
+        for s_ in range(warmup + steps):
+            reset()
+            torch.cuda.synchronize()
+            barrier(ws)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _native.check(L.pt_universe_set_train(us, _native.ptr(losses), stream))
+            torch.cuda.synchronize()
+            barrier(ws)
+            if s_ >= warmup:
+                el += time.perf_counter() - t0
+        assert torch.isfinite(losses).all(), "non-finite universe loss"
+        return el
+
+    every = list(range(len(jobs)))
+    uset, reset = make_set(every)
+    el = time_set(uset, reset, every, args.c3_steps, args.c3_warmup)
     tot = torch.tensor([el, float(slots_step), float(bytes_step)], dtype=torch.float64, device=dev)
     if ws > 1:
         import torch.distributed as dist
@@ -250,32 +281,52 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
         all_reduce(tot, dist.ReduceOp.SUM)
         el = float(mx.item())
     slots_all, bytes_all = float(tot[1].item()), float(tot[2].item())
-    assert torch.isfinite(losses).all(), "non-finite universe loss"
-    if os.environ.get("PT_UNI_PROF") == "1":
+    longest = None
+    if prof_on:
         prof = np.zeros(64 * max(len(jobs), 1), dtype=np.uint64)
         _native.check(L.pt_universe_set_profile(uset, prof.ctypes.data))
         prof = prof.reshape(-1, 64).astype(np.float64)
         span = prof[:, :3].sum(axis=1)
+        longest = float(span.max())
         for i in np.argsort(-span)[:6]:   # the longest universes (cycles of the last run)
             steps = max(prof[i, 3], 1)
             print("universe-prof span %.1f Mcyc steps %d bs %d D %d E %d  cycles/step: presample %.0f"
                   "  A %.0f  B %.0f" % (span[i] / 1e6, steps, prof[i, 4], prof[i, 5], prof[i, 6],
                                        prof[i, 0] / steps, prof[i, 1] / steps, prof[i, 2] / steps), file=sys.stderr)
-        lu = int(np.argmax(span))
-        st = prof[lu, 8:]
-        if st.any():   # measurement build: stamps of one step of the longest universe (lane group 0)
-            base = st[38]
-            rel = lambda v: "%.0f" % (v - base) if v else "-"
-            print("universe-trace A rounds [start pos-fwd neg-fwd neg-sink bwd rel-sink h-sink end]: " +
-                  " | ".join(" ".join(rel(v) for v in st[8 * r:8 * r + 8]) for r in range(4) if st[8 * r]),
-                  file=sys.stderr)
-            print("universe-trace B start %s rounds %s end %s" % (rel(st[39]), " ".join(rel(v) for v in st[40:54] if v),
-                                                                  rel(st[55])), file=sys.stderr)
         tot_p = prof[:, :3].sum(axis=0) / max(prof[:, 3].sum(), 1)
         print("universe-prof all: cycles/step presample %.0f A %.0f B %.0f" % tuple(tot_p), file=sys.stderr)
         print("universe-prof longest universe: %.1f Mcycles (%.1f ms at 2.4 GHz); run %.1f ms" %
               (span.max() / 1e6, span.max() / 2.4e6, el * 1e3 / args.c3_steps), file=sys.stderr)
+    det_s = None
+    if args.deterministic_timing and ws == 1:
+        # the reference-order mode (bit-identical to the oracle) on the same set, one training from the start
+        _native.check(L.pt_universe_set_deterministic(uset, 1))
+        det_s = time_set(uset, reset, every, 1, 0)
+        _native.check(L.pt_universe_set_deterministic(uset, 0))
     _native.check(L.pt_universe_set_free(uset))
+    placement = None
+    if args.place_world > 1 and ws == 1:
+        # one GPU, the per-rank critical path of a place_world-way job: each rank's LPT share (place_universes,
+        # as Parallel_Universe_Config places a wave) trained alone, from the initial state
+        pw = args.place_world
+        po = place_universes({k: universe_cost(all_draws[k][3], all_draws[k][0], all_dims[k]) for k in own}, pw)
+        shares, spans = [], []
+        for r in range(pw):
+            idx = [i for i, k in enumerate(own) if po[k] == r]
+            us, rs = make_set(idx)
+            if not prof_on:
+                _native.check(L.pt_universe_set_profiling(us, 1))
+            shares.append(time_set(us, rs, idx, args.c3_steps, 1) / args.c3_steps)
+            pr = np.zeros(64 * max(len(idx), 1), dtype=np.uint64)
+            _native.check(L.pt_universe_set_profile(us, pr.ctypes.data))
+            spans.append(float(pr.reshape(-1, 64)[:, :3].astype(np.float64).sum(axis=1).max()) if idx else 0.0)
+            _native.check(L.pt_universe_set_free(us))
+        placement = {"world": pw, "universes_per_rank": [sum(1 for k in own if po[k] == r) for r in range(pw)],
+                     "share_s": shares, "max_share_s": max(shares), "rank0_share_s": shares[0],
+                     "full_set_s": el / args.c3_steps, "max_share_over_full": max(shares) / (el / args.c3_steps),
+                     "longest_universe_cycles_per_share": spans,
+                     "note": "one GPU: rank r's LPT share of a %d-way placement trained alone (the N = %d per-rank "
+                             "critical path); longest-universe spans in shader-clock cycles" % (pw, pw)}
     for i in range(len(own)):
         L.pt_universe_free(handles[i])
     achieved = bytes_all * args.c3_steps / el / 1e9 / max(ws, 1)
@@ -286,17 +337,81 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
            "value": slots_all * args.c3_steps / el, "unit": "triples/s", "scaling": "weak" if per_gpu else "strong",
            "steps": args.c3_steps, "warmup": args.c3_warmup, "s_per_step": el / args.c3_steps,
            "universes_per_gpu": len(own), "host_universe_build_s": build_s,
+           "note_runs": "every timed run trains every universe from its initial tables, Adagrad state and sampler "
+                        "streams (restored before the run, outside the timed region)",
            "roofline": {"bound": "latency (per-universe dependent step chain)", "achieved_per_gpu": achieved,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                         "note": "algorithmic bytes (SURVEY 8(d) per slot) per wall second vs the HBM peak, not an HBM "
                                 "measurement: a universe's working set (tables, Adagrad state, contribution rows, "
                                 "a few hundred KB) is cache-resident and its work lists, relation gradient rows and "
                                 "presampled batches live in LDS, so frac > 1 (C4) means on-chip service"}}
+    if det_s is not None:
+        out["deterministic_s_per_step"] = det_s
+        out["deterministic_triples_per_s"] = slots_step / det_s
+    if placement is not None:
+        out["placement"] = placement
+    if longest is not None:
+        out["longest_universe_cycles"] = longest
     if do_lp:
         out["link_prediction"] = universe_link_prediction(L, path, unis, mid, p_norm, ws, dev)
     L.pt_graph_free(g)
     if cpu and ws == 1 and rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = universe_cpu_baseline(path, name, args.cpu_seconds)
+    return out
+
+
+def run_dropin(args, ws, rank, dev, name="c3"):
+    """The drop-in universe path timed as the reference's experiments drive it
+    (experiments/static_experiment_PuTransE_on_WN18.py:40-91): TrainDataLoader(nbatches 20, threads 8, normal
+    sampling, bern 0, filter 0, neg 1) and TestDataLoader on the same synthetic graph, Parallel_Universe_Config
+    with the workload's hyperparameter ranges, train_parallel_universes(n) with valid_steps = n / 4 (a divisor of
+    n: validation, early-stopping bookkeeping and best-model checkpoints at 4 points, as the experiment's
+    valid_steps 100 does over its 6,000 universes), then run_link_prediction() for C4. The universes are those
+    of the kernel-only line (same seeds 4 + k, draws, dims). Reported: wall seconds of each call and the
+    breakdown Parallel_Universe_Config records (draws, native construction, torch modules, H2D, the training
+    launch, commits, validation + checkpoints)."""
+    import shutil
+    import synth_kg
+    from openke.config import Parallel_Universe_Config
+    from openke.data import TestDataLoader, TrainDataLoader
+    from openke.module.model import TransE, TransH
+    shape, n_univ, model, dim_spec, p_norm, tc_range, margin_range, do_lp = PU_WORKLOADS[name]
+    path = synth_kg.ensure_dataset(os.path.join(args.data_dir, "rank%d" % rank), shape)
+    t0 = time.perf_counter()
+    train_dl = TrainDataLoader(in_path=path, nbatches=20, threads=8, sampling_mode="normal", bern_flag=0,
+                               filter_flag=0, neg_ent=1, neg_rel=0, random_seed=4)
+    test_dl = TestDataLoader(train_dl.in_path, "link")
+    ck = tempfile.mkdtemp(prefix="pu_dropin_") + os.sep
+    cfg = Parallel_Universe_Config(
+        training_identifier="bench_%s" % name, train_dataloader=train_dl, test_dataloader=test_dl,
+        initial_num_universes=None, min_margin=margin_range[0], max_margin=margin_range[1], min_lr=0.001,
+        max_lr=0.1, min_num_epochs=50, max_num_epochs=200, min_triple_constraint=tc_range[0],
+        max_triple_constraint=tc_range[1], min_balance=0.25, max_balance=0.5,
+        embedding_model=TransE if model == "TransE" else TransH,
+        embedding_model_param={"dim": dim_spec, "p_norm": p_norm, "norm_flag": 1},
+        checkpoint_dir=ck, valid_steps=max(n_univ // 4, 1), save_steps=10000, training_setting="static",
+        incremental_strategy=None)
+    setup_s = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    barrier(ws)
+    t0 = time.perf_counter()
+    cfg.train_parallel_universes(n_univ)
+    torch.cuda.synchronize()
+    barrier(ws)
+    train_s = time.perf_counter() - t0
+    out = {"setup_s": setup_s, "train_parallel_universes_s": train_s, "wave_size": cfg.wave_size(),
+           "valid_steps": cfg.valid_steps, "universes_committed": cfg.next_universe_id,
+           "breakdown_s": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in cfg.last_train_timing.items()}}
+    if do_lp:
+        torch.cuda.synchronize()
+        barrier(ws)
+        t0 = time.perf_counter()
+        met = cfg.run_link_prediction()
+        torch.cuda.synchronize()
+        barrier(ws)
+        out["run_link_prediction_s"] = time.perf_counter() - t0
+        out["mrr_mr_hit10_hit3_hit1"] = [float(x) for x in met]
+    shutil.rmtree(ck, ignore_errors=True)
     return out
 
 
@@ -460,11 +575,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS) + sorted(PU_WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--repeats", type=int, default=5, help="timed repeats of the K-step run (value = median)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--data-dir", default=os.path.join(tempfile.gettempdir(), "putranse_bench"))
     ap.add_argument("--no-c3", action="store_true", help="skip the PuTransE universe workload (C3) field")
     ap.add_argument("--c3-steps", type=int, default=2)
     ap.add_argument("--c3-warmup", type=int, default=1)
+    ap.add_argument("--place-world", type=int, default=0,
+                    help="universe workloads on one GPU: also time each rank's LPT share of a PLACE_WORLD-way job")
+    ap.add_argument("--deterministic-timing", type=int, default=1,
+                    help="also time the reference-order (deterministic) mode (1: yes)")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="universe workloads: skip the drop-in Parallel_Universe_Config timing")
     args = ap.parse_args()
 
     ws, rank, local = dist_setup()
@@ -472,6 +594,7 @@ def main():
         dev = torch.device("cuda", torch.cuda.current_device())
         args.c3_steps, args.c3_warmup = args.steps, args.warmup
         c3 = run_universes(args, ws, rank, dev, args.workload)
+        dropin = None if args.no_dropin else run_dropin(args, ws, rank, dev, args.workload)
         if rank == 0:
             rec = {"metric": "training triples/sec (pos+neg)", "value": c3["value"], "unit": "triples/s",
                    "n_gpus": ws, "steps": args.steps, "warmup": args.warmup, "ms_per_step": c3["s_per_step"] * 1e3,
@@ -482,6 +605,8 @@ def main():
                    "roofline": c3["roofline"], "universes_per_gpu": c3["universes_per_gpu"]}
             if "link_prediction" in c3:
                 rec["link_prediction"] = c3["link_prediction"]
+            if dropin is not None:
+                rec["dropin"] = dropin
             if "cpu_baseline" in c3:
                 rec["cpu_baseline"] = c3["cpu_baseline"]
             print(json.dumps(rec), flush=True)
@@ -526,19 +651,39 @@ def main():
                                    _native.stream()))
     torch.cuda.synchronize()
 
-    barrier(ws)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    _native.check(L.pt_trainer_run(tr._native, sampler, bs, neg, bern, filt, args.steps, _native.ptr(losses),
-                                   _native.stream()))
-    torch.cuda.synchronize()
-    barrier(ws)
-    el = time.perf_counter() - t0
-    if ws > 1:
-        import torch.distributed as dist
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        all_reduce(tt, dist.ReduceOp.MAX)
-        el = float(tt.item())
+    # the K-step replay timed `repeats` times (each bracketed by barrier + synchronize, max over ranks); value is
+    # the median (box-to-box and run-to-run spread shows in the min / max alongside)
+    runs = []
+    for _ in range(max(args.repeats, 1)):
+        barrier(ws)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _native.check(L.pt_trainer_run(tr._native, sampler, bs, neg, bern, filt, args.steps, _native.ptr(losses),
+                                       _native.stream()))
+        torch.cuda.synchronize()
+        barrier(ws)
+        el = time.perf_counter() - t0
+        if ws > 1:
+            import torch.distributed as dist
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            all_reduce(tt, dist.ReduceOp.MAX)
+            el = float(tt.item())
+        runs.append(el)
+    el = float(np.median(runs))
+    det_ms = None
+    if args.deterministic_timing:
+        # the reference-order mode (Trainer(deterministic=True): bit-identical to the oracle), same K steps
+        _native.check(L.pt_trainer_set_deterministic(tr._native, 1))
+        dl_ = torch.zeros(args.steps, device=dev)
+        _native.check(L.pt_trainer_run(tr._native, sampler, bs, neg, bern, filt, args.steps, _native.ptr(dl_),
+                                       _native.stream()))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _native.check(L.pt_trainer_run(tr._native, sampler, bs, neg, bern, filt, args.steps, _native.ptr(dl_),
+                                       _native.stream()))
+        torch.cuda.synchronize()
+        det_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+        _native.check(L.pt_trainer_set_deterministic(tr._native, 0))
     loss_last = float(losses[-1].item())
     assert np.isfinite(loss_last), "non-finite loss"
 
@@ -584,6 +729,9 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": el * 1e3 / args.steps,
+        "repeats": len(runs),
+        "ms_per_step_runs": [r * 1e3 / args.steps for r in runs],
+        "value_best": args.steps * seq * ws / min(runs),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -615,6 +763,9 @@ def main():
                              (args.workload, 4e-6 * dl.get_ent_tot() * dim)},
         "loss_last_step": loss_last,
     }
+    if det_ms is not None:
+        rec["deterministic_ms_per_step"] = det_ms
+        rec["deterministic_triples_per_s"] = seq * 1e3 / det_ms
     if c3 is not None:
         rec["pu_c3"] = c3
     if c3w is not None:

@@ -214,6 +214,9 @@ int pt_universe_set_profiling(pt_universe_set *s, int32_t on);
 int pt_universe_set_profile(pt_universe_set *s, uint64_t *out);
 /* the current LCG states of job `job` (input order) of a set: `threads` values (host copy; synchronizes) */
 int pt_universe_set_states(pt_universe_set *s, int64_t job, uint64_t *out);
+/* every job's LCG states back to their values at pt_universe_set_create (re-running the same trainings from the
+ * same start, e.g. a benchmark's repeats; the caller restores tables and optimizer state) */
+int pt_universe_set_reset(pt_universe_set *s);
 /* reference-order (deterministic) mode of a set (see pt_trainer_set_deterministic): one workgroup per
  * universe runs its steps with the ordered per-row sums; its workspace is allocated on first use */
 int pt_universe_set_deterministic(pt_universe_set *s, int32_t on);

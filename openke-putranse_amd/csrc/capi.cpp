@@ -984,6 +984,7 @@ struct pt_universe_set {
     std::vector<pt::UniverseDev> host;    // same order; loss pointers patched per train call
     std::vector<int64_t> host_loss_off;
     std::vector<int64_t> host_of_job;     // job index -> index in host / d_us
+    std::vector<uint64_t> seeds0;         // [host][64]: the jobs' LCG states at creation (pt_universe_set_reset)
     uint64_t *prof = nullptr;             // PT_UNI_PROF=1: [n][64] cycle counters + shape (+ stamps) (device)
     // reference-order (deterministic) mode (pt_universe_set_deterministic): ordered.hip's universe kernel
     bool ordered = false;
@@ -1138,6 +1139,8 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         U.g = g.dev;
         U.states = (uint64_t *)(base + slots[i].states);
         PT_HIP(hipMemcpy(U.states, J.seeds, 8 * J.threads, hipMemcpyHostToDevice));
+        set->seeds0.insert(set->seeds0.end(), J.seeds, J.seeds + J.threads);
+        set->seeds0.resize(64 * (set->host.size() + 1), 0);
         U.ent = J.ent; U.rel = J.rel; U.normv = J.normv;
         U.ent_acc = J.ent_acc; U.rel_acc = J.rel_acc; U.norm_acc = J.norm_acc;
         float *gr = (float *)(base + slots[i].grad);
@@ -1211,8 +1214,12 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
 
 extern "C" int pt_universe_set_deterministic(pt_universe_set *set, int32_t on) {
     PT_CHECK(set, PT_EINVAL, "null universe set");
-    set->ordered = on != 0;
-    if (!set->ordered || set->ord_arena || set->host.empty()) return PT_OK;
+    // the set enters reference-order mode only once its workspace exists: a failed call leaves the mode as it
+    // was (a later train call then runs the fast kernel, never the ordered one without its arena)
+    if (!on || set->host.empty() || set->ord_arena) {
+        set->ordered = on != 0;
+        return PT_OK;
+    }
     auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
     int64_t total = 0, max_seq = 0;
     std::vector<int64_t> off(set->host.size());
@@ -1223,13 +1230,19 @@ extern "C" int pt_universe_set_deterministic(pt_universe_set *set, int32_t on) {
         total += al(16 * seq * U.dim);
         max_seq = std::max(max_seq, seq);
     }
-    int dev_lds = 64 << 10;
-    (void)hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, set->device);
-    PT_CHECK(pt::ordered_universe_lds_bytes(max_seq) <= std::min<int64_t>(dev_lds, 160 << 10), PT_ENOTSUP,
+    // the launch's LDS (dynamic plan + the kernel's static variables) against the per-workgroup limit
+    int blk_lds = 64 << 10;
+    (void)hipDeviceGetAttribute(&blk_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, set->device);
+    size_t static_lds = 0;
+    PT_HIP(pt::ordered_universe_static_lds(&static_lds));
+    PT_CHECK(pt::ordered_universe_lds_bytes(max_seq) + (int64_t)static_lds <= (int64_t)blk_lds, PT_ENOTSUP,
              "reference-order mode: universe batch too large for the LDS plan");
-    PT_HIP(hipMalloc(&set->ord_arena, (size_t)std::max<int64_t>(total, 256)));
+    void *arena = nullptr;
+    PT_HIP(hipMalloc(&arena, (size_t)std::max<int64_t>(total, 256)));
+    set->ord_arena = arena;
     for (size_t i = 0; i < set->host.size(); ++i) set->host[i].ord = (float *)((char *)set->ord_arena + off[i]);
     set->ord_max_seq = max_seq;
+    set->ordered = true;
     return PT_OK;
 }
 
@@ -1288,6 +1301,16 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
     }
     // the host array must outlive the async copy: this call returns only after it has been consumed
     PT_HIP(hipStreamSynchronize(st));
+    return PT_OK;
+}
+
+// the sampler streams back to the jobs' creation states (a benchmark re-runs the same training from the same
+// start: the caller restores the tables and optimizer state)
+extern "C" int pt_universe_set_reset(pt_universe_set *set) {
+    PT_CHECK(set, PT_EINVAL, "null universe set");
+    for (size_t i = 0; i < set->host.size(); ++i)
+        PT_HIP(hipMemcpy(set->host[i].states, set->seeds0.data() + 64 * i, 8 * (size_t)set->host[i].threads,
+                         hipMemcpyHostToDevice));
     return PT_OK;
 }
 

@@ -111,6 +111,17 @@ __global__ __launch_bounds__(256) void k_sample_csr(DeviceGraph g, const uint64_
     w.off[o] = atomicAdd(&w.cnt[call * w.cnt_stride + e], 1);
 }
 
+// The split sampler's cross-workgroup exchange (k_sample_part): relaxed read-modify-writes at AGENT scope,
+// spelled out. Agent-scope atomics are performed at the device's coherence point (not in an XCD's L2), so
+// every part's count adds and ticket are seen by the last part whatever XCDs the parts run on; nothing else
+// the parts share inside the launch is read before a kernel boundary.
+__device__ __forceinline__ int32_t agent_add(int32_t *p, int32_t v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t agent_exch(int32_t *p, int32_t v) {
+    return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // One negative slot's draw from its positive's LDS record (k_sample_sort, k_sample_part): the coin and the
 // corruption draw of draw_negative with the same stream offsets and arithmetic; when the drawn index
 // falls inside the known-entity run, the boundary search over it (corrupt_in_run) is left to the caller
@@ -412,7 +423,7 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
             v[u] = i < cwords ? cnt[i] : 0;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) r[u] = v[u] ? atomicAdd(&gcnt[i0 + u * NT], v[u]) : 0;
+        for (int u = 0; u < 8; ++u) r[u] = v[u] ? agent_add(&gcnt[i0 + u * NT], v[u]) : 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u)
             if (v[u]) cnt[i0 + u * NT] = r[u];
@@ -436,18 +447,18 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
     // later launches. (Measured on the driver's 20-step chunk: thread 0 fencing around the tickets 2.7 ->
     // 3.4-4.1 us per step, every thread fencing 9.5-11.4 us: each fence writes back the XCD's L2.)
     __syncthreads();
-    if (tid == 0) is_last = atomicAdd(&w.tick[call], 1) == (int32_t)(parts - 1);
+    if (tid == 0) is_last = agent_add(&w.tick[call], 1) == (int32_t)(parts - 1);
     __syncthreads();
     PT_PHASE(4);
     if (prof && tid == 0) prof[7] = is_last;
     if (!is_last) return;
-    if (tid == 0) w.tick[call] = 0;   // read again only by a later launch
+    if (tid == 0) w.tick[call] = 0;   // plain store: read again only by a later launch (kernel boundary)
     // last part: the call's bucket sizes, exchanged with zeros (atomics on both sides: every part's adds
     // are seen, and the counts are clear for the next chunk) into LDS, 8 exchanges in flight per thread
     for (int64_t i0 = tid; i0 < cwords; i0 += 8 * NT) {
         int32_t r[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) r[u] = i0 + u * NT < cwords ? atomicExch(&gcnt[i0 + u * NT], 0) : 0;
+        for (int u = 0; u < 8; ++u) r[u] = i0 + u * NT < cwords ? agent_exch(&gcnt[i0 + u * NT], 0) : 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u)
             if (i0 + u * NT < cwords) cnt[i0 + u * NT] = r[u];
@@ -492,10 +503,12 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
     // the last call's last part advances the sampler streams past every call's draws: every part of every
     // call read them (positive draws) before its count atomics and tickets
     __syncthreads();
-    if (tid == 0) is_last = atomicAdd(&w.tick[gridDim.x / parts], 1) == (int32_t)(gridDim.x / parts - 1);
+    if (tid == 0) is_last = agent_add(&w.tick[gridDim.x / parts], 1) == (int32_t)(gridDim.x / parts - 1);
     __syncthreads();
     if (!is_last) return;
-    if (tid == 0) w.tick[gridDim.x / parts] = 0;
+    if (tid == 0) w.tick[gridDim.x / parts] = 0;   // plain store: read again only by a later launch
+    // plain stores of the advanced states: read only by later launches (every part of this launch read them
+    // before its ticket add, which returned before this last part's)
     if (tid < 64) advance_states(states, threads, bs, dpp * (int64_t)(gridDim.x / parts), tid);
 }
 

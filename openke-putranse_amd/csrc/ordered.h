@@ -27,6 +27,8 @@ bool ordered_dim_supported(int64_t dim);
 hipError_t launch_ordered_step(const OrderedStep &S, float *loss, int assign, hipStream_t st);
 // dynamic LDS of the ordered universe kernel for universes of at most max_seq slots per step
 int64_t ordered_universe_lds_bytes(int64_t max_seq);
+// static LDS of the reference-order universe kernel (its __shared__ variables, next to the dynamic area)
+hipError_t ordered_universe_static_lds(size_t *bytes);
 // every universe of d_us[0..n) trained in reference order, one 256-thread workgroup per universe taken
 // from *counter; each UniverseDev needs `ord` scratch of 4 * seq * dim floats
 hipError_t launch_universes_ordered(const UniverseDev *d_us, int64_t n, int *counter, int64_t cus, int model,

@@ -531,6 +531,13 @@ bool ordered_dim_supported(int64_t dim) { return dim > 0 && dim <= 256 * 8; }
 
 int64_t ordered_universe_lds_bytes(int64_t max_seq) { return 4 * (11 * max_seq + 12 * max_seq); }
 
+hipError_t ordered_universe_static_lds(size_t *bytes) {
+    hipFuncAttributes a{};
+    const hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(dev::k_universes_ordered<256>));
+    if (e == hipSuccess) *bytes = a.sharedSizeBytes;
+    return e;
+}
+
 hipError_t launch_universes_ordered(const UniverseDev *d_us, int64_t n, int *counter, int64_t cus, int model,
                                     int p_norm, int norm_flag, int opt, int64_t neg, int bern, int filter,
                                     int64_t max_seq, hipStream_t st) {

@@ -26,6 +26,12 @@ struct UniverseDev {
     int32_t shape;                                  // universe_shape_id(dim)
 };
 
+// workgroup size of each shape class's kernel (the 16-float class keeps 512 threads at 256 VGPRs)
+#ifndef PT_UNI_NT
+#define PT_UNI_NT 512
+#endif
+constexpr int kUniverseClassThreads[3] = {PT_UNI_NT, PT_UNI_NT, 512};
+
 // launch configuration of one group of universes (host-chosen for the largest universe of the group)
 struct UniverseLaunch {
     int threads = 512;          // workgroup size

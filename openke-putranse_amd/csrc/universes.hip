@@ -46,7 +46,7 @@ int universe_shape_class(int shape) {
 // lane groups of a universe workgroup for a shape (positives of a step processed concurrently)
 int universe_shape_groups(int shape) {
 #define PT_UGPB(ID_, G_, V_, K_) \
-    if (shape == ID_) return 512 / G_;
+    if (shape == ID_) return kUniverseClassThreads[PT_UCLASS(V_, K_)] / G_;
     PT_USHAPES(PT_UGPB)
 #undef PT_UGPB
     return 1;

@@ -606,7 +606,8 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // loads in flight together: the pass is a chain of dependent memory round trips otherwise)
             const int n = s_count;
             // (TransH: 2 rows of 8 floats per lane in flight spill its step's registers; TransE keeps 2)
-            constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? (MODEL == 1 ? 1 : 2) : 4);
+            // (1024-thread workgroups: half the rows per lane group, twice the lane groups; 128 VGPRs per lane)
+            constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? (MODEL == 1 || NT > 512 ? 1 : 2) : (NT > 512 ? 2 : 4));
             constexpr bool kFastUpd = kUF && VEC * KCH <= 8;
             // (guards, not breaks, inside the unrolled loops: the row arrays must stay in registers)
             PT_USTAMP(tr, 47);
@@ -802,8 +803,8 @@ namespace detail {
 template <int MODEL, int WPE, int CLS, int PLAN>
 hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int64_t cus, int p_norm, int norm_flag, int opt,
                     int64_t neg, int bern, int filter, const UniverseLaunch &cfg, hipStream_t st) {
-    constexpr int NT = 512;
-    auto kern = dev::k_universes<MODEL, NT, WPE, CLS, PLAN>;
+    constexpr int NT = kUniverseClassThreads[CLS];
+    auto kern = dev::k_universes<MODEL, NT, WPE * NT / 512, CLS, PLAN>;
     if (cfg.lds_bytes > (64 << 10)) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)cfg.lds_bytes);

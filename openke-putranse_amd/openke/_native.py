@@ -6,9 +6,11 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# PT_LIB_PATH: an alternative build of the same library (A/B measurements of two builds on one box)
-LIB_PATH = os.environ.get("PT_LIB_PATH") or os.path.join(_HERE, "release", "libputranse_hip.so")
+# The product library, in-tree. No environment variable selects another build: A/B measurements of two
+# builds go through tools_gpu/ablib.py, which calls use_alternative_library() before anything loads it.
+LIB_PATH = os.path.join(_HERE, "release", "libputranse_hip.so")
 _LIB = None
+_ALTERNATIVE = False
 
 c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32
@@ -104,6 +106,7 @@ SIGNATURES = {
     "pt_universe_set_deterministic": (ctypes.c_int, [c_vp, c_i32]),
     "pt_universe_set_profiling": (ctypes.c_int, [c_vp, c_i32]),
     "pt_universe_set_states": (ctypes.c_int, [c_vp, c_i64, c_vp]),
+    "pt_universe_set_reset": (ctypes.c_int, [c_vp]),
     "pt_universes_train": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
                                           c_i64, c_vp, c_vp]),
     "pt_universes_train_ex": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
@@ -188,13 +191,23 @@ def lib():
                               "make -C openke-putranse_amd" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            if os.environ.get("PT_LIB_PATH") and not hasattr(L, name):
+            if _ALTERNATIVE and not hasattr(L, name):
                 continue   # an older build under A/B: entry points added since are absent
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
         _LIB = L
     return _LIB
+
+
+def use_alternative_library(path):
+    """Measurement tooling only (tools_gpu/ablib.py): load another build of the library instead of the
+    product one. Must run before the first lib() call of the process."""
+    global LIB_PATH, _ALTERNATIVE
+    if _LIB is not None:
+        raise NativeError("use_alternative_library: the library is already loaded (%s)" % LIB_PATH)
+    LIB_PATH = os.path.abspath(path)
+    _ALTERNATIVE = True
 
 
 def check(rc):

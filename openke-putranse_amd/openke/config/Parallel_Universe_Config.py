@@ -81,12 +81,18 @@ def universe_cost(epochs, triples, dim):
     return float(max(epochs, 0)) * float(max(triples, 0)) * (float(dim) + 32.0)
 
 
-def place_universes(costs, world_size):
+def place_universes(costs, world_size, loads=None):
     """LPT placement (longest processing time first) of independent universes over ranks: universes in
     decreasing cost (ties by id) each go to the rank with the least cost so far (ties to the lowest
-    rank). `costs` maps universe id -> cost; returns {universe id: rank}. A pure function of its
-    arguments, so every rank computes the same map from the same draws with no communication."""
-    loads = [0.0] * max(int(world_size), 1)
+    rank). `costs` maps universe id -> cost; returns {universe id: rank}. `loads` (optional, one float per
+    rank) is the cost each rank already carries - earlier training waves - and is updated in place, so
+    consecutive waves balance the whole run instead of each wave starting from zero (which would give
+    rank 0 the heaviest universe of every wave, and every universe of one-universe waves). A pure function
+    of its arguments, so every rank computes the same map from the same draws with no communication."""
+    if loads is None:
+        loads = [0.0] * max(int(world_size), 1)
+    if len(loads) != max(int(world_size), 1):
+        raise ValueError("place_universes: %d loads for %d ranks" % (len(loads), world_size))
     owners = {}
     for uid, c in sorted(costs.items(), key=lambda kv: (-kv[1], kv[0])):
         r = min(range(len(loads)), key=lambda i: (loads[i], i))
@@ -223,7 +229,37 @@ class _KeyStore(object):
         return None if idx is None else idx
 
 
+def universe_dim(dim_param, uid):
+    """Embedding dim of universe `uid`: `dim_param` as given (the reference's fixed dim), or - a build
+    extension for BASELINE config C3 (dim ~ U{lo..hi} per universe) - a (lo, hi) pair, drawn from numpy's
+    default_rng(1000 + uid) (a stream of its own: the reference's Python / torch / glibc draws are untouched)."""
+    if isinstance(dim_param, (tuple, list)):
+        lo, hi = int(dim_param[0]), int(dim_param[1])
+        return int(np.random.default_rng(1000 + int(uid)).integers(lo, hi + 1))
+    return int(dim_param)
+
+
+def _id_map_property(name):
+    """A reference attribute holding per-universe id maps (entity_id_mappings, ...): universes committed since
+    the last read are registered first (_materialize_maps), in one batch."""
+    def get(self):
+        self._materialize_maps()
+        return self.__dict__[name]
+
+    def put(self, value):
+        if name == "_entity_id_mappings":
+            self.__dict__["_pending_maps"] = []   # a replaced state (load / best state) drops pending ones
+        self.__dict__[name] = value
+    return property(get, put)
+
+
 class Parallel_Universe_Config(Tester):
+    # the reference's dictionaries (universe -> global id -> local id, global id -> universes); filled lazily
+    entity_id_mappings = _id_map_property("_entity_id_mappings")
+    relation_id_mappings = _id_map_property("_relation_id_mappings")
+    entity_universes = _id_map_property("_entity_universes")
+    relation_universes = _id_map_property("_relation_universes")
+
     def __init__(self,
                  train_dataloader=None, training_identifier='', valid_dataloader=None, test_dataloader=None,
                  initial_num_universes=5000,
@@ -236,6 +272,7 @@ class Parallel_Universe_Config(Tester):
                  incremental_strategy="normal",
                  universe_wave_size=None, deterministic=False):
         super(Parallel_Universe_Config, self).__init__(data_loader=test_dataloader, use_gpu=torch.cuda.is_available())
+        self._pending_maps = []           # (uid, ent_remap, rel_remap) committed, not yet in the dictionaries
         if training_setting != "static":
             raise NotImplementedError("the incremental setting is outside the accelerated path")
 
@@ -321,6 +358,7 @@ class Parallel_Universe_Config(Tester):
         # multi-GPU: universe_id -> rank that trains / holds it (place_universes per training wave, re-made
         # by load_parameters for the loading job's world size); ids absent here are round-robin
         self.universe_owners = {}
+        self._rank_loads = []             # per rank: cost of the universes placed on it so far (all waves)
 
     # ------------------------------------------------------------------ reference API -----------
     def get_default_value_list(self):
@@ -345,7 +383,7 @@ class Parallel_Universe_Config(Tester):
         self._stores.pop('test', None)
 
     def embedding_model_factory(self, ent_tot, rel_tot, margin):
-        embedding_method = self.embedding_model(ent_tot, rel_tot, **self.embedding_model_param)
+        embedding_method = self.embedding_model(ent_tot, rel_tot, **self._model_param(self.next_universe_id))
         return NegativeSampling(
             model=embedding_method,
             loss=MarginLoss(margin=margin),
@@ -381,22 +419,37 @@ class Parallel_Universe_Config(Tester):
         _native.require_gpu()
 
     def _universe_draws(self, uid):
-        """Python-RNG draws of universe uid in the reference's order (:210-236), after set_random_seed."""
-        self.set_random_seed(self.initial_random_seed + uid)
-        tc = randrange(self.min_triple_constraint, self.max_triple_constraint)
-        balance = round(uniform(self.min_balance, self.max_balance), 2)
-        margin = randrange(self.min_margin, self.max_margin)
+        """Python-RNG draws of universe uid in the reference's order (:210-236): set_random_seed(seed0 + uid)
+        seeds Python's generator, then randrange(tc), uniform(balance), randrange(margin), randrange(epochs),
+        uniform(lr). Drawn from a private random.Random(seed0 + uid) - the same numbers - so a wave's draws need
+        no global reseeding per universe (_train_wave reseeds the globals once, after the wave)."""
+        rs = random.Random(self.initial_random_seed + uid)
+        tc = rs.randrange(self.min_triple_constraint, self.max_triple_constraint)
+        balance = round(rs.uniform(self.min_balance, self.max_balance), 2)
+        margin = rs.randrange(self.min_margin, self.max_margin)
         epochs = self.const_num_epochs if self.const_num_epochs is not None \
-            else randrange(self.min_num_epochs, self.max_num_epochs)
-        lr = round(uniform(self.min_lr, self.max_lr), len(str(self.min_lr).split('.')[1]))
+            else rs.randrange(self.min_num_epochs, self.max_num_epochs)
+        lr = round(rs.uniform(self.min_lr, self.max_lr), len(str(self.min_lr).split('.')[1]))
         return tc, balance, margin, epochs, lr
 
+    def _model_param(self, uid):
+        """embedding_model_param of universe uid (a (lo, hi) dim resolved per universe: universe_dim)."""
+        param = dict(self.embedding_model_param)
+        if "dim" in param:
+            param["dim"] = universe_dim(param["dim"], uid)
+        return param
+
     def _train_wave(self, ids):
-        """Build and train universes `ids` (this rank's share on the GPU); returns records in id order."""
+        """Build and train universes `ids` (this rank's share on the GPU); returns records in id order.
+        self.last_wave_timing: seconds spent in the Python draws, the native universe construction, the torch
+        modules (factory init, owned universes only), their H2D copy, the GPU training launch (job setup,
+        kernel, loss readback), per wave."""
         L = _native.lib()
         dl = self.train_dataloader
         world, rank = _dist()
         n = len(ids)
+        tm = {"wave_universes": n}
+        t0 = time.perf_counter()
         draws = [self._universe_draws(uid) for uid in ids]
         seeds = np.array([self.initial_random_seed + uid for uid in ids], dtype=np.int64)
         tcs = np.array([d[0] for d in draws], dtype=np.int64)
@@ -405,16 +458,24 @@ class Parallel_Universe_Config(Tester):
         graph = L.pt_legacy_graph()
         if not graph:
             raise RuntimeError("no training graph imported (TrainDataLoader.read() imports it)")
+        t1 = time.perf_counter()
+        tm["draws_s"] = t1 - t0
         _native.check(L.pt_universe_build_many(graph, n, seeds.ctypes.data, dl.work_threads, tcs.ctypes.data,
                                                bals.ctypes.data, 0, handles))
+        t0 = time.perf_counter()
+        tm["native_build_s"] = t0 - t1
         recs, jobs, keep = [], [], []
         dev = torch.device("cuda", torch.cuda.current_device())
+        tm["modules_s"] = tm["h2d_s"] = 0.0
         try:
+            dims = [universe_dim(self.embedding_model_param.get("dim", 100), uid) for uid in ids]
             if world > 1:   # LPT over the wave from the draws and the built universes' sizes (same on every rank)
-                dim = int(self.embedding_model_param.get("dim", 100))
+                if len(self._rank_loads) != world:
+                    self._rank_loads = [0.0] * world
                 self.universe_owners.update(place_universes(
-                    {uid: universe_cost(draws[i][3], L.pt_universe_train_total(handles[i]), dim)
-                     for i, uid in enumerate(ids)}, world))
+                    {uid: universe_cost(draws[i][3], L.pt_universe_train_total(handles[i]), dims[i])
+                     for i, uid in enumerate(ids)}, world, self._rank_loads))
+            sizes = []
             for i, uid in enumerate(ids):
                 tc, balance, margin, epochs, lr = draws[i]
                 h = handles[i]
@@ -424,16 +485,35 @@ class Parallel_Universe_Config(Tester):
                 rm = np.zeros(max(R_u, 1), dtype=np.int64)
                 _native.check(L.pt_universe_remaps(h, em.ctypes.data, rm.ctypes.data))
                 bs = N_u // dl.nbatches
-                # the model factory after torch.manual_seed(seed0 + uid) (set_random_seed, :157-161)
-                torch.manual_seed(self.initial_random_seed + uid)
-                kge = self.embedding_model(E_u, R_u, **self.embedding_model_param)
-                rec = {"id": uid, "kge": kge, "ent_remap": em[:E_u], "rel_remap": rm[:R_u], "tc": tc,
-                       "balance": balance, "margin": margin, "epochs": epochs, "lr": lr, "batch_size": bs,
-                       "train_total": N_u, "losses": None}
-                recs.append(rec)
-                if self.owner(uid) != rank:
-                    continue   # trained on another rank
-                kge.to(dev)
+                recs.append({"id": uid, "kge": None, "ent_remap": em[:E_u], "rel_remap": rm[:R_u], "tc": tc,
+                             "balance": balance, "margin": margin, "epochs": epochs, "lr": lr, "batch_size": bs,
+                             "train_total": N_u, "losses": None})
+                sizes.append((E_u, R_u))
+            # the model factory after torch.manual_seed(seed0 + uid) (set_random_seed, :157-161) for the universes
+            # this rank trains (placement never changes a universe's init): Model.seeded draws the same tables from
+            # a private generator, so the wave's modules are built on a thread pool
+            mine = [i for i, uid in enumerate(ids) if self.owner(uid) == rank]
+            ta = time.perf_counter()
+
+            def build(i):
+                return self.embedding_model.seeded(self.initial_random_seed + ids[i], sizes[i][0], sizes[i][1],
+                                                   **self._model_param(ids[i]))
+            if len(mine) > 1:
+                from concurrent.futures import ThreadPoolExecutor
+                with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1, len(mine))) as ex:
+                    built = list(ex.map(build, mine))
+            else:
+                built = [build(i) for i in mine]
+            tb = time.perf_counter()
+            tm["modules_s"] = tb - ta
+            for i, kge in zip(mine, built):
+                recs[i]["kge"] = kge.to(dev)
+            tm["h2d_s"] = time.perf_counter() - tb
+            for i in mine:
+                uid, rec, h = ids[i], recs[i], handles[i]
+                tc, balance, margin, epochs, lr = draws[i]
+                bs = rec["batch_size"]
+                kge = rec["kge"]
                 ent, rel, nv = kge.tables()
                 accs = tuple(torch.zeros_like(x) if x is not None else None for x in (ent, rel, nv))
                 st = np.zeros(dl.work_threads, dtype=np.uint64)
@@ -453,6 +533,11 @@ class Parallel_Universe_Config(Tester):
                 j.dim = ent.shape[1]
                 jobs.append(j)
                 keep.append((st, accs, rec))
+            # the process-global generators as the last set_random_seed of the wave leaves them (:157-161)
+            self.set_random_seed(self.initial_random_seed + ids[-1])
+            t1 = time.perf_counter()
+            tm["jobs_s"] = t1 - t0 - tm["modules_s"] - tm["h2d_s"]
+            tm["trained_here"] = len(jobs)
             if jobs:
                 kge0 = keep[0][2]["kge"]
                 total_epochs = sum(int(j.epochs) for j in jobs)
@@ -468,24 +553,47 @@ class Parallel_Universe_Config(Tester):
                 for j, (_, _, rec) in zip(jobs, keep):
                     rec["losses"] = lh[off:off + int(j.epochs)].copy()
                     off += int(j.epochs)
+            tm["train_launch_s"] = time.perf_counter() - t1
         finally:
             for i in range(n):
                 if handles[i]:
                     L.pt_universe_free(handles[i])
+        self.last_wave_timing = tm
         return recs
 
     def _register_maps(self, uid, ent_remap, rel_remap):
+        """process_universe_mappings (:179-207) for universe uid: the GPU paths read the arrays (_remap_cache)
+        at once; the reference's dictionaries get the universe at their next read (_materialize_maps)."""
         em = np.ascontiguousarray(ent_remap, dtype=np.int64)
         rm = np.ascontiguousarray(rel_remap, dtype=np.int64)
-        emap = self.entity_id_mappings[uid]
-        for local, g in enumerate(em.tolist()):
-            self.entity_universes[g].add(uid)
-            emap[g] = local
-        rmap = self.relation_id_mappings[uid]
-        for local, g in enumerate(rm.tolist()):
-            self.relation_universes[g].add(uid)
-            rmap[g] = local
+        self._pending_maps.append((uid, em, rm))
         self._remap_cache[uid] = self._remaps_from_arrays(em, rm)
+
+    def _materialize_maps(self):
+        """Register the pending universes' maps in the reference's dictionaries, all at once: the per-universe
+        maps built by dict.update (C loops), the id -> universes sets grouped by id over every pending universe
+        (one set update per id instead of one add per (id, universe))."""
+        pend = self.__dict__.get("_pending_maps")
+        if not pend:
+            return
+        self.__dict__["_pending_maps"] = []
+        d = self.__dict__
+        emaps, rmaps = d["_entity_id_mappings"], d["_relation_id_mappings"]
+        for uid, em, rm in pend:
+            el, rl = em.tolist(), rm.tolist()
+            emaps[uid].update(zip(el, range(len(el))))
+            rmaps[uid].update(zip(rl, range(len(rl))))
+        for key, col in (("_entity_universes", 1), ("_relation_universes", 2)):
+            target = d[key]
+            ids = np.concatenate([p[col] for p in pend])
+            us = np.repeat(np.array([p[0] for p in pend], dtype=np.int64), [len(p[col]) for p in pend])
+            o = np.argsort(ids, kind="stable")
+            ids, us = ids[o], us[o]
+            keys, starts = np.unique(ids, return_index=True)
+            ends = np.append(starts[1:], len(ids)).tolist()
+            ul = us.tolist()
+            for k, lo, hi in zip(keys.tolist(), starts.tolist(), ends):
+                target[k].update(ul[lo:hi])
 
     def add_universe(self, embedding_space, ent_remap, rel_remap):
         """Register a trained universe as id next_universe_id: add_embedding_space +
@@ -569,17 +677,26 @@ class Parallel_Universe_Config(Tester):
     def _after_universe(self, universe_id):
         """Validation / early stopping / checkpoint schedule after universe `universe_id` of this call
         (Parallel_Universe_Config.py:329-365); True when training stops early."""
+        tm = getattr(self, "last_train_timing", None)
         if (universe_id + 1) % self.valid_steps == 0:
             print("Universe %d has finished, validating..." % (self.next_universe_id - 1))
+            t0 = time.perf_counter()
             self.eval_universes(eval_mode='valid')
             hit10 = self.valid()
+            if tm is not None:
+                tm["validations"] = tm.get("validations", 0) + 1
+                tm["validate_s"] = tm.get("validate_s", 0.0) + time.perf_counter() - t0
             print("Current hit@10: {}".format(hit10))
             if hit10 > self.best_hit10:
                 self.best_hit10 = hit10
                 print("Best model | hit@10 of valid set is %f" % self.best_hit10)
                 print('Save model at universe %d.' % self.next_universe_id)
+                t0 = time.perf_counter()
                 self.save_model("Best_model_Pu{}_{}.ckpt".format(self.embedding_model.__name__,
                                                                  self.training_identifier))
+                if tm is not None:
+                    tm["checkpoints"] = tm.get("checkpoints", 0) + 1
+                    tm["checkpoint_s"] = tm.get("checkpoint_s", 0.0) + time.perf_counter() - t0
                 self.bad_counts = 0
             else:
                 print("Hit@10 of valid set is %f | bad count is %d" % (hit10, self.bad_counts))
@@ -612,24 +729,46 @@ class Parallel_Universe_Config(Tester):
             return
         done = 0
         stop = False
+        wave_size = self.wave_size()
+        self.last_train_timing = timing = {"waves": 0, "universes": 0, "wave_s": 0.0, "commit_s": 0.0,
+                                           "validate_save_s": 0.0}
         while done < num_of_embedding_spaces and not stop:
-            wave = num_of_embedding_spaces - done
-            if self.universe_wave_size:
-                wave = min(wave, int(self.universe_wave_size))
+            wave = min(num_of_embedding_spaces - done, wave_size)
             ids = list(range(self.next_universe_id, self.next_universe_id + wave))
             t0 = time.time()
             recs = self._train_wave(ids)
-            per_universe = (time.time() - t0) / max(len(recs), 1)
-            print("trained universes %d..%d on the GPU (%.3f s)" % (ids[0], ids[-1], per_universe * len(recs)))
+            wave_s = time.time() - t0
+            per_universe = wave_s / max(len(recs), 1)
+            timing["waves"] += 1
+            timing["wave_s"] += wave_s
+            for k, v in self.last_wave_timing.items():
+                timing[k] = timing.get(k, 0) + v
+            print("trained universes %d..%d on the GPU (%.3f s)" % (ids[0], ids[-1], wave_s))
             for rec in recs:
                 universe_id = done
+                ta = time.time()
                 self._commit(rec)
+                tb = time.time()
+                timing["commit_s"] += tb - ta
                 training_duration += per_universe
-                if self._after_universe(universe_id):
-                    stop = True
+                stop = self._after_universe(universe_id)
+                timing["validate_save_s"] += time.time() - tb
+                if stop:
                     break
                 done += 1
+                timing["universes"] += 1
         print('Time took for creation of embedding spaces: {:5.3f}s'.format(training_duration), end='\n')
+
+    def wave_size(self):
+        """Universes per training launch: universe_wave_size if set, else a multiple of valid_steps of about
+        512 per rank (two per CU of an MI355X: enough to fill the GPU), so an early stop - decided at a
+        validation point - discards at most the rest of one wave."""
+        if self.universe_wave_size:
+            return max(int(self.universe_wave_size), 1)
+        world, _ = _dist()
+        vs = max(int(self.valid_steps or 1), 1)
+        target = 512 * world
+        return vs * max(1, int(round(target / float(vs))))
 
     # ------------------------------------------------------------------ global energy estimation -
     @staticmethod
@@ -1161,12 +1300,22 @@ class Parallel_Universe_Config(Tester):
         dist.gather_object(mine, got, dst=0)
         if rank != 0:
             return None
+        # a universe held by several ranks (the one-universe protocol, add_embedding_space, registers every
+        # universe on every rank): the owner's copy, else the lowest rank's
+        chosen = {}
+        for r, part in enumerate(got):
+            for x in part:
+                uid = x[0]
+                if uid not in chosen or (chosen[uid][0] != self.owner(uid) and r == self.owner(uid)):
+                    chosen[uid] = (r, x)
         spaces = defaultdict(Model)
         with torch.random.fork_rng(devices=[]):
-            for uid, E_u, R_u, sd in sorted((x for part in got for x in part), key=lambda x: x[0]):
-                if uid in spaces:
-                    raise RuntimeError("universe %d is held by more than one rank" % uid)
-                m = self.embedding_model(E_u, R_u, **self.embedding_model_param)
+            for uid in sorted(chosen):
+                _, E_u, R_u, sd = chosen[uid][1]
+                param = dict(self.embedding_model_param)
+                if "dim" in param:   # the universe's own dim (a (lo, hi) dim range draws one per universe)
+                    param["dim"] = int(sd["ent_embeddings.weight"].shape[1])
+                m = self.embedding_model(E_u, R_u, **param)
                 m.load_state_dict(sd)
                 for p in m.parameters():
                     p.requires_grad = False

@@ -35,7 +35,7 @@ class TestDataSampler(object):
 class TestDataLoader(object):
 
     def __init__(self, in_path="./", sampling_mode='link', random_seed=4, mode='test', setting="static",
-                 load_all_triples=False, count_header=False):
+                 load_all_triples=False, count_header=None):
         self.lib = _native.lib()
         if setting != "static":
             raise NotImplementedError("only the static setting is part of the accelerated path")
@@ -45,7 +45,10 @@ class TestDataLoader(object):
         self.in_path = in_path
         self.sampling_mode = sampling_mode
         self.random_seed = random_seed
-        self.count_header = bool(count_header)   # see TrainDataLoader
+        # see TrainDataLoader. None (default): the file format the process already reads with - the train
+        # loader's choice - so a TrainDataLoader(count_header=True) followed by a default TestDataLoader does
+        # not make importTrainFiles see a format change and re-read train2id.txt under the other format
+        self.count_header = None if count_header is None else bool(count_header)
         self.read()
 
     def set_path(self, in_path):
@@ -53,6 +56,8 @@ class TestDataLoader(object):
 
     def read(self):
         self.set_path(self.in_path)
+        if self.count_header is None:
+            self.count_header = bool(self.lib.pt_get_count_header())
         _native.check(self.lib.pt_set_count_header(1 if self.count_header else 0))
         self.lib.setRandomSeed(self.random_seed)
         self.lib.randReset()

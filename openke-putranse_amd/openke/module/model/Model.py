@@ -1,12 +1,16 @@
 import ctypes
+import threading
 
 import numpy as np
 import torch
+import torch.nn as nn
 
 from ... import _native
 from ..BaseModule import BaseModule
 
 _MODES = {"normal": 0, "head_batch": 1, "tail_batch": 2}
+# per-thread torch.Generator of Model.seeded (None: the default generator, as the reference's constructors use)
+_INIT = threading.local()
 
 
 class Model(BaseModule):
@@ -19,6 +23,34 @@ class Model(BaseModule):
         super(Model, self).__init__()
         self.ent_tot = ent_tot
         self.rel_tot = rel_tot
+
+    # -- initialisation from a private generator ---------------------------------------------------
+    @classmethod
+    def seeded(cls, seed, ent_tot, rel_tot, **param):
+        """The module `torch.manual_seed(seed); cls(ent_tot, rel_tot, **param)` builds - bit for bit the same
+        tables (nn.Embedding's normal_ draws, then the xavier / uniform init, in the constructor's order) -
+        drawn from a private torch.Generator seeded with `seed` instead of the process-global one. Thread-safe:
+        Parallel_Universe_Config builds a wave's universes on a thread pool with it (torch releases the GIL
+        inside the draws)."""
+        _INIT.gen = torch.Generator().manual_seed(int(seed))
+        try:
+            return cls(ent_tot, rel_tot, **param)
+        finally:
+            _INIT.gen = None
+
+    @staticmethod
+    def _generator():
+        return getattr(_INIT, "gen", None)
+
+    @staticmethod
+    def _embedding(rows, dim):
+        """nn.Embedding(rows, dim) with its default N(0, 1) init drawn from the active generator."""
+        gen = getattr(_INIT, "gen", None)
+        if gen is None:
+            return nn.Embedding(rows, dim)
+        w = torch.empty(rows, dim)
+        w.normal_(generator=gen)
+        return nn.Embedding(rows, dim, _weight=w)
 
     # -- native plumbing --------------------------------------------------------------------------
     def tables(self):

@@ -618,6 +618,9 @@ typedef struct {
     float *gh, *gt, *gr, *gw;                     /* [seq][d] */
     int64_t *hoff, *hlist, *toff, *tlist, *roff, *rlist;
     int64_t cap_seq, cap_e, cap_r, cap_d;
+    /* oracle_grad_mass: per row element the summed gradient and the sum of its contributions' magnitudes
+     * ([E + R (+ R)][d], entity rows then relation then norm_vector rows); the tables are not updated */
+    float *gsum, *gmass;
 } ostep;
 
 static void slot_ws_bind(slot_ws *ws, float *buf, int64_t d) {
@@ -692,6 +695,27 @@ static void row_update(const ostep *S, float *w, float *acc, const float *ga, co
     apply_update(S->opt, S->lr, w, acc, g, d);
 }
 
+/* oracle_grad_mass's phase 2 for one row: the row gradient as row_update sums it, and sum |contribution| */
+static void row_mass(const ostep *S, float *gs, float *gm, const float *ga, const int64_t *la, int64_t na,
+                     const float *gb, const int64_t *lb, int64_t nb) {
+    const int64_t d = S->d;
+    for (int64_t i = 0; i < d; ++i) {
+        float a = 0, b = 0, m = 0;
+        for (int64_t k = 0; k < na; ++k) {
+            const float x = ga[la[k] * d + i];
+            a += x;
+            m += fabsf(x);
+        }
+        for (int64_t k = 0; k < nb; ++k) {
+            const float x = gb[lb[k] * d + i];
+            b += x;
+            m += fabsf(x);
+        }
+        gs[i] = nb ? a + b : a;
+        gm[i] = m;
+    }
+}
+
 /* counting sort of the slots with ds != 0 by key (stable: slots ascending inside a key) */
 static void slot_csr(const ostep *S, const int64_t *key, int64_t nkeys, int64_t *off, int64_t *list) {
     memset(off, 0, sizeof(int64_t) * (size_t)(nkeys + 1));
@@ -728,6 +752,18 @@ static void run_range(const ostep *S, int phase, int64_t lo, int64_t hi) {
     } else {
         /* rows: entities [0, E), relations [E, E + R), norm_vector rows [E + R, E + 2R) */
         for (int64_t q = lo; q < hi; ++q) {
+            if (S->gsum) {   /* oracle_grad_mass: sums only */
+                float *gs = S->gsum + q * d, *gm = S->gmass + q * d;
+                if (q < S->E)
+                    row_mass(S, gs, gm, S->gh, S->hlist + S->hoff[q], S->hoff[q + 1] - S->hoff[q], S->gt,
+                             S->tlist + S->toff[q], S->toff[q + 1] - S->toff[q]);
+                else {
+                    const int64_t k = (q - S->E) % S->R;
+                    row_mass(S, gs, gm, q < S->E + S->R ? S->gr : S->gw, S->rlist + S->roff[k],
+                             S->roff[k + 1] - S->roff[k], NULL, NULL, 0);
+                }
+                continue;
+            }
             if (q < S->E) {
                 const int64_t na = S->hoff[q + 1] - S->hoff[q], nb = S->toff[q + 1] - S->toff[q];
                 if (na + nb == 0) continue;
@@ -858,6 +894,28 @@ float oracle_train_step_mt(int model, int p, int norm_flag, int opt, float lr, f
     S.ent = ent; S.rel = rel; S.normv = normv; S.ent_acc = ent_acc; S.rel_acc = rel_acc; S.norm_acc = norm_acc;
     S.h = h; S.t = t; S.r = r;
     const float loss = ostep_run(&S, workers);
+    ostep_release(&S);
+    return loss;
+}
+
+/* Test infrastructure for the fast kernels' step tolerance (tests/helpers.py assert_step_close): the step's
+ * gradient of every table element - summed in the reference's order (row_update) - and the sum of the
+ * magnitudes of its per-slot contributions, without updating anything. kappa = gmass / |gsum| is the element's
+ * condition number for the sum: an implementation summing the same contributions in another order may differ
+ * from gsum by about n * eps * gmass. Outputs [E + R (+ R for TransH)][d]: entity rows, relation rows,
+ * norm_vector rows. Returns the loss. */
+float oracle_grad_mass(int model, int p, int norm_flag, float margin, int64_t E, int64_t R, int64_t d, float *ent,
+                       float *rel, float *normv, const int64_t *h, const int64_t *t, const int64_t *r, int64_t bs,
+                       int64_t neg, float *gsum, float *gmass) {
+    ostep S;
+    memset(&S, 0, sizeof(S));
+    S.model = model; S.p = p; S.norm_flag = norm_flag; S.opt = 0; S.lr = 0.f; S.margin = margin;
+    S.E = E; S.R = R; S.d = d; S.bs = bs; S.neg = neg; S.seq = bs * (1 + neg);
+    S.ent = ent; S.rel = rel; S.normv = normv;
+    S.h = h; S.t = t; S.r = r;
+    S.gsum = gsum;
+    S.gmass = gmass;
+    const float loss = ostep_run(&S, 1);
     ostep_release(&S);
     return loss;
 }

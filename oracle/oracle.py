@@ -60,6 +60,9 @@ def lib():
         L.oracle_rank_constrained.argtypes = ([ctypes.c_int64] + [i64p] * 3 + [ctypes.c_int64] + [i64p] * 3 +
                                               [ctypes.c_int64] + [f32p] * 2 + [i64p] * 6 + [i64p] * 4 + [f32p])
         L.oracle_metrics_from_ranks.argtypes = [ctypes.c_int64, i64p, i64p, f32p]
+        L.oracle_grad_mass.restype = ctypes.c_float
+        L.oracle_grad_mass.argtypes = ([ctypes.c_int] * 3 + [ctypes.c_float] + [ctypes.c_int64] * 3 + [f32p] * 3 +
+                                       [i64p] * 3 + [ctypes.c_int64] * 2 + [f32p] * 2)
         L.oracle_train_step_mt.restype = ctypes.c_float
         L.oracle_train_step_mt.argtypes = ([ctypes.c_int] * 4 + [ctypes.c_float] * 2 + [ctypes.c_int64] * 3 +
                                            [f32p] * 6 + [i64p] * 3 + [ctypes.c_int64] * 3)
@@ -185,6 +188,27 @@ def train_step(model, p, norm_flag, opt, lr, margin, ent, rel, normv, accs, h, t
     return lib().oracle_train_step(MODELS[model], p, int(norm_flag), OPTS[opt], lr, margin, E, R, D,
                                    _p(ent, f32p), _p(rel, f32p), _p(nv, f32p), _p(ea, f32p), _p(ra, f32p),
                                    _p(na, f32p), _p(h, i64p), _p(t, i64p), _p(r, i64p), bs, neg)
+
+
+def grad_mass(model, p, norm_flag, margin, ent, rel, normv, h, t, r, bs, neg):
+    """Test infrastructure (helpers.assert_step_close): the step's gradient of every element of the tables
+    (summed in the reference's order) and the sum of its per-slot contributions' magnitudes, at the given
+    tables, without updating them. Returns ({"ent", "rel", "norm"} -> (gsum, gmass)) arrays of the tables'
+    shapes (the norm entry only for TransH)."""
+    E, D = ent.shape
+    R = rel.shape[0]
+    rows = E + R * (2 if model == "TransH" else 1)
+    gs = np.zeros((rows, D), dtype=np.float32)
+    gm = np.zeros((rows, D), dtype=np.float32)
+    nv = normv if normv is not None else np.zeros(1, dtype=np.float32)
+    h, t, r = (np.ascontiguousarray(x, dtype=np.int64) for x in (h, t, r))
+    lib().oracle_grad_mass(MODELS[model], p, int(norm_flag), margin, E, R, D, _p(np.ascontiguousarray(ent), f32p),
+                           _p(np.ascontiguousarray(rel), f32p), _p(np.ascontiguousarray(nv), f32p), _p(h, i64p),
+                           _p(t, i64p), _p(r, i64p), bs, neg, _p(gs, f32p), _p(gm, f32p))
+    out = {"ent": (gs[:E], gm[:E]), "rel": (gs[E:E + R], gm[E:E + R])}
+    if model == "TransH":
+        out["norm"] = (gs[E + R:], gm[E + R:])
+    return out
 
 
 def score(model, p, norm_flag, mode, ent, rel, normv, h, t, r):

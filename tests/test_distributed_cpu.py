@@ -244,3 +244,64 @@ def test_multi_rank_checkpoint_matches_single_process(tmp_path):
             assert p[4] == {u: dict(m) for u, m in single.entity_id_mappings.items()}   # maps stay complete
             got.update(p[2])
         _assert_same_spaces(got, want)
+
+
+def test_lpt_loads_carry_across_waves():
+    """placement per training wave keeps each rank's cumulative cost. One-universe waves spread
+    over every rank (a fresh LPT per wave would give rank 0 all of them), and wave-by-wave placement of
+    equal-cost universes is exactly round-robin."""
+    rng = np.random.default_rng(2)
+    costs = {k: float(rng.integers(1, 100)) for k in range(40)}
+    for world in (2, 3, 8):
+        loads = [0.0] * world
+        owners = {}
+        for k in range(40):
+            owners.update(place_universes({k: costs[k]}, world, loads))
+        assert sorted(set(owners.values())) == list(range(world))
+        got = np.zeros(world)
+        for k, r in owners.items():
+            got[r] += costs[k]
+        np.testing.assert_allclose(got, loads)
+        assert max(loads) <= sum(loads) / world + max(costs.values()) + 1e-9   # online greedy bound
+        loads = [0.0] * world
+        eq = {}
+        for w0 in range(0, 12, 3):   # waves of 3 equal-cost universes
+            eq.update(place_universes({k: 1.0 for k in range(w0, w0 + 3)}, world, loads))
+        assert np.bincount(list(eq.values()), minlength=world).max() - \
+            np.bincount(list(eq.values()), minlength=world).min() <= 1
+    with pytest.raises(ValueError):
+        place_universes({0: 1.0}, 2, [0.0])
+
+
+def _dup_worker(rank, world, port, ckpt_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # the one-universe protocol registers every universe on every rank (add_embedding_space has no owner
+        # test): the same weights everywhere
+        cfg = _ck_config(ckpt_dir)
+        for uid in range(_CK_N):
+            rng = np.random.default_rng(uid)
+            em = np.sort(rng.choice(_CK_E, 10 + 3 * uid, replace=False))
+            rm = np.sort(rng.choice(_CK_R, 2 + uid % 3, replace=False))
+            torch.manual_seed(100 + uid)
+            cfg.add_embedding_space(TransE(len(em), len(rm), **_CK_PARAM))
+            cfg._register_maps(uid, em, rm)
+            cfg.next_universe_id += 1
+        cfg.save_model("dup.ckpt")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_multi_rank_checkpoint_with_every_rank_holding_every_universe(tmp_path):
+    """universes held by more than one rank are saved once (the owner's copy), not rejected."""
+    ckpt_dir = str(tmp_path) + os.sep
+    single = _ck_config(ckpt_dir)
+    _ck_inject(single)
+    mp.spawn(_dup_worker, args=(2, _free_port(), ckpt_dir), nprocs=2, join=True)
+    b = torch.load(ckpt_dir + "dup.ckpt", weights_only=False)
+    assert b["next_universe_id"] == _CK_N
+    _assert_same_spaces(_ck_summary(single),
+                        {u: {n: t.numpy() for n, t in m.state_dict().items()}
+                         for u, m in b["trained_embedding_spaces"].items()})

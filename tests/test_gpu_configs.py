@@ -227,13 +227,16 @@ def test_pu_workload_whole_set_and_longest_universes(name, data_dir):
         w.close()
 
 
+C4_LP_QUERIES = 240   # test queries of C4's link-prediction parity (of 6,000), every key against 1024 universes
+
+
 def test_c4_link_prediction_ranks_match_oracle(data_dir):
     """C4's link prediction (global energy estimation over 1024 trained universes, Parallel_Universe_Config.py
     :446-642): the device path (pt_lp_min_scores key rows -> pt_rank_rows) on a subset of test queries ranks
     every query as the oracle does on the same trained tables (equal up to float near-ties of the truth's
     score), and the metrics are those of the ranks."""
     from helpers import assert_ranks_match, metrics_match_ranks
-    from openke.config.Parallel_Universe_Config import lp_pair_array, lp_pairs_all
+    from openke.config.Parallel_Universe_Config import lookup_local, lp_pair_array, lp_pairs_all
     w = Workload("c4", data_dir)
     L, n = w.L, w.n
     try:
@@ -242,7 +245,7 @@ def test_c4_link_prediction_ranks_match_oracle(data_dir):
         trip = {f: np.loadtxt(os.path.join(w.path, f), dtype=np.int64, ndmin=2)
                 for f in ("train2id.txt", "valid2id.txt", "test2id.txt")}
         allt = np.concatenate(list(trip.values()))
-        test = trip["test2id.txt"][:12]
+        test = trip["test2id.txt"][:C4_LP_QUERIES]
         th, tt, tr = (np.ascontiguousarray(test[:, c]) for c in range(3))
         nq = len(th)
         ems, rms = [], []
@@ -300,30 +303,42 @@ def test_c4_link_prediction_ranks_match_oracle(data_dir):
                                 ranks[3].ctypes.data, nq, met.ctypes.data))
         metrics_match_ranks(met[:5], tuple(ranks))
         # the oracle: per key the MIN over every universe holding the anchor and the relation of its scores
-        # of every local entity, in candidate order (getHeadBatch / getTailBatch)
-        g2l = [{int(g): l for l, g in enumerate(em)} for em in ems]
-        r2l = [{int(g): l for l, g in enumerate(rm)} for rm in rms]
+        # of every local entity, in candidate order (getHeadBatch / getTailBatch); one oracle.score call per
+        # (universe, side) over all the queries the universe holds, universes on a thread pool
         tabs = [[x.cpu().numpy() for x in keep[k][0][:2]] for k in range(w.n_univ)]
-        con_h = np.full((nq, E), np.inf, dtype=np.float32)
-        con_t = np.full((nq, E), np.inf, dtype=np.float32)
-        for q in range(nq):
-            h, t, r = int(th[q]), int(tt[q]), int(tr[q])
-            head_vec = np.full(E, np.inf, dtype=np.float32)
-            tail_vec = np.full(E, np.inf, dtype=np.float32)
-            for k in range(w.n_univ):
-                if r not in r2l[k]:
+        head_vec = np.full((nq, E), np.inf, dtype=np.float32)
+        tail_vec = np.full((nq, E), np.inf, dtype=np.float32)
+
+        def universe_scores(k):
+            eo = np.argsort(ems[k], kind="stable")
+            ro = np.argsort(rms[k], kind="stable")
+            lh = lookup_local(ems[k][eo], eo, th)
+            lt = lookup_local(ems[k][eo], eo, tt)
+            lr = lookup_local(rms[k][ro], ro, tr)
+            out = []
+            Ek = w.E[k]
+            loc = np.arange(Ek, dtype=np.int64)
+            for mode, anchor in (("tail_batch", lh), ("head_batch", lt)):
+                qs = np.nonzero((lr >= 0) & (anchor >= 0))[0]
+                if len(qs) == 0:
                     continue
-                loc = np.arange(w.E[k], dtype=np.int64)
-                if h in g2l[k]:
-                    s = oracle.score("TransE", w.p, True, "tail_batch", tabs[k][0], tabs[k][1], None,
-                                     np.array([g2l[k][h]]), loc, np.array([r2l[k][r]]))
-                    tail_vec[ems[k]] = np.minimum(tail_vec[ems[k]], s)
-                if t in g2l[k]:
-                    s = oracle.score("TransE", w.p, True, "head_batch", tabs[k][0], tabs[k][1], None, loc,
-                                     np.array([g2l[k][t]]), np.array([r2l[k][r]]))
-                    head_vec[ems[k]] = np.minimum(head_vec[ems[k]], s)
-            con_h[q] = head_vec[oracle.candidates(E, h)]
-            con_t[q] = tail_vec[oracle.candidates(E, t)]
+                a = np.repeat(anchor[qs], Ek)
+                c = np.tile(loc, len(qs))
+                rr = np.repeat(lr[qs], Ek)
+                sc = oracle.score("TransE", w.p, True, mode, tabs[k][0], tabs[k][1], None,
+                                  a if mode == "tail_batch" else c, c if mode == "tail_batch" else a, rr)
+                out.append((mode, qs, sc.reshape(len(qs), Ek)))
+            return k, out
+
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=16) as ex:
+            for k, out in ex.map(universe_scores, range(w.n_univ)):
+                for mode, qs, sc in out:
+                    vec = tail_vec if mode == "tail_batch" else head_vec
+                    sub = vec[np.ix_(qs, ems[k])]
+                    vec[np.ix_(qs, ems[k])] = np.minimum(sub, sc)
+        con_h = np.stack([head_vec[q][oracle.candidates(E, int(th[q]))] for q in range(nq)])
+        con_t = np.stack([tail_vec[q][oracle.candidates(E, int(tt[q]))] for q in range(nq)])
         _, want = oracle.link_prediction(E, [allt[:, 0], allt[:, 1], allt[:, 2]], (th, tt, tr), con_h, con_t)
         assert_ranks_match(tuple(ranks), want, con_h, con_t)
     finally:
@@ -371,11 +386,13 @@ def test_c1_wn18_steps_match_oracle(bs, data_dir):
             got = [t.detach().cpu().numpy() for t in kge.tables()[:2]]
             before = (ent.copy(), rel.copy())
             h, t, r, _ = kg.sample(st, 8, bs, neg, bern, filt)
+            gm = oracle.grad_mass(model, p, True, margin, ent, rel, None, h, t, r, bs, neg)
             want = oracle.train_step(model, p, True, opt, lr, margin, ent, rel, None, (None, None, None), h, t, r, bs,
                                      neg)
             assert abs(float(loss.item()) - want) <= 1e-5 * max(1.0, abs(want)), (k, float(loss.item()), want)
             for gg, ww, b0, nm in zip(got, (ent, rel), before, ("ent", "rel")):
-                assert_step_close(gg, ww, 2e-6, what="step %d %s" % (k, nm), before=b0)
+                assert_step_close(gg, ww, 2e-6, what="step %d %s" % (k, nm), before=b0, grad=gm[nm][0],
+                                  mass=gm[nm][1], lr=lr)
     finally:
         torch.cuda.synchronize()
         L.pt_trainer_free(tr)

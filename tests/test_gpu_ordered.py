@@ -342,3 +342,33 @@ def test_deterministic_mode_switches_per_trainer():
     finally:
         L.pt_trainer_free(a)
         L.pt_trainer_free(b)
+
+
+def test_failed_deterministic_enable_leaves_fast_mode():
+    """a universe set whose batch is too large for the reference-order LDS plan refuses
+    pt_universe_set_deterministic (PT_ENOTSUP) and stays in the fast mode - a later train call runs the fast
+    kernel (finite losses, trained tables) instead of launching the ordered kernel without its workspace."""
+    import ctypes
+    from openke import _native
+    L = _native.lib()
+    g, jobs, cases = _universe_jobs("TransE", [20], 1, 0, 0, 3, "adagrad", epochs=1, nbatches=2)
+    try:
+        jobs[0].batch_size = cases[0]["bs"] = 1100   # 2,200 slots: 202 KB of ordered-mode LDS (> 160 KB)
+        arr = (_native.UniverseJob * 1)(*jobs)
+        uset = ctypes.c_void_p()
+        _native.check(L.pt_universe_set_create(arr, 1, 0, 1, 1, _native.PT_ADAGRAD, 0, 0, ctypes.byref(uset)))
+        try:
+            before = cases[0]["dev"][0].clone()
+            assert L.pt_universe_set_deterministic(uset, 1) != 0
+            assert b"too large" in L.pt_last_error()
+            losses = torch.zeros(1, device="cuda")
+            _native.check(L.pt_universe_set_train(uset, _native.ptr(losses), _native.stream()))
+            torch.cuda.synchronize()
+            assert torch.isfinite(losses).all() and float(losses[0]) > 0
+            assert not torch.equal(before, cases[0]["dev"][0])
+        finally:
+            L.pt_universe_set_free(uset)
+    finally:
+        for c in cases:
+            L.pt_universe_free(c["h"])
+        L.pt_graph_free(g)

@@ -109,6 +109,8 @@ def _teacher_forced_universes(L, cases, model, p, opt, neg, bern, filt, atol=2e-
             acc0 = [None if a is None else a.copy() for a in x["accs"]]
             tab0 = [None if a is None else a.copy() for a in x["tabs"]]
             hh, tt, rr, _ = c["ug"].sample(x["st"], 8, c["bs"], neg, bern, filt)
+            gm = oracle.grad_mass(model, p, True, c["margin"], x["tabs"][0], x["tabs"][1], x["tabs"][2], hh, tt, rr,
+                                  c["bs"], neg)
             want = oracle.train_step(model, p, True, opt, c["lr"], c["margin"], x["tabs"][0], x["tabs"][1],
                                      x["tabs"][2], x["accs"] if ada else (None, None, None), hh, tt, rr, c["bs"], neg)
             assert abs(float(lh[q]) - want) <= 1e-5 * max(1.0, abs(want)), (i, k, float(lh[q]), want)
@@ -119,7 +121,7 @@ def _teacher_forced_universes(L, cases, model, p, opt, neg, bern, filt, atol=2e-
                 mask = step_noise(a0, x["accs"][("ent", "rel", "norm").index(name)], ga) if ada else None
                 masked += 0 if mask is None else int(mask.sum())
                 assert_step_close(g.cpu().numpy(), w, atol, mask, what="universe %d step %d %s" % (i, k, name),
-                                  before=w0)
+                                  before=w0, grad=gm[name][0], mass=gm[name][1], lr=c["lr"])
     return masked
 
 

@@ -315,3 +315,43 @@ def test_count_header_legacy_loaders(tmp_path):
     finally:
         L.pt_set_count_header(0)
         load(KG_SMALL)   # leave the global context as other tests expect it
+
+
+def test_test_loader_inherits_count_header(tmp_path):
+    """A default TestDataLoader after TrainDataLoader(count_header=True) reads with the train loader's format
+    (it does not switch the process back to the line-count reader, which would re-read train2id.txt and fail)."""
+    from openke.data import TestDataLoader, TrainDataLoader
+    L = _native.lib()
+    hdr = _header_copy(tmp_path)
+    try:
+        tr = TrainDataLoader(in_path=hdr, nbatches=10, threads=8, count_header=True)
+        te = TestDataLoader(tr.in_path, "link")
+        assert te.count_header is True and L.pt_get_count_header() == 1
+        assert (te.entTotal, te.relTotal, L.getTrainTotal(), L.getTestTotal()) == (500, 7, 3000, 100)
+        # an explicit choice still wins
+        assert TestDataLoader(tr.in_path, "link", count_header=True).count_header is True
+    finally:
+        L.pt_set_count_header(0)
+        L.setInPath(ctypes.create_string_buffer(KG_SMALL.encode(), len(KG_SMALL) * 2))
+        L.importTrainFiles()
+        L.importTestFiles()
+
+
+@pytest.mark.parametrize("san", ["address", "thread"])
+def test_host_sanitizers(san):
+    """the host side under ASan + UBSan and under TSan (make san: the reader, universe construction
+    single and pt_universe_build_many on 8 threads, host ranking on 8 workers, the Base.so-compatible context,
+    the oracle's multi-threaded loop; each multi-threaded result equal to its one-thread form). Any sanitizer
+    report fails the driver (ASan / UBSan abort, TSan exits non-zero)."""
+    import subprocess
+    pkg = os.path.join(REPO, "openke-putranse_amd")
+    if not os.path.exists(os.path.join(pkg, "build", "kernels.hip.o")):
+        pytest.skip("product build objects absent (make -C openke-putranse_amd first)")
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66", ASAN_OPTIONS="detect_leaks=1",
+               UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1")
+    r = subprocess.run(["make", "-C", pkg, "san", "SAN=" + san, "-j8"], capture_output=True, text=True, env=env,
+                       timeout=900)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "san_driver: ok (0 failed checks)" in out
+    assert "Sanitizer" not in out and "runtime error" not in out, out[-4000:]

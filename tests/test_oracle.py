@@ -231,3 +231,26 @@ def test_validator_hit10_matches_reference(path):
         con_t[q] = oracle.score(model, p, True, "tail_batch", ent, rel, nv, [h], oracle.candidates(E, t), [r])
     _, ranks = oracle.link_prediction(E, all_tr, ev, con_h, con_t)
     assert valid_hit10(ranks) == pytest.approx(float(z["hit10"]), rel=1e-6, abs=1e-7)
+
+
+@pytest.mark.parametrize("model", ["TransE", "TransH"])
+def test_grad_mass_is_the_step_gradient(model):
+    """oracle.grad_mass (the tolerance model of helpers.assert_step_close): its gradient is the one the SGD step
+    applies (lr 1: w_after == w + (-1) * g bit for bit), and the contributions' magnitude sum bounds it."""
+    kg = oracle.KG.load(KG_SMALL)
+    rng = np.random.default_rng(5)
+    d = 21
+    ent = rng.uniform(-0.3, 0.3, (kg.ent_total, d)).astype(np.float32)
+    rel = rng.uniform(-0.3, 0.3, (kg.rel_total, d)).astype(np.float32)
+    nv = rng.uniform(-0.3, 0.3, (kg.rel_total, d)).astype(np.float32) if model == "TransH" else None
+    st = oracle.GlibcRand(9).rand_reset(8)
+    h, t, r, _ = kg.sample(st, 8, 40, 3, 1, 1)
+    gm = oracle.grad_mass(model, 1, True, 2.0, ent, rel, nv, h, t, r, 40, 3)
+    before = {"ent": ent.copy(), "rel": rel.copy(), "norm": None if nv is None else nv.copy()}
+    oracle.train_step(model, 1, True, "sgd", 1.0, 2.0, ent, rel, nv, (None, None, None), h, t, r, 40, 3)
+    for name, after in (("ent", ent), ("rel", rel), ("norm", nv)):
+        if after is None:
+            continue
+        g, m = gm[name]
+        np.testing.assert_array_equal(after, before[name] + (-1.0) * g)
+        assert (m >= np.abs(g) * (1 - 1e-6)).all() and m.max() > 0

@@ -1,0 +1,98 @@
+"""Host-side logic of the drop-in Parallel_Universe_Config (CPU, no GPU): the private-generator model factory
+equals the reference's manual_seed + constructor init bit for bit, the private per-universe Python draws equal
+the reference's globally seeded draws, the lazily registered id dictionaries equal the reference's per-entity
+registration (Parallel_Universe_Config.py:179-207), and the default wave size is a multiple of valid_steps."""
+import random
+from collections import defaultdict
+
+import numpy as np
+import pytest
+import torch
+
+from openke import _native
+from openke.config.Parallel_Universe_Config import Parallel_Universe_Config, universe_dim
+from openke.module.model import TransE, TransH
+
+
+@pytest.mark.parametrize("cls", [TransE, TransH])
+@pytest.mark.parametrize("kw", [{"dim": 23, "p_norm": 1, "norm_flag": True}, {"dim": 8, "margin": 4.0, "epsilon": 2.0}])
+def test_seeded_factory_equals_manual_seed_init(cls, kw):
+    torch.manual_seed(11)
+    a = cls(97, 5, **kw)
+    state = torch.get_rng_state()
+    b = cls.seeded(11, 97, 5, **kw)
+    assert torch.equal(state, torch.get_rng_state())   # the process-global generator is untouched
+    sa, sb = a.state_dict(), b.state_dict()
+    assert sa.keys() == sb.keys()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+
+
+class _Loader(object):
+    def __init__(self):
+        self.lib = _native.lib()
+        self.entTotal, self.relTotal = 400, 9
+        self.in_path = "unused/"
+        self.batch_size, self.nbatches = 10, 20
+
+
+def _config(**kw):
+    return Parallel_Universe_Config(train_dataloader=_Loader(), valid_dataloader=object(), embedding_model=TransE,
+                                    embedding_model_param={"dim": 8, "p_norm": 1, "norm_flag": True}, **kw)
+
+
+def test_private_draws_equal_reference_draws():
+    cfg = _config(min_lr=0.001, max_lr=0.1)
+    for uid in range(20):
+        random.seed(cfg.initial_random_seed + uid)   # set_random_seed(seed0 + uid) then the reference's order
+        tc = random.randrange(cfg.min_triple_constraint, cfg.max_triple_constraint)
+        bal = round(random.uniform(cfg.min_balance, cfg.max_balance), 2)
+        margin = random.randrange(cfg.min_margin, cfg.max_margin)
+        epochs = random.randrange(cfg.min_num_epochs, cfg.max_num_epochs)
+        lr = round(random.uniform(cfg.min_lr, cfg.max_lr), 3)
+        assert cfg._universe_draws(uid) == (tc, bal, margin, epochs, lr)
+
+
+def test_lazy_id_maps_equal_reference_registration():
+    rng = np.random.default_rng(4)
+    cfg = _config()
+    want_e, want_r = defaultdict(dict), defaultdict(dict)
+    want_eu, want_ru = defaultdict(set), defaultdict(set)
+    for uid in range(30):
+        em = rng.choice(400, int(rng.integers(1, 120)), replace=False)
+        rm = rng.choice(9, int(rng.integers(1, 9)), replace=False)
+        for local, g in enumerate(em.tolist()):   # the reference's loop (:179-207)
+            want_e[uid][g] = local
+            want_eu[g].add(uid)
+        for local, g in enumerate(rm.tolist()):
+            want_r[uid][g] = local
+            want_ru[g].add(uid)
+        cfg._register_maps(uid, em, rm)
+        if uid == 14:   # a read in between registers the pending universes; later ones stay pending
+            assert dict(cfg.entity_universes) == dict(want_eu)
+    assert {u: dict(m) for u, m in cfg.entity_id_mappings.items()} == dict(want_e)
+    assert {u: dict(m) for u, m in cfg.relation_id_mappings.items()} == dict(want_r)
+    assert dict(cfg.entity_universes) == dict(want_eu)
+    assert dict(cfg.relation_universes) == dict(want_ru)
+    assert cfg.gather_embedding_spaces(int(list(want_eu)[0]), int(list(want_ru)[0])) == \
+        want_eu[list(want_eu)[0]] & want_ru[list(want_ru)[0]]
+    # a replaced state (get_best_state / load) drops universes registered after it
+    snap = cfg.get_state()
+    cfg.best_state = snap
+    cfg._register_maps(30, np.array([1, 2]), np.array([0]))
+    cfg.get_best_state()
+    assert 30 not in cfg.entity_id_mappings and 30 not in cfg.entity_universes[1]
+
+
+def test_default_wave_size_is_a_multiple_of_valid_steps():
+    for vs in (1, 5, 100, 128, 600, 1000):
+        w = _config(valid_steps=vs).wave_size()
+        assert w % vs == 0 and w >= vs and (vs > 512 or abs(w - 512) <= vs / 2)
+    assert _config(valid_steps=100, universe_wave_size=7).wave_size() == 7
+
+
+def test_universe_dim_range():
+    assert universe_dim(20, 5) == 20
+    dims = [universe_dim((20, 100), u) for u in range(200)]
+    assert min(dims) >= 20 and max(dims) <= 100 and len(set(dims)) > 30
+    assert dims[:3] == [int(np.random.default_rng(1000 + u).integers(20, 101)) for u in range(3)]
