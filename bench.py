@@ -293,6 +293,10 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
             print("universe-prof span %.1f Mcyc steps %d bs %d D %d E %d  cycles/step: presample %.0f"
                   "  A %.0f  B %.0f" % (span[i] / 1e6, steps, prof[i, 4], prof[i, 5], prof[i, 6],
                                        prof[i, 0] / steps, prof[i, 1] / steps, prof[i, 2] / steps), file=sys.stderr)
+        if os.environ.get("PT_UNI_PROF_DUMP"):   # every universe's phase cycles + its job (time-model fits)
+            np.savez(os.environ["PT_UNI_PROF_DUMP"], prof=prof, dims=np.array([int(j.dim) for j in jobs]),
+                     bs=np.array([int(j.batch_size) for j in jobs]), epochs=np.array([int(j.epochs) for j in jobs]),
+                     E=np.array([u["ent"].shape[0] for u in unis]), run_s=el / args.c3_steps)
         tot_p = prof[:, :3].sum(axis=0) / max(prof[:, 3].sum(), 1)
         print("universe-prof all: cycles/step presample %.0f A %.0f B %.0f" % tuple(tot_p), file=sys.stderr)
         print("universe-prof longest universe: %.1f Mcycles (%.1f ms at 2.4 GHz); run %.1f ms" %
@@ -546,26 +550,26 @@ def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
             "note": "universe scoring 4D+4 B per (key, universe entity); ranking 4 B per (query, entity)"}
 
 
-def load_traffic_by_kernel(tag):
-    """Per-kernel (2 x FETCH_SIZE + WRITE_SIZE) bytes per step from the committed PMC summary, if present."""
-    f = os.path.join(HERE, "profiles", "pmc_%s.json" % tag)
-    if not os.path.exists(f):
-        return None
-    try:
-        return json.load(open(f)).get("bytes_per_step_by_kernel")
-    except Exception:
-        return None
+def library_sha256():
+    """sha256 of the library this process loaded (the product build unless tools_gpu/ablib.py swapped it)."""
+    import hashlib
+    from openke import _native
+    return hashlib.sha256(open(_native.LIB_PATH, "rb").read()).hexdigest()
 
 
-def load_traffic(tag):
-    """Per-launch HBM bytes of k_step + k_apply from a committed rocprofv3 --pmc summary, if present."""
+def load_pmc(tag):
+    """The committed rocprofv3 --pmc summary profiles/pmc_<tag>.json when it was taken on THIS library build
+    (its lib_sha256 equals the loaded library's), else None: counter evidence is never borrowed from another
+    build. Returns (summary or None, its digest)."""
     f = os.path.join(HERE, "profiles", "pmc_%s.json" % tag)
     if not os.path.exists(f):
-        return None
+        return None, None
     try:
-        return json.load(open(f)).get("bytes_per_step")
+        rec = json.load(open(f))
     except Exception:
-        return None
+        return None, None
+    sha = rec.get("lib_sha256")
+    return (rec if sha and sha == library_sha256() else None), sha
 
 
 def main():
@@ -607,6 +611,10 @@ def main():
                 rec["link_prediction"] = c3["link_prediction"]
             if dropin is not None:
                 rec["dropin"] = dropin
+            for k in ("placement", "deterministic_s_per_step", "deterministic_triples_per_s", "longest_universe_cycles",
+                      "note_runs", "host_universe_build_s"):
+                if k in c3:
+                    rec[k] = c3[k]
             if "cpu_baseline" in c3:
                 rec["cpu_baseline"] = c3["cpu_baseline"]
             print(json.dumps(rec), flush=True)
@@ -703,8 +711,9 @@ def main():
     bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
     step_kernel_s = sum(per_kernel.values()) * 1e-3
     achieved = bytes_step / step_kernel_s / 1e9
-    traffic = load_traffic(args.workload)
-    counted = load_traffic_by_kernel(args.workload)
+    pmc, pmc_sha = load_pmc(args.workload)
+    traffic = pmc.get("bytes_per_step") if pmc else None
+    counted = pmc.get("bytes_per_step_by_kernel") if pmc else None
     kernel_detail = {}
     for kname, ms in per_kernel.items():
         b = next((v for k, v in counted.items() if kname in k), None) if counted else None
@@ -749,6 +758,8 @@ def main():
                      "algorithmic_bytes_per_step": bytes_step,
                      "counted_frac": None if traffic is None else traffic / (step_kernel_s * 1e9) / HBM_PEAK_GBS,
                      "per_kernel": kernel_detail,
+                     "lib_sha256": library_sha256(), "counters_lib_sha256": pmc_sha,
+                     "counters_match_build": pmc is not None,
                      "contrib_roundtrip_bytes": contrib_rt if spath != _native.PT_PATH_SAMPLED else 0,
                      "contrib_share_of_counted": None if traffic is None or spath == _native.PT_PATH_SAMPLED
                      else contrib_rt / traffic,

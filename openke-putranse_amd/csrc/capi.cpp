@@ -10,6 +10,7 @@
 #include <mutex>
 #include <thread>
 #include <tuple>
+#include <unordered_map>
 #include <queue>
 #include <vector>
 
@@ -985,6 +986,7 @@ struct pt_universe_set {
     std::vector<int64_t> host_loss_off;
     std::vector<int64_t> host_of_job;     // job index -> index in host / d_us
     std::vector<uint64_t> seeds0;         // [host][64]: the jobs' LCG states at creation (pt_universe_set_reset)
+    void *graph_arena = nullptr;          // the universes' device graphs (one allocation, one copy)
     uint64_t *prof = nullptr;             // PT_UNI_PROF=1: [n][64] cycle counters + shape (+ stamps) (device)
     // reference-order (deterministic) mode (pt_universe_set_deterministic): ordered.hip's universe kernel
     bool ordered = false;
@@ -996,6 +998,7 @@ struct pt_universe_set {
         if (arena) (void)hipFree(arena);
         if (prof) (void)hipFree(prof);
         if (ord_arena) (void)hipFree(ord_arena);
+        if (graph_arena) (void)hipFree(graph_arena);
     }
 };
 
@@ -1017,7 +1020,8 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         int64_t states, contrib, grad, flags;
     };
     std::vector<Slot> slots((size_t)n);
-    int64_t total = 0;
+    // every universe's LCG states first, 64 words each in set order (one upload, one reset copy)
+    int64_t total = al(512 * std::max<int64_t>(n, 1));
     for (int64_t i = 0; i < n; ++i) {
         const pt_universe_job &J = jobs[i];
         PT_CHECK(J.graph && J.seeds && J.ent && J.rel, PT_EINVAL, "universe job: null graph / seeds / tables");
@@ -1034,7 +1038,6 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         PT_CHECK(g.train_total > 0 || J.batch_size == 0, PT_EINVAL, "universe job: empty graph");
         PT_CHECK(J.batch_size * (4 + J.neg) <= 16384, PT_EINVAL, "universe job: batch too large for the LDS work list");
         const int64_t rows = g.ent_total + g.rel_total * (model == 1 ? 2 : 1);
-        slots[i].states = total; total += al(8 * J.threads);
         slots[i].contrib = total; total += al(4 * J.batch_size * (4 + J.neg) * J.dim);
         slots[i].grad = total;   total += al(4 * rows * J.dim);
         slots[i].flags = total;  total += al(4 * (g.ent_total + 2 * g.rel_total));
@@ -1090,7 +1093,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
             const auto &gr = set->groups[k];
             for (int64_t q = gr.off; q < gr.off + gr.n; ++q) {
                 const pt_universe_job &J = jobs[order[q]];
-                const int64_t gpb = pt::universe_shape_groups(pt::universe_shape_id(J.dim, model));
+                const int64_t gpb = pt::universe_shape_groups(pt::universe_shape_id(J.dim, model), model);
                 const int64_t rounds = (std::max<int64_t>(J.batch_size, 1) + gpb - 1) / gpb;
                 tg[k].push_back((double)J.epochs * (double)J.nbatches * (double)(uni_fixed + rounds));
             }
@@ -1129,18 +1132,53 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         loss_of[i] = loss_off;
         loss_off += jobs[i].epochs;
     }
+    // the universes' device graphs: host images built on worker threads (each distinct graph once), placed in
+    // one allocation with one copy
+    std::vector<const pt::Graph *> uniq;
+    std::vector<int64_t> gidx((size_t)n);
+    {
+        std::unordered_map<const pt::Graph *, int64_t> seen;
+        for (int64_t i = 0; i < n; ++i) {
+            const pt::Graph *gp = &reinterpret_cast<const pt_graph *>(jobs[i].graph)->g;
+            auto it = seen.find(gp);
+            if (it == seen.end()) {
+                it = seen.emplace(gp, (int64_t)uniq.size()).first;
+                uniq.push_back(gp);
+            }
+            gidx[i] = it->second;
+        }
+    }
+    std::vector<std::vector<char>> images(uniq.size());
+    {
+        std::atomic<int64_t> next{0};
+        auto work = [&]() {
+            for (int64_t k; (k = next.fetch_add(1)) < (int64_t)uniq.size();)
+                images[k] = const_cast<pt::Graph *>(uniq[k])->device_image();
+        };
+        const int64_t nw = std::min<int64_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+        std::vector<std::thread> pool;
+        for (int64_t w = 1; w < std::min<int64_t>(nw, (int64_t)uniq.size()); ++w) pool.emplace_back(work);
+        work();
+        for (auto &th : pool) th.join();
+    }
+    std::vector<int64_t> goff(uniq.size() + 1, 0);
+    for (size_t k = 0; k < uniq.size(); ++k) goff[k + 1] = goff[k] + al((int64_t)images[k].size());
+    {
+        std::vector<char> staging((size_t)std::max<int64_t>(goff.back(), 1));
+        for (size_t k = 0; k < uniq.size(); ++k) memcpy(staging.data() + goff[k], images[k].data(), images[k].size());
+        PT_HIP(hipMalloc(&set->graph_arena, staging.size()));
+        PT_HIP(hipMemcpy(set->graph_arena, staging.data(), staging.size(), hipMemcpyHostToDevice));
+    }
     int64_t max_bs = 0, max_relg = 0, max_ent = 0, max_rel = 0, max_seq = 0, max_nb = 0;
+    set->seeds0.assign((size_t)(64 * std::max<int64_t>(n, 1)), 0);
     for (int64_t i : order) {
         const pt_universe_job &J = jobs[i];
-        pt::Graph &g = const_cast<pt::Graph &>(reinterpret_cast<const pt_graph *>(J.graph)->g);
-        int rc = g.upload();
-        if (rc) return rc;
+        const pt::Graph &g = *uniq[(size_t)gidx[i]];
+        const int64_t k = (int64_t)set->host.size();   // position in the set
         pt::UniverseDev U{};
-        U.g = g.dev;
-        U.states = (uint64_t *)(base + slots[i].states);
-        PT_HIP(hipMemcpy(U.states, J.seeds, 8 * J.threads, hipMemcpyHostToDevice));
-        set->seeds0.insert(set->seeds0.end(), J.seeds, J.seeds + J.threads);
-        set->seeds0.resize(64 * (set->host.size() + 1), 0);
+        U.g = g.bind_image((char *)set->graph_arena + goff[(size_t)gidx[i]]);
+        U.states = (uint64_t *)(base + 512 * k);
+        std::copy(J.seeds, J.seeds + J.threads, set->seeds0.begin() + 64 * k);
         U.ent = J.ent; U.rel = J.rel; U.normv = J.normv;
         U.ent_acc = J.ent_acc; U.rel_acc = J.rel_acc; U.norm_acc = J.norm_acc;
         float *gr = (float *)(base + slots[i].grad);
@@ -1168,6 +1206,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         max_seq = std::max(max_seq, J.batch_size * (1 + J.neg));
         max_nb = std::max(max_nb, J.nbatches);
     }
+    if (n > 0) PT_HIP(hipMemcpy(base, set->seeds0.data(), 8 * set->seeds0.size(), hipMemcpyHostToDevice));
     // LDS plan (within the device's per-workgroup limit and half a CU): the work list is required;
     // then, each if it still fits, the relation gradient rows (the contended rows of the scatter), the
     // entity contribution lists (replace the entity float atomics), the touched flags, and as many
@@ -1308,9 +1347,8 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
 // start: the caller restores the tables and optimizer state)
 extern "C" int pt_universe_set_reset(pt_universe_set *set) {
     PT_CHECK(set, PT_EINVAL, "null universe set");
-    for (size_t i = 0; i < set->host.size(); ++i)
-        PT_HIP(hipMemcpy(set->host[i].states, set->seeds0.data() + 64 * i, 8 * (size_t)set->host[i].threads,
-                         hipMemcpyHostToDevice));
+    if (!set->host.empty())   // the states block at the arena's start, in set order
+        PT_HIP(hipMemcpy(set->arena, set->seeds0.data(), 8 * set->seeds0.size(), hipMemcpyHostToDevice));
     return PT_OK;
 }
 

@@ -196,12 +196,25 @@ int load_graph(const std::string &dir, Graph &g) {
     return PT_OK;
 }
 
-int Graph::upload() {
-    int cur = 0;
-    PT_HIP(hipGetDevice(&cur));
-    if (dev_block && device == cur) return PT_OK;
-    PT_CHECK(!dev_block, PT_ESTATE, "graph already uploaded to another device");
+namespace {
+struct ImageLayout {
+    size_t rec, ht, th, bp, rr, hr, total;
+    ImageLayout(int64_t n, int64_t R) {
+        auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+        rec = 0;
+        ht = rec + al(sizeof(TripleRec) * n);
+        th = ht + al(4 * n);
+        bp = th + al(4 * n);
+        rr = bp + al(4 * (R ? R : 1));
+        hr = rr + al(4 * n);
+        total = hr + al(8 * n);
+    }
+};
+}  // namespace
+
+std::vector<char> Graph::device_image() {
     const int64_t n = train_total, R = rel_total;
+    const ImageLayout L(n, R);
     std::vector<TripleRec> rec((size_t)n);
     // (h,r) runs of the cmp_head list
     for (int64_t i = 0; i < n;) {
@@ -226,20 +239,16 @@ int Graph::upload() {
         }
         i = j + 1;
     }
-    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t off_rec = 0, off_ht = off_rec + al(sizeof(TripleRec) * n), off_th = off_ht + al(4 * n),
-                 off_bp = off_th + al(4 * n), off_rr = off_bp + al(4 * (R ? R : 1)), off_hr = off_rr + al(4 * n),
-                 total = off_hr + al(8 * n);
-    std::vector<char> host(total, 0);
-    memcpy(host.data() + off_rec, rec.data(), sizeof(TripleRec) * n);
-    int32_t *ht = (int32_t *)(host.data() + off_ht), *th = (int32_t *)(host.data() + off_th);
+    std::vector<char> host(L.total, 0);
+    memcpy(host.data() + L.rec, rec.data(), sizeof(TripleRec) * n);
+    int32_t *ht = (int32_t *)(host.data() + L.ht), *th = (int32_t *)(host.data() + L.th);
     for (int64_t i = 0; i < n; ++i) {
         ht[i] = (int32_t)head[i].t;
         th[i] = (int32_t)tail[i].h;
     }
     // corrupt_rel (Corrupt.h:108-189): the relations of the cmp_rel list and, per triple in head order,
     // the (h,t) run [ll, rr] its two binary searches find
-    int32_t *rr_col = (int32_t *)(host.data() + off_rr), *hr_run = (int32_t *)(host.data() + off_hr);
+    int32_t *rr_col = (int32_t *)(host.data() + L.rr), *hr_run = (int32_t *)(host.data() + L.hr);
     std::vector<int64_t> rorder((size_t)n);
     for (int64_t i = 0; i < n; ++i) rorder[i] = i;
     std::sort(rorder.begin(), rorder.end(), [&](int64_t a, int64_t b) { return cmp_rel(list[a], list[b]); });
@@ -255,20 +264,35 @@ int Graph::upload() {
         if (j - i + 1 >= R) ht_full = true;
         i = j + 1;
     }
-    float *bp = (float *)(host.data() + off_bp);
+    float *bp = (float *)(host.data() + L.bp);
     for (int64_t r = 0; r < R; ++r) bp[r] = 1000 * right_mean[r] / (right_mean[r] + left_mean[r]);
-    PT_HIP(hipMalloc(&dev_block, total));
-    PT_HIP(hipMemcpy(dev_block, host.data(), total, hipMemcpyHostToDevice));
-    char *b = (char *)dev_block;
-    dev.ent_total = ent_total;
-    dev.rel_total = R;
-    dev.train_total = n;
-    dev.rec = (const TripleRec *)(b + off_rec);
-    dev.head_t = (const int32_t *)(b + off_ht);
-    dev.tail_h = (const int32_t *)(b + off_th);
-    dev.bern_prob = (const float *)(b + off_bp);
-    dev.rel_r = (const int32_t *)(b + off_rr);
-    dev.ht_run = (const int2 *)(b + off_hr);
+    return host;
+}
+
+DeviceGraph Graph::bind_image(char *b) const {
+    const ImageLayout L(train_total, rel_total);
+    DeviceGraph d;
+    d.ent_total = ent_total;
+    d.rel_total = rel_total;
+    d.train_total = train_total;
+    d.rec = (const TripleRec *)(b + L.rec);
+    d.head_t = (const int32_t *)(b + L.ht);
+    d.tail_h = (const int32_t *)(b + L.th);
+    d.bern_prob = (const float *)(b + L.bp);
+    d.rel_r = (const int32_t *)(b + L.rr);
+    d.ht_run = (const int2 *)(b + L.hr);
+    return d;
+}
+
+int Graph::upload() {
+    int cur = 0;
+    PT_HIP(hipGetDevice(&cur));
+    if (dev_block && device == cur) return PT_OK;
+    PT_CHECK(!dev_block, PT_ESTATE, "graph already uploaded to another device");
+    const std::vector<char> host = device_image();
+    PT_HIP(hipMalloc(&dev_block, host.size()));
+    PT_HIP(hipMemcpy(dev_block, host.data(), host.size(), hipMemcpyHostToDevice));
+    dev = bind_image((char *)dev_block);
     device = cur;
     return PT_OK;
 }

@@ -47,6 +47,11 @@ struct Graph {
     ~Graph();
     void build_helpers();                 // loadHelpers / loadUniverseHelpers (Reader.h:58-167)
     int upload();                         // PT_OK or error; idempotent
+    // the device image of the graph as host bytes (layout of DeviceGraph, 256-byte aligned parts; sets
+    // ht_full) and the DeviceGraph of that image placed at device address `base` (upload() = image + one
+    // allocation + bind; a universe set places many images in one allocation)
+    std::vector<char> device_image();
+    DeviceGraph bind_image(char *base) const;
 };
 
 int load_graph(const std::string &dir, Graph &g);   // importTrainFiles (Reader.h:169-234)

@@ -26,11 +26,18 @@ struct UniverseDev {
     int32_t shape;                                  // universe_shape_id(dim)
 };
 
-// workgroup size of each shape class's kernel (the 16-float class keeps 512 threads at 256 VGPRs)
+// workgroup size of each (model, shape class) kernel. TransE's classes below PT_UNI_NT_CLS run 1,024
+// threads (16 waves, 4 per SIMD, 128 VGPRs: twice the lane groups, so a step's positives take half the rounds
+// and twice the waves hide each other's latency; measured C3 57.4 -> 52.5 ms, its longest universe 135 -> 100
+// Mcycles); the 16-float class and TransH (whose step keeps more rows live: at 128 VGPRs it spills, C5 37 -> 89
+// ms) keep 512 threads at 256 VGPRs
 #ifndef PT_UNI_NT
-#define PT_UNI_NT 512
+#define PT_UNI_NT 1024
 #endif
-constexpr int kUniverseClassThreads[3] = {PT_UNI_NT, PT_UNI_NT, 512};
+#ifndef PT_UNI_NT_CLS
+#define PT_UNI_NT_CLS 3
+#endif
+constexpr int universe_class_threads(int model, int cls) { return model == 0 && cls < PT_UNI_NT_CLS ? PT_UNI_NT : 512; }
 
 // launch configuration of one group of universes (host-chosen for the largest universe of the group)
 struct UniverseLaunch {
@@ -58,6 +65,6 @@ hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, in
                             int p_norm, int norm_flag, int opt, int64_t neg, int bern, int filter,
                             const UniverseLaunch &cfg, hipStream_t st);
 int universe_shape_class(int shape);
-int universe_shape_groups(int shape);
+int universe_shape_groups(int shape, int model);
 
 }  // namespace pt

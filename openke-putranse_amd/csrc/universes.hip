@@ -44,9 +44,9 @@ int universe_shape_class(int shape) {
 }
 
 // lane groups of a universe workgroup for a shape (positives of a step processed concurrently)
-int universe_shape_groups(int shape) {
+int universe_shape_groups(int shape, int model) {
 #define PT_UGPB(ID_, G_, V_, K_) \
-    if (shape == ID_) return kUniverseClassThreads[PT_UCLASS(V_, K_)] / G_;
+    if (shape == ID_) return universe_class_threads(model, PT_UCLASS(V_, K_)) / G_;
     PT_USHAPES(PT_UGPB)
 #undef PT_UGPB
     return 1;

@@ -83,6 +83,75 @@ __device__ __forceinline__ void unormalize_bwd(const V<G, VEC, KCH> &x, float n,
     for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = (g.x[i] - x.x[i] * c) * inv;
 }
 
+// Rows of up to 128 floats (16 lanes or fewer) take KCH = ceil(chunks / G) chunks per lane instead of the next
+// power of two: e.g. D = 69 on 16 lanes holds 5 floats per lane, not 8 (C3 48.3 -> 43.3 ms, the longest
+// universe's phase A 21.1k -> 19.2k cycles/step); G = 2 rows and longer rows keep power-of-two chunk counts
+// (2-lane groups: any KCH <= p is already exact; G = 32 / 64: fewer shapes per class kernel)
+constexpr bool exact_kch_shape(int G, int VEC) { return G >= (VEC == 4 ? 2 : 4) && G <= (VEC == 4 ? 8 : 16); }
+
+// Row access of the universe kernels. HBM-typed (global_load / global_store: they count in vmcnt only, so a
+// wait for an LDS read - the batch, the contribution lists - never waits for row traffic in flight, as a flat
+// access would) and branch-free: every chunk of an exact shape but its last is full for every dim the shape
+// takes (pick_universe_shape: D in ((KCH - 1) G VEC, KCH G VEC]), so those chunks load unconditionally; the
+// last (and every chunk of the power-of-two shapes) loads from a clamped in-row address and selects zero past
+// the row's end, instead of an exec-masked branch per chunk. Stores skip only lanes past the end.
+// PT_UNI_GLOBAL=0 keeps the generic (flat, masked) vload / vstore of device.h.
+#ifndef PT_UNI_GLOBAL
+#define PT_UNI_GLOBAL 1
+#endif
+template <int G, int VEC, int KCH>
+constexpr int full_chunks() { return exact_kch_shape(G, VEC) ? KCH - 1 : 0; }
+
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void uload(V<G, VEC, KCH> &o, const float *row_, int D, int lane) {
+#if PT_UNI_GLOBAL
+    const gfloat *row = (const gfloat *)(const void *)row_;
+    constexpr int F = full_chunks<G, VEC, KCH>();
+#pragma unroll
+    for (int k = 0; k < KCH; ++k) {
+        const int c = k * G + lane;
+        const bool ok = k < F || c * VEC < D;
+        const int cc = k < F ? c : (ok ? c : 0);   // chunk 0 is inside every row
+        if constexpr (VEC == 4) {
+            const f32x4 f = *reinterpret_cast<const gf32x4 *>(row + cc * 4);
+            o.x[k * 4 + 0] = ok ? f.x : 0.f; o.x[k * 4 + 1] = ok ? f.y : 0.f;
+            o.x[k * 4 + 2] = ok ? f.z : 0.f; o.x[k * 4 + 3] = ok ? f.w : 0.f;
+        } else {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+                const float v = row[cc * VEC + q];
+                o.x[k * VEC + q] = ok ? v : 0.f;
+            }
+        }
+    }
+#else
+    vload(o, row_, D, lane);
+#endif
+}
+
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void ustore(const V<G, VEC, KCH> &o, float *row_, int D, int lane) {
+#if PT_UNI_GLOBAL
+    gfloat *row = (gfloat *)(void *)row_;
+    constexpr int F = full_chunks<G, VEC, KCH>();
+#pragma unroll
+    for (int k = 0; k < KCH; ++k) {
+        const int c = k * G + lane;
+        if (k < F || c * VEC < D) {
+            if constexpr (VEC == 4) {
+                const f32x4 f = {o.x[k * 4 + 0], o.x[k * 4 + 1], o.x[k * 4 + 2], o.x[k * 4 + 3]};
+                *reinterpret_cast<gf32x4 *>(row + c * 4) = f;
+            } else {
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) row[c * VEC + q] = o.x[k * VEC + q];
+            }
+        }
+    }
+#else
+    vstore(o, row_, D, lane);
+#endif
+}
+
 // Gradient sink of one universe.
 //   contrib != null: entity rows go to contribution slots (plain stores) linked per row in LDS
 //   (head[row] -> c -> next[c] -> ... -> -1); otherwise float atomics into gent.
@@ -111,7 +180,7 @@ struct UniverseSink {
     __device__ __forceinline__ void link(int32_t *h, int row, int table, const V<G, VEC, KCH> &g, int D,
                                          int lane) const {
         const int c = slot++;   // group-uniform: every lane of the group makes the same calls
-        vstore(g, contrib + c * D, D, lane);
+        ustore(g, contrib + c * D, D, lane);
         if (lane == 0) {
             const int32_t prev = atomicExch(h + row, c);
             next[c] = prev;
@@ -167,14 +236,20 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     Vec hh[NP], th[NP], rh[NP];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
-        vload(hh[q], P.ent + hp[q] * D, D, lane);
-        vload(th[q], P.ent + tp[q] * D, D, lane);
-        vload(rh[q], P.rel + rp[q] * D, D, lane);
+        uload(hh[q], P.ent + hp[q] * D, D, lane);
+        uload(th[q], P.ent + tp[q] * D, D, lane);
+        uload(rh[q], P.rel + rp[q] * D, D, lane);
     }
     // long wide rows (16 floats per lane over >= 16 lanes, D > 128): the first negative's row loads
     // with the positive's, the rest one at a time in the loop (measured: C4, D = 200, 129 -> 108 ms; for
     // the short rows of C3 the extra live row costs more than the round trip it hides, 66 -> 74 ms)
     constexpr bool kPrefetch = VEC * KCH >= 16 && G >= 16;   // (for every shape: C3 / C4 / C5 unchanged, r03)
+    // rows of at most 8 floats per lane: the first negative's row loads with the positive's too, and the four
+    // rows are normalized together (vnormalize_rows: their reductions overlap), the positive's and the first
+    // negative's score norms too (vpnorm2) - a round's chain of dependent reductions is then 2 long instead of 5
+    // (with HBM-typed branch-free row loads, uload; the extra live row fits the 1,024-thread budget)
+    constexpr bool kJoint = VEC * KCH <= 6;
+    constexpr bool kPre = kPrefetch || kJoint;
     int e[NP];
     bool tail_side[NP];
     Vec x[NP];
@@ -182,23 +257,38 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     for (int q = 0; q < NP; ++q) {
         e[q] = 0;
         tail_side[q] = false;
-        if (kPrefetch && neg > 0) {
+        if (kPre && neg > 0) {
             get_neg(q, 0, e[q], tail_side[q]);
-            vload(x[q], P.ent + e[q] * D, D, lane);
+            uload(x[q], P.ent + e[q] * D, D, lane);
         }
     }
-    float ps[NP], csum[NP], lsum[NP];
+    float ps[NP], csum[NP], lsum[NP], ns0[NP];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
+        const bool pre = kPre && neg > 0;
         if (nf) {
-            vnormalize<kFm>(hh[q], hh[q]);
-            vnormalize<kFm>(rh[q], rh[q]);
-            vnormalize<kFm>(th[q], th[q]);
+            float nn[4];
+            if (pre) {
+                Vec *const rows[4] = {&hh[q], &rh[q], &th[q], &x[q]};
+                vnormalize_rows<kFm>(rows, nn);
+            } else {
+                Vec *const rows[3] = {&hh[q], &rh[q], &th[q]};
+                float n3[3];
+                vnormalize_rows<kFm>(rows, n3);
+            }
         }
         Vec vpos;
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh[q].x[i] + rh[q].x[i]) - th[q].x[i];
-        ps[q] = vpnorm<kFm>(vpos, p);
+        if (pre) {   // the first negative's v (as in the loop below) and both score norms at once
+#pragma unroll
+            for (int i = 0; i < Vec::N; ++i)
+                x[q].x[i] = tail_side[q] ? (hh[q].x[i] + rh[q].x[i]) - x[q].x[i] : (x[q].x[i] + rh[q].x[i]) - th[q].x[i];
+            vpnorm2<kFm>(vpos, x[q], p, ps[q], ns0[q]);
+        } else {
+            ps[q] = vpnorm<kFm>(vpos, p);
+            ns0[q] = 0.f;
+        }
         csum[q] = lsum[q] = 0.f;
     }
     PT_USTAMP(sk[0].trace, 1);
@@ -212,20 +302,26 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     }
     const float m = P.margin, inv = P.inv_count;
     for (int k = 0; k < neg; ++k) {
-        if (!kPrefetch || k > 0) {
+        if (!kPre || k > 0) {
 #pragma unroll
             for (int q = 0; q < NP; ++q) {
                 get_neg(q, k, e[q], tail_side[q]);
-                vload(x[q], P.ent + e[q] * D, D, lane);
+                uload(x[q], P.ent + e[q] * D, D, lane);
             }
         }
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
-            if (nf) vnormalize<kFm>(x[q], x[q]);
+            float ns;
+            if (kPre && k == 0) {
+                ns = ns0[q];   // normalized, formed and scored with the positive's rows
+            } else {
+                if (nf) vnormalize<kFm>(x[q], x[q]);
 #pragma unroll
-            for (int i = 0; i < Vec::N; ++i)
-                x[q].x[i] = tail_side[q] ? (hh[q].x[i] + rh[q].x[i]) - x[q].x[i] : (x[q].x[i] + rh[q].x[i]) - th[q].x[i];
-            const float ns = vpnorm<kFm>(x[q], p);
+                for (int i = 0; i < Vec::N; ++i)
+                    x[q].x[i] = tail_side[q] ? (hh[q].x[i] + rh[q].x[i]) - x[q].x[i]
+                                             : (x[q].x[i] + rh[q].x[i]) - th[q].x[i];
+                ns = vpnorm<kFm>(x[q], p);
+            }
             PT_USTAMP(sk[0].trace, 2);
             const float a = ps[q] - ns;
             lsum[q] += a > -m ? a : -m;
@@ -295,52 +391,89 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int hp, int rp
     const int p = P.p_norm;
     const bool nf = P.norm_flag != 0;
     Vec H, T, rh, nW, hh, th, vpos;
-    vload(H, P.ent + hp * D, D, lane);
-    vload(T, P.ent + tp * D, D, lane);
-    vload(rh, P.rel + rp * D, D, lane);
-    vload(nW, P.normv + rp * D, D, lane);
+    uload(H, P.ent + hp * D, D, lane);
+    uload(T, P.ent + tp * D, D, lane);
+    uload(rh, P.rel + rp * D, D, lane);
+    uload(nW, P.normv + rp * D, D, lane);
     int e = 0;   // the first negative's row loads with the positive's
     bool tail_side = false;
     Vec X;
     if (neg > 0) {
         get_neg(0, e, tail_side);
-        vload(X, P.ent + e * D, D, lane);
+        uload(X, P.ent + e * D, D, lane);
+    } else {
+        vzero(X);
     }
-    vnormalize<kFm>(nW, nW);
-    const float hdot = vdot(H, nW), tdot = vdot(T, nW);
+    // the forward's reductions grouped (vnormalize_rows / gsum_n / vpnorm2: bit-identical per value, their
+    // dependent chains overlapping): n-hat with r-hat; the dots of H, T and the first negative with n-hat; the
+    // three projected rows' normalizations; the positive's and the first negative's score norms
+    if (nf) {
+        Vec *const r2[2] = {&nW, &rh};
+        float n2[2];
+        vnormalize_rows<kFm>(r2, n2);
+    } else {
+        vnormalize<kFm>(nW, nW);
+    }
+    float dd[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < Vec::N; ++i) {
+        dd[0] += H.x[i] * nW.x[i];
+        dd[1] += T.x[i] * nW.x[i];
+        dd[2] += X.x[i] * nW.x[i];
+    }
+    gsum_n<G, 3>(dd);
+    const float hdot = dd[0], tdot = dd[1], ed0 = dd[2];
+    Vec xs0, xh0, vk0;
 #pragma unroll
     for (int i = 0; i < Vec::N; ++i) {
         hh.x[i] = H.x[i] - hdot * nW.x[i];
         th.x[i] = T.x[i] - tdot * nW.x[i];
+        xs0.x[i] = X.x[i] - ed0 * nW.x[i];
     }
-    float hn = 0.f, tn = 0.f;
+    float hn = 0.f, tn = 0.f, en0 = 0.f;
+    xh0 = xs0;
     if (nf) {
-        hn = vnormalize<kFm>(hh, hh);
-        vnormalize<kFm>(rh, rh);
-        tn = vnormalize<kFm>(th, th);
+        Vec *const r3[3] = {&hh, &th, &xh0};
+        float n3[3];
+        vnormalize_rows<kFm>(r3, n3);
+        hn = n3[0];
+        tn = n3[1];
+        en0 = n3[2];
     }
 #pragma unroll
-    for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
-    const float ps = vpnorm<kFm>(vpos, p);
+    for (int i = 0; i < Vec::N; ++i) {
+        vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
+        vk0.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - xh0.x[i] : (xh0.x[i] + rh.x[i]) - th.x[i];
+    }
+    float ps, ns0;
+    vpnorm2<kFm>(vpos, vk0, p, ps, ns0);
     Vec aH, aT, aR, aW;
     vzero(aH); vzero(aT); vzero(aR); vzero(aW);
     float csum = 0.f, lsum = 0.f;
     const float m = P.margin, inv = P.inv_count;
     for (int k = 0; k < neg; ++k) {
-        if (k > 0) {
-            get_neg(k, e, tail_side);
-            vload(X, P.ent + e * D, D, lane);
-        }
         Vec xs, xh, vk;
-        const float ed = vdot(X, nW);
+        float ed, en, ns;
+        if (k == 0) {   // formed with the positive's rows above
+            xs = xs0;
+            xh = xh0;
+            vk = vk0;
+            ed = ed0;
+            en = en0;
+            ns = ns0;
+        } else {
+            get_neg(k, e, tail_side);
+            uload(X, P.ent + e * D, D, lane);
+            ed = vdot(X, nW);
 #pragma unroll
-        for (int i = 0; i < Vec::N; ++i) xs.x[i] = X.x[i] - ed * nW.x[i];
-        float en = 0.f;
-        if (nf) en = vnormalize<kFm>(xs, xh); else xh = xs;
+            for (int i = 0; i < Vec::N; ++i) xs.x[i] = X.x[i] - ed * nW.x[i];
+            en = 0.f;
+            if (nf) en = vnormalize<kFm>(xs, xh); else xh = xs;
 #pragma unroll
-        for (int i = 0; i < Vec::N; ++i)
-            vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - xh.x[i] : (xh.x[i] + rh.x[i]) - th.x[i];
-        const float ns = vpnorm<kFm>(vk, p);
+            for (int i = 0; i < Vec::N; ++i)
+                vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - xh.x[i] : (xh.x[i] + rh.x[i]) - th.x[i];
+            ns = vpnorm<kFm>(vk, p);
+        }
         const float a = ps - ns;
         lsum += a > -m ? a : -m;
         const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
@@ -624,15 +757,15 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                         const int row = code[u] >> 2;
                         const float *wp = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
                         const float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
-                        vload(x[u], wp, (int)D, lane);
-                        if (opt != 0) vload(a[u], ap, (int)D, lane);
+                        uload(x[u], wp, (int)D, lane);
+                        if (opt != 0) uload(a[u], ap, (int)D, lane);
                         if ((table == 0 && contrib) || (table > 0 && rel_list)) {
                             // the row's contributions (linked in LDS): the first two loads issued with the
                             // row's own, the rest walked below; summed in list order
                             const int32_t c0 = s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row];
-                            vload(gs[u], U.contrib + c0 * D, (int)D, lane);
+                            uload(gs[u], U.contrib + c0 * D, (int)D, lane);
                             c1[u] = s_next[c0];
-                            if (c1[u] >= 0) vload(y[u], U.contrib + c1[u] * D, (int)D, lane);
+                            if (c1[u] >= 0) uload(y[u], U.contrib + c1[u] * D, (int)D, lane);
                         } else {
                             vload(gs[u], (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D,
                                   (int)D, lane);
@@ -645,7 +778,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
 #pragma unroll
                         for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
                         for (int32_t c = s_next[c1[u]]; c >= 0; c = s_next[c]) {
-                            vload(y[u], U.contrib + c * D, (int)D, lane);
+                            uload(y[u], U.contrib + c * D, (int)D, lane);
 #pragma unroll
                             for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
                         }
@@ -661,9 +794,20 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     // ent rows of TransE and every rel / norm_vector row carry normalized-space gradients
                     const bool jac = table == 0 ? (MODEL == 0 && norm_flag) : (table == 1 ? norm_flag != 0 : true);
                     Vec gg;
-                    if (jac) {
-                        const float nx = fsqrt<kFastUpd>(vdot(x[u], x[u]));
-                        unormalize_bwd<kFastUpd>(x[u], nx, gs[u], gg);
+                    if (jac) {   // |x| and x.g reduced together (the values of vdot / unormalize_bwd, bit for bit)
+                        float sd[2] = {0.f, 0.f};
+#pragma unroll
+                        for (int j = 0; j < Vec::N; ++j) {
+                            sd[0] += x[u].x[j] * x[u].x[j];
+                            sd[1] += gs[u].x[j] * x[u].x[j];
+                        }
+                        gsum_n<G, 2>(sd);
+                        const float nx = fsqrt<kFastUpd>(sd[0]);
+                        const bool big = nx > kEps;
+                        const float iv = big ? frcp<kFastUpd>(nx) : 1.0f / kEps;
+                        const float cc = big ? sd[1] * (iv * iv) : 0.f;
+#pragma unroll
+                        for (int j = 0; j < Vec::N; ++j) gg.x[j] = (gs[u].x[j] - x[u].x[j] * cc) * iv;
                     } else {
                         gg = gs[u];
                     }
@@ -679,9 +823,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                             else
                                 x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j] / (sqrtf(a[u].x[j]) + 1e-10f);
                         }
-                        vstore(a[u], ap, (int)D, lane);
+                        ustore(a[u], ap, (int)D, lane);
                     }
-                    vstore(x[u], wp, (int)D, lane);
+                    ustore(x[u], wp, (int)D, lane);
                     if ((table == 0 && contrib) || (table > 0 && rel_list)) {
                         if (lane == 0) s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row] = -1;
                     } else {
@@ -733,14 +877,11 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     X(33, 4, 1, 5) X(34, 4, 1, 6) X(35, 4, 1, 7) X(36, 2, 4, 3) X(37, 4, 4, 3) X(38, 8, 4, 3)           \
     X(39, 4, 1, 3) X(40, 8, 1, 3) X(41, 16, 1, 3)
 
-// shape class (one kernel each): 0 = at most 4 floats per lane, 1 = 8, 2 = 16 (TransE's wide shapes)
-#define PT_UCLASS(V_, K_) ((V_) * (K_) <= 4 ? 0 : ((V_) * (K_) <= 8 ? 1 : 2))
+// shape class (one kernel each) by floats per lane: 0 = at most 4, 1 = 5-6, 2 = 7-8, 3 = 9-16 (TransE's wide
+// shapes). 5-6 and 7-8 are separate kernels so the narrower (C3's longest universes, 65-96 dims over 16 lanes)
+// keep their prefetched negative in registers at 1024 threads (one 5-8 kernel spilled ~600 B per lane there)
+#define PT_UCLASS(V_, K_) ((V_) * (K_) <= 4 ? 0 : ((V_) * (K_) <= 6 ? 1 : ((V_) * (K_) <= 8 ? 2 : 3)))
 
-// Rows of up to 128 floats (16 lanes or fewer) take KCH = ceil(chunks / G) chunks per lane instead of the next
-// power of two: e.g. D = 69 on 16 lanes holds 5 floats per lane, not 8 (C3 48.3 -> 43.3 ms, the longest
-// universe's phase A 21.1k -> 19.2k cycles/step); G = 2 rows and longer rows keep power-of-two chunk counts
-// (2-lane groups: any KCH <= p is already exact; G = 32 / 64: fewer shapes per class kernel)
-constexpr bool exact_kch_shape(int G, int VEC) { return G >= (VEC == 4 ? 2 : 4) && G <= (VEC == 4 ? 8 : 16); }
 // whether pick_universe_shape can return (G, VEC, KCH) for the model (TransE: wide shapes, TransH: narrow):
 // with p chunks per lane, a group of more than 2 and fewer than 64 lanes holds exactly p, the 2-lane group
 // up to p and the 64-lane group p or more. Each class kernel compiles only these shapes (fewer paths, a
@@ -780,8 +921,8 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
         if (u >= n) break;   // every wave of the workgroup reads the same u: the whole group exits
         // the 16-float class reads the descriptor's fields where they are used (fewer live scalars: C4 113 ->
         // 104 ms); the narrower classes keep a register copy (C3 65 vs 68 ms)
-        const UniverseDev Uc = CLS == 2 ? UniverseDev{} : us[u];
-        const UniverseDev &U = CLS == 2 ? us[u] : Uc;
+        const UniverseDev Uc = CLS == 3 ? UniverseDev{} : us[u];
+        const UniverseDev &U = CLS == 3 ? us[u] : Uc;
         switch (U.shape) {
 #define PT_URUN(ID_, G_, V_, K_)                                                                       \
     case ID_:                                                                                          \
@@ -803,7 +944,7 @@ namespace detail {
 template <int MODEL, int WPE, int CLS, int PLAN>
 hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int64_t cus, int p_norm, int norm_flag, int opt,
                     int64_t neg, int bern, int filter, const UniverseLaunch &cfg, hipStream_t st) {
-    constexpr int NT = kUniverseClassThreads[CLS];
+    constexpr int NT = universe_class_threads(MODEL, CLS);
     auto kern = dev::k_universes<MODEL, NT, WPE * NT / 512, CLS, PLAN>;
     if (cfg.lds_bytes > (64 << 10)) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -838,8 +979,11 @@ hipError_t launch_universes_plan(const UniverseDev *d_us, int64_t n, int *counte
     if (cls == 1)
         return model == 0 ? launch_q<0, 2, 1, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
                           : launch_q<1, 2, 1, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
+    if (cls == 2)
+        return model == 0 ? launch_q<0, 2, 2, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
+                          : launch_q<1, 2, 2, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
     if (model == 0)
-        return launch_q<0, 2, 2, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
+        return launch_q<0, 2, 3, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
     return hipErrorInvalidValue;   // TransH universes use the narrow shapes
 }
 extern template hipError_t launch_universes_plan<1>(const UniverseDev *, int64_t, int *, int, int64_t, int, int, int,

@@ -108,8 +108,14 @@ def min_combine(tensors):
     world, _ = _dist()
     if world > 1:
         import torch.distributed as dist
+        host = dist.get_backend() != "nccl"   # gloo reduces host tensors (RCCL reduces in HBM over xGMI)
         for t in tensors:
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            if host and t.is_cuda:
+                h = t.cpu()
+                dist.all_reduce(h, op=dist.ReduceOp.MIN)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return tensors
 
 

@@ -898,15 +898,34 @@ float oracle_train_step_mt(int model, int p, int norm_flag, int opt, float lr, f
     return loss;
 }
 
-/* Test infrastructure for the fast kernels' step tolerance (tests/helpers.py assert_step_close): the step's
- * gradient of every table element - summed in the reference's order (row_update) - and the sum of the
- * magnitudes of its per-slot contributions, without updating anything. kappa = gmass / |gsum| is the element's
- * condition number for the sum: an implementation summing the same contributions in another order may differ
- * from gsum by about n * eps * gmass. Outputs [E + R (+ R for TransH)][d]: entity rows, relation rows,
- * norm_vector rows. Returns the loss. */
+/* Test infrastructure for the fast kernels' step tolerance (tests/helpers.py kappa_bound): at the given tables
+ * and batch, without updating anything, per table element
+ *   gsum  - the step's gradient, summed in the reference's order (row_update);
+ *   gmass - the sum of its per-slot contributions' magnitudes;
+ *   gabs  - the same gradient evaluated with absolute values throughout (|.| of every operand of the forward
+ *           pieces a contribution depends on, the normalize / projection Jacobians with |x| and sums of
+ *           magnitudes): standard forward-error analysis bounds the rounding error of ANY evaluation order of the
+ *           gradient by k * eps * gabs, k the length of the longest chain of operations;
+ * per row
+ *   gcnt  - contributions (slots with a nonzero score gradient touching the row);
+ *   gtie  - 1 when a slot touching the row had a near-tie decision: a margin comparison p - n vs -m, or (p = 1)
+ *           a sign(v_i), within rounding of its threshold. There two correct float32 implementations may take
+ *           different branches (a discrete difference no eps bound covers), so the tests exempt those rows.
+ * Outputs [E + R (+ R for TransH)][d] (entity, relation, norm_vector rows) and [E + R (+ R)]. Returns the loss. */
+static void nb_abs(const float *x, float n, const float *g, float *out, int64_t d) {
+    if (n > 1e-12f) {
+        float c = 0;
+        for (int64_t i = 0; i < d; ++i) c += fabsf(x[i]) * g[i];
+        c /= n * n;
+        for (int64_t i = 0; i < d; ++i) out[i] = (g[i] + fabsf(x[i]) * c) / n;
+    } else {
+        for (int64_t i = 0; i < d; ++i) out[i] = g[i] / 1e-12f;
+    }
+}
+
 float oracle_grad_mass(int model, int p, int norm_flag, float margin, int64_t E, int64_t R, int64_t d, float *ent,
                        float *rel, float *normv, const int64_t *h, const int64_t *t, const int64_t *r, int64_t bs,
-                       int64_t neg, float *gsum, float *gmass) {
+                       int64_t neg, float *gsum, float *gmass, float *gabs, int32_t *gcnt, int32_t *gtie) {
     ostep S;
     memset(&S, 0, sizeof(S));
     S.model = model; S.p = p; S.norm_flag = norm_flag; S.opt = 0; S.lr = 0.f; S.margin = margin;
@@ -915,7 +934,100 @@ float oracle_grad_mass(int model, int p, int norm_flag, float margin, int64_t E,
     S.h = h; S.t = t; S.r = r;
     S.gsum = gsum;
     S.gmass = gmass;
-    const float loss = ostep_run(&S, 1);
+    const float loss = ostep_run(&S, 1);   /* scores, ds, per-slot rows, gsum / gmass */
+    const int64_t seq = S.seq, rows = E + R * (model == 1 ? 2 : 1);
+    const float eps = 5.9604645e-8f;   /* 2^-24 */
+    memset(gabs, 0, sizeof(float) * (size_t)(rows * d));
+    memset(gcnt, 0, sizeof(int32_t) * (size_t)rows);
+    memset(gtie, 0, sizeof(int32_t) * (size_t)rows);
+    float *buf = calloc((size_t)(20 * d), sizeof(float));
+    float *sabs = calloc((size_t)seq, sizeof(float));
+    int8_t *tie = calloc((size_t)seq, 1);
+    slot_ws ws;
+    slot_ws_bind(&ws, buf, d);
+    float *gv = buf + 7 * d, *ga = buf + 8 * d, *gb = buf + 9 * d, *gc = buf + 10 * d, *gw = buf + 11 * d;
+    float *x1 = buf + 12 * d, *x2 = buf + 13 * d, *t1 = buf + 14 * d, *t2 = buf + 15 * d;
+    /* absolute evaluation of every score (the terms of v) and the sign near-ties (p = 1) */
+    for (int64_t s = 0; s < seq; ++s) {
+        slot_forward(model, p, norm_flag, 0, &ws, ent + h[s] * d, ent + t[s] * d, rel + r[s] * d,
+                     model == 1 ? normv + r[s] * d : NULL);
+        float a = 0;
+        for (int64_t i = 0; i < d; ++i) {
+            const float m = fabsf(ws.nh[i]) + fabsf(ws.nr[i]) + fabsf(ws.nt[i]);
+            a += m;
+            if (p == 1 && fabsf(ws.v[i]) <= 2.f * (float)(d + 8) * eps * m) tie[s] = 1;
+        }
+        sabs[s] = a;
+    }
+    /* margin near-ties: p - n within rounding of -m (MarginLoss.py:24-28) */
+    for (int64_t i = 0; i < bs; ++i)
+        for (int64_t k = 0; k < neg; ++k) {
+            const int64_t q = bs + k * bs + i;
+            const float a = S.score[i] - S.score[q];
+            if (fabsf(a + margin) <= 2.f * (float)(d + 16) * eps * (sabs[i] + sabs[q])) tie[i] = tie[q] = 1;
+        }
+    for (int64_t s = 0; s < seq; ++s) {
+        const int64_t rh = h[s], rt = t[s], rr = E + r[s], rw = E + R + r[s];
+        if (tie[s]) {
+            gtie[rh] = gtie[rt] = gtie[rr] = 1;
+            if (model == 1) gtie[rw] = 1;
+        }
+        if (S.ds[s] == 0.0f) continue;
+        const float *he = ent + h[s] * d, *te = ent + t[s] * d, *re = rel + r[s] * d;
+        const float *W = model == 1 ? normv + r[s] * d : NULL;
+        const float sc = slot_forward(model, p, norm_flag, 0, &ws, he, te, re, W);
+        const float ads = fabsf(S.ds[s]);
+        for (int64_t i = 0; i < d; ++i)
+            gv[i] = p == 1 ? ads : (sc == 0.0f ? 0.0f : ads / sc * (fabsf(ws.v[i]) + fabsf(ws.nh[i]) +
+                                                                       fabsf(ws.nr[i]) + fabsf(ws.nt[i])));
+        const float *hsrc = model == 1 ? ws.hp : he, *tsrc = model == 1 ? ws.tp : te;
+        if (norm_flag) {
+            nb_abs(hsrc, ws.hpn, gv, ga, d);
+            nb_abs(re, ws.rn, gv, gb, d);
+            nb_abs(tsrc, ws.tpn, gv, gc, d);
+        } else {
+            memcpy(ga, gv, sizeof(float) * (size_t)d);
+            memcpy(gb, gv, sizeof(float) * (size_t)d);
+            memcpy(gc, gv, sizeof(float) * (size_t)d);
+        }
+        if (model == 1) {   /* the projection's Jacobians (TransH.py:68-76) with magnitudes */
+            float nga = 0, ngc = 0, hd = 0, td = 0;
+            for (int64_t i = 0; i < d; ++i) {
+                nga += fabsf(ws.nw[i]) * ga[i];
+                ngc += fabsf(ws.nw[i]) * gc[i];
+                hd += fabsf(he[i]) * fabsf(ws.nw[i]);
+                td += fabsf(te[i]) * fabsf(ws.nw[i]);
+            }
+            for (int64_t i = 0; i < d; ++i) {
+                t1[i] = hd * ga[i] + nga * fabsf(he[i]);
+                t2[i] = td * gc[i] + ngc * fabsf(te[i]);
+            }
+            nb_abs(W, ws.wn, t1, x1, d);
+            nb_abs(W, ws.wn, t2, x2, d);
+            for (int64_t i = 0; i < d; ++i) {
+                gw[i] = x1[i] + x2[i];
+                ga[i] = ga[i] + fabsf(ws.nw[i]) * nga;
+                gc[i] = gc[i] + fabsf(ws.nw[i]) * ngc;
+            }
+        }
+        float *ah = gabs + rh * d, *at = gabs + rt * d, *ar = gabs + rr * d;
+        for (int64_t i = 0; i < d; ++i) {
+            ah[i] += ga[i];
+            at[i] += gc[i];
+            ar[i] += gb[i];
+        }
+        gcnt[rh] += 1;
+        gcnt[rt] += 1;
+        gcnt[rr] += 1;
+        if (model == 1) {
+            float *aw = gabs + rw * d;
+            for (int64_t i = 0; i < d; ++i) aw[i] += gw[i];
+            gcnt[rw] += 1;
+        }
+    }
+    free(buf);
+    free(sabs);
+    free(tie);
     ostep_release(&S);
     return loss;
 }

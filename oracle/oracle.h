@@ -72,12 +72,13 @@ float oracle_train_step_mt(int model, int p_norm, int norm_flag, int opt, float 
                            float *rel_acc, float *norm_acc, const int64_t *h, const int64_t *t, const int64_t *r,
                            int64_t bs, int64_t neg, int64_t workers);
 
-/* Test infrastructure (tests/helpers.py): the step's gradient of every table element, summed in the
- * reference's order, and the sum of its per-slot contributions' magnitudes (no update). Outputs
- * [E + R (+ R for TransH)][d] (entity, relation, norm_vector rows); returns the loss. */
+/* Test infrastructure (tests/helpers.py kappa_bound): per table element the step's gradient summed in the
+ * reference's order, the sum of its contributions' magnitudes and its absolute-value evaluation; per row the
+ * contribution count and a near-tie flag (no update). Outputs [E + R (+ R for TransH)][d] (entity, relation,
+ * norm_vector rows) and [E + R (+ R)]; returns the loss. */
 float oracle_grad_mass(int model, int p, int norm_flag, float margin, int64_t E, int64_t R, int64_t d, float *ent,
                        float *rel, float *normv, const int64_t *h, const int64_t *t, const int64_t *r, int64_t bs,
-                       int64_t neg, float *gsum, float *gmass);
+                       int64_t neg, float *gsum, float *gmass, float *gabs, int32_t *gcnt, int32_t *gtie);
 
 /* Scores as model.predict(...) computes them; mode 0 normal, 1 head_batch, 2 tail_batch (TransE.py:46-60). */
 void oracle_score(int model, int p_norm, int norm_flag, int mode, int64_t dim, const float *ent, const float *rel,

@@ -61,8 +61,9 @@ def lib():
                                               [ctypes.c_int64] + [f32p] * 2 + [i64p] * 6 + [i64p] * 4 + [f32p])
         L.oracle_metrics_from_ranks.argtypes = [ctypes.c_int64, i64p, i64p, f32p]
         L.oracle_grad_mass.restype = ctypes.c_float
+        i32p = ctypes.POINTER(ctypes.c_int32)
         L.oracle_grad_mass.argtypes = ([ctypes.c_int] * 3 + [ctypes.c_float] + [ctypes.c_int64] * 3 + [f32p] * 3 +
-                                       [i64p] * 3 + [ctypes.c_int64] * 2 + [f32p] * 2)
+                                       [i64p] * 3 + [ctypes.c_int64] * 2 + [f32p] * 3 + [i32p] * 2)
         L.oracle_train_step_mt.restype = ctypes.c_float
         L.oracle_train_step_mt.argtypes = ([ctypes.c_int] * 4 + [ctypes.c_float] * 2 + [ctypes.c_int64] * 3 +
                                            [f32p] * 6 + [i64p] * 3 + [ctypes.c_int64] * 3)
@@ -191,24 +192,30 @@ def train_step(model, p, norm_flag, opt, lr, margin, ent, rel, normv, accs, h, t
 
 
 def grad_mass(model, p, norm_flag, margin, ent, rel, normv, h, t, r, bs, neg):
-    """Test infrastructure (helpers.assert_step_close): the step's gradient of every element of the tables
-    (summed in the reference's order) and the sum of its per-slot contributions' magnitudes, at the given
-    tables, without updating them. Returns ({"ent", "rel", "norm"} -> (gsum, gmass)) arrays of the tables'
-    shapes (the norm entry only for TransH)."""
+    """Test infrastructure (helpers.kappa_bound): at the given tables and batch (nothing updated), per table
+    {"ent", "rel", "norm"} a dict with the step's gradient "g" (summed in the reference's order), the sum of its
+    contributions' magnitudes "mass", its absolute-value evaluation "abs" (the forward-error scale of any
+    evaluation order), per row the contribution count "n" and the near-tie flag "tie" (oracle_grad_mass)."""
     E, D = ent.shape
     R = rel.shape[0]
     rows = E + R * (2 if model == "TransH" else 1)
     gs = np.zeros((rows, D), dtype=np.float32)
     gm = np.zeros((rows, D), dtype=np.float32)
+    ga = np.zeros((rows, D), dtype=np.float32)
+    cnt = np.zeros(rows, dtype=np.int32)
+    tie = np.zeros(rows, dtype=np.int32)
     nv = normv if normv is not None else np.zeros(1, dtype=np.float32)
     h, t, r = (np.ascontiguousarray(x, dtype=np.int64) for x in (h, t, r))
+    i32p = ctypes.POINTER(ctypes.c_int32)
     lib().oracle_grad_mass(MODELS[model], p, int(norm_flag), margin, E, R, D, _p(np.ascontiguousarray(ent), f32p),
                            _p(np.ascontiguousarray(rel), f32p), _p(np.ascontiguousarray(nv), f32p), _p(h, i64p),
-                           _p(t, i64p), _p(r, i64p), bs, neg, _p(gs, f32p), _p(gm, f32p))
-    out = {"ent": (gs[:E], gm[:E]), "rel": (gs[E:E + R], gm[E:E + R])}
+                           _p(t, i64p), _p(r, i64p), bs, neg, _p(gs, f32p), _p(gm, f32p), _p(ga, f32p),
+                           _p(cnt, i32p), _p(tie, i32p))
+    spans = {"ent": slice(0, E), "rel": slice(E, E + R)}
     if model == "TransH":
-        out["norm"] = (gs[E + R:], gm[E + R:])
-    return out
+        spans["norm"] = slice(E + R, rows)
+    return {k: {"g": gs[v], "mass": gm[v], "abs": ga[v], "n": cnt[v], "tie": tie[v].astype(bool)}
+            for k, v in spans.items()}
 
 
 def score(model, p, norm_flag, mode, ent, rel, normv, h, t, r):

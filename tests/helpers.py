@@ -169,62 +169,74 @@ def step_noise(acc_before, acc_oracle, acc_ours, noise2=1e-14):
 
 
 EPS32 = 2.0 ** -24   # float32 unit roundoff
-# Constant of the step tolerance (kappa_bound). Two float32 implementations that sum the same n contributions of
-# an element in different orders differ by at most about (n - 1) * eps * mass (mass = the sum of the contributions'
-# magnitudes: the element's condition number times |sum|); the fast kernels also apply the normalize Jacobian
-# once to a normalized-space sum instead of per contribution (a dot product over the row couples the elements)
-# and use the hardware sqrt / rcp in the update. KAPPA_C covers those factors; calibrated on the GPU suite
-# (tests log the largest ratio they see: PT_KAPPA_LOG).
-KAPPA_C = float(os.environ.get("PT_KAPPA_C", "64"))
 
 
-def kappa_bound(before, want, grad, mass, lr, atol=2e-6, c=None):
-    """Per-element tolerance of one optimizer step: atol + c * eps * kappa * |delta|, where delta = want - before
-    is the oracle's update, kappa = mass / |grad| the condition number of the element's gradient sum
-    (oracle.grad_mass) and |delta| / |grad| the update's sensitivity to its gradient (SGD: lr; Adagrad's
-    lr * g / sqrt(A + g^2) moves by at most that ratio relative to g); where grad is 0, lr."""
-    c = KAPPA_C if c is None else c
-    delta = np.abs(np.asarray(want, dtype=np.float64) - np.asarray(before, dtype=np.float64))
-    g = np.abs(np.asarray(grad, dtype=np.float64))
-    scale = np.where(g > 0, delta / np.where(g > 0, g, 1.0), lr)
-    return atol + c * EPS32 * np.asarray(mass, dtype=np.float64) * scale, EPS32 * np.asarray(mass, np.float64) * scale
+def kappa_bound(before, want, gm, lr, acc_before=None, atol=2e-6):
+    """Per-element tolerance of one optimizer step of the fast kernels against the oracle's.
+
+    gm (oracle.grad_mass at the step's input state) gives per element the gradient g summed in the reference's
+    order and its absolute-value evaluation A (every operand of the contributions, the normalize / projection
+    Jacobians, the sums, with magnitudes): forward-error analysis bounds the rounding error of any evaluation
+    order of g by k * eps * A, k the length of its longest chain of operations - here the row's n contributions,
+    two dot products over the row (normalization forward, Jacobian) and a few elementary operations - so two
+    correct float32 implementations differ by at most 2 * k * eps * A with k = n + 2D + 16. The update passes a
+    gradient difference on with |d delta / d g| <= |delta| / |g| (SGD: exactly lr; Adagrad's lr * g / sqrt(A + g^2)
+    never more), plus its own rounding (a few ulp of delta, the hardware sqrt / rcp included). Returns
+    (bound, unit = eps * A * |d delta / d g|, k)."""
+    want = np.asarray(want, dtype=np.float64)
+    delta = np.abs(want - np.asarray(before, dtype=np.float64))
+    g = np.abs(np.asarray(gm["g"], dtype=np.float64))
+    if acc_before is None:
+        flat = np.full(g.shape, float(lr))
+    else:
+        a0 = np.asarray(acc_before, dtype=np.float64)
+        flat = np.where(a0 > 0, lr / np.sqrt(np.where(a0 > 0, a0, 1.0)), lr)
+    scale = np.where(g > 0, delta / np.where(g > 0, g, 1.0), flat)
+    unit = EPS32 * np.asarray(gm["abs"], dtype=np.float64) * scale
+    k = 2.0 * (np.asarray(gm["n"], dtype=np.float64)[:, None] + 2.0 * want.shape[1] + 16.0)
+    return atol + k * unit + 4.0 * EPS32 * delta, unit, k
 
 
-def _log_kappa(what, ratio):
+def _log_kappa(what, rec):
     path = os.environ.get("PT_KAPPA_LOG")
     if path:
         import json
+        rec = dict(rec, test=os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], what=what)
         with open(path, "a") as f:
-            f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], "what": what,
-                                "max_c": ratio}) + "\n")
+            f.write(json.dumps(rec) + "\n")
 
 
-def assert_step_close(ours, want, atol, mask=None, max_frac=1e-2, what="", before=None, grad=None, mass=None,
-                      lr=None):
-    """One step from the same state: |ours - want| <= kappa_bound(...) elementwise (atol + KAPPA_C * eps * kappa *
-    |delta|: the conditioning of each element's gradient sum, from the oracle) when the oracle's gradient and
-    contribution mass are given, else <= atol; except on the step's noise-decided components (mask: an Adagrad
-    step whose gradient cancelled to rounding level, so its +-lr sign is set by summation order), which must be
-    rare (at most a few, or max_frac of a large table). The largest error relative to eps * kappa * |delta| is
-    logged (PT_KAPPA_LOG) and returned."""
+def assert_step_close(ours, want, atol, mask=None, max_frac=1e-2, what="", before=None, gm=None, lr=None,
+                      acc_before=None):
+    """One step from the same state: |ours - want| <= kappa_bound(...) elementwise when the oracle's gradient
+    analysis gm is given, else <= atol. Exempt, and required rare: the step's noise-decided components (mask: an
+    Adagrad step whose gradient cancelled to rounding level, so its +-lr sign is set by summation order; at most a
+    few, or max_frac of a large table) and the rows a near-tie decision touched (gm["tie"]: a margin comparison
+    or a p = 1 sign(v_i) within rounding of its threshold, where the implementations may branch differently; at
+    most max(8, 2 %) of the rows). Returns the largest error in units of the bound's rounding term (<= 1 when the
+    bound holds) and logs it with the mask counts (PT_KAPPA_LOG)."""
     ours = np.asarray(ours, dtype=np.float64)
     want = np.asarray(want, dtype=np.float64)
     err = np.abs(ours - want)
-    if grad is not None:
-        tol, unit = kappa_bound(before, want, grad, mass, lr, atol)
-    else:
-        tol, unit = np.full(err.shape, atol), None
-    bad = err > tol
+    keep = np.ones(err.shape, dtype=bool)
     if mask is not None:
         assert mask.sum() <= max(4, max_frac * mask.size), "%s: %d noise-decided components" % (what,
                                                                                               int(mask.sum()))
-        bad &= ~mask
-    ratio = 0.0
-    if unit is not None:
-        keep = (unit > 0) & (err > atol) & (~mask if mask is not None else True)
-        ratio = float(((err - atol)[keep] / unit[keep]).max()) if keep.any() else 0.0
-        _log_kappa(what, ratio)
-    assert not bad.any(), "%s: max err %g at %d entries (atol %g, worst err / (eps kappa |delta|) %g)" % (
+        keep &= ~mask
+    ratio, ties = 0.0, 0
+    if gm is not None:
+        tol, unit, k = kappa_bound(before, want, gm, lr, acc_before, atol)
+        ties = int(np.count_nonzero(gm["tie"]))
+        assert ties <= max(8, 0.02 * len(gm["tie"])), "%s: %d rows with near-tie decisions" % (what, ties)
+        keep &= ~gm["tie"][:, None]
+        over = (err - atol - 4.0 * EPS32 * np.abs(want - np.asarray(before, dtype=np.float64))) / (k * unit + 1e-300)
+        ratio = float(over[keep & (unit > 0)].max()) if (keep & (unit > 0)).any() else 0.0
+        _log_kappa(what, {"ratio": ratio, "tie_rows": ties, "noise": int(mask.sum()) if mask is not None else 0,
+                          "max_err": float(err[keep].max()) if keep.any() else 0.0})
+    else:
+        tol = np.full(err.shape, atol)
+    bad = (err > tol) & keep
+    assert not bad.any(), "%s: max err %g at %d entries (atol %g, worst err / bound's rounding term %g)" % (
         what, float(err[bad].max()), int(bad.sum()), atol, ratio)
     return ratio
 

@@ -391,8 +391,7 @@ def test_c1_wn18_steps_match_oracle(bs, data_dir):
                                      neg)
             assert abs(float(loss.item()) - want) <= 1e-5 * max(1.0, abs(want)), (k, float(loss.item()), want)
             for gg, ww, b0, nm in zip(got, (ent, rel), before, ("ent", "rel")):
-                assert_step_close(gg, ww, 2e-6, what="step %d %s" % (k, nm), before=b0, grad=gm[nm][0],
-                                  mass=gm[nm][1], lr=lr)
+                assert_step_close(gg, ww, 2e-6, what="step %d %s" % (k, nm), before=b0, gm=gm[nm], lr=lr)
     finally:
         torch.cuda.synchronize()
         L.pt_trainer_free(tr)

@@ -572,8 +572,9 @@ def test_static_experiment_flow(tmp_path):
 
 # The fast single-model trainer teacher-forced: every step starts from the oracle's state (tables, Adagrad
 # state, sampler streams) and must equal the oracle's step - loss within 1e-5 relative, tables within 2e-6
-# absolute + KAPPA_C * eps * kappa * |update| per element, kappa the condition number of the element's gradient
-# sum from the oracle (helpers.assert_step_close / kappa_bound), except on the components whose
+# absolute + the forward-error bound of the step per element (helpers.kappa_bound: 2 k eps A |d update / d g|, A the
+# oracle's absolute-value evaluation of the element's gradient, k = contributions + 2D + 16), except on the rows a
+# near-tie decision touched (margin or p = 1 sign within rounding) and the components whose
 # Adagrad update was noise-decided in either implementation
 # (helpers.step_noise). Covers the small-neg in-step sampler path and the counting-sort path (neg >= 4)
 # with its split sampler, TransE / TransH, p 1 / 2, SGD / Adagrad, the odd dims. Whole trajectories are
@@ -642,7 +643,7 @@ def test_fast_trainer_steps_teacher_forced(case):
                     continue
                 mask = step_noise(acc0[i], accs[i], got_acc[i]) if ada else None
                 assert_step_close(got[i], w, 2e-6, mask, what="step %d %s" % (k, name), before=tab0[i],
-                                  grad=gm[name][0], mass=gm[name][1], lr=lr)
+                                  gm=gm[name], lr=lr, acc_before=acc0[i])
         # the streams advanced exactly like one sampling() call per step
         nxt = np.zeros(8, dtype=np.uint64)
         _native.check(L.pt_sampler_get_seeds(smp, nxt.ctypes.data))

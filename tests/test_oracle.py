@@ -251,6 +251,10 @@ def test_grad_mass_is_the_step_gradient(model):
     for name, after in (("ent", ent), ("rel", rel), ("norm", nv)):
         if after is None:
             continue
-        g, m = gm[name]
+        x = gm[name]
+        g, m, a = x["g"], x["mass"], x["abs"]
         np.testing.assert_array_equal(after, before[name] + (-1.0) * g)
         assert (m >= np.abs(g) * (1 - 1e-6)).all() and m.max() > 0
+        assert (a >= m * (1 - 1e-5)).all()   # the absolute evaluation bounds the contributions' magnitudes
+        touched = (m > 0).any(axis=1)
+        assert (x["n"][touched] > 0).all() and (x["n"][~touched] == 0).all()

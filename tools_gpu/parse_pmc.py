@@ -8,6 +8,15 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+# the library the passes profiled (the product build of this tree): bench.py uses the counted bytes only when
+# this digest equals the loaded library's
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "openke-putranse_amd", "openke",
+                   "release", "libputranse_hip.so")
+
+
+def lib_sha256():
+    import hashlib
+    return hashlib.sha256(open(LIB, "rb").read()).hexdigest() if os.path.exists(LIB) else None
 vals = defaultdict(lambda: defaultdict(list))
 durs = defaultdict(list)
 for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
@@ -29,6 +38,12 @@ for k, d in vals.items():
     if durs.get(k):
         out[short]["mean_ns_profiled"] = sum(durs[k]) / len(durs[k])
 print(json.dumps(out, indent=1))
+if len(sys.argv) > 2 and sys.argv[2].endswith("_uni.json"):   # universe workloads: per-kernel counters only
+    json.dump({"lib_sha256": lib_sha256(), "per_kernel": out,
+               "method": "rocprofv3 --pmc passes over bench.py --workload (separate passes, --kernel-trace)"},
+              open(sys.argv[2], "w"), indent=1)
+    print("wrote", sys.argv[2])
+    sys.exit(0)
 
 # HBM traffic of one C2 training step for bench.py's roofline.traffic (MI355X_MICROARCH.md §HBM:
 # FETCH_SIZE / WRITE_SIZE are kilobytes; on gfx950 FETCH_SIZE counts half the bytes of wide coalesced
@@ -55,7 +70,7 @@ if len(sys.argv) > 2:
         elif any(s in k for s in samplers) and n and sampled:
             parts[short] = kb(d) / sampled * 1024.0
     if parts:
-        rec = {"bytes_per_step": sum(parts.values()), "bytes_per_step_by_kernel": parts,
+        rec = {"lib_sha256": lib_sha256(), "bytes_per_step": sum(parts.values()), "bytes_per_step_by_kernel": parts,
                "step_dispatches_counted": steps, "sampled_steps": sampled,
                "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py; "
                          "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B: mean per dispatch of the step and apply "

@@ -1,17 +1,15 @@
 #!/bin/bash
-# PMC passes over a short bench run (counters collected in separate passes, --kernel-trace only).
+# PMC passes over the driver-shaped C2 bench run (counters collected in separate passes, --kernel-trace only),
+# summarised into gpurun_out/pmc_c2.json with the profiled library's sha256 (bench.py reads it from profiles/
+# only when the digest matches the library it loaded).
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/pmc
-timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1
-echo "list rc=$?" >> gpurun_out/steps.log
-TAG=${1:-c2}
-EXTRA=${2:-}
+K=${STEPS:-20}; W=${WARMUP:-5}
 i=0
 for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
     i=$((i+1))
-    timeout -k 10 240 rocprofv3 --kernel-trace --pmc $set -d gpurun_out/pmc/p$i -o run --output-format csv -- python3 bench.py --steps ${STEPS:-20} --warmup ${WARMUP:-5} --no-cpu-baseline $EXTRA > gpurun_out/pmc/p$i.log 2>&1
-    rc=$?
-    echo "pmc $i ($set) rc=$rc" >> gpurun_out/steps.log
-    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+    timeout -k 10 240 rocprofv3 --kernel-trace --pmc $set -d gpurun_out/pmc/p$i -o run --output-format csv -- python3 bench.py --steps $K --warmup $W --repeats 1 --deterministic-timing 0 --no-cpu-baseline --no-c3 > gpurun_out/pmc/p$i.log 2>&1 || exit $?
 done
+# sampled steps of that command: warmup W + graph capture K + timed K + the per-kernel timing run K
+python3 tools_gpu/parse_pmc.py gpurun_out/pmc gpurun_out/pmc_c2.json $((W + 3 * K)) > gpurun_out/pmc/summary.txt

@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 T=${TAG:-r04b}
-PT_KAPPA_C=${PT_KAPPA_C:-1e9} PT_KAPPA_LOG=$PWD/gpurun_out/${T}_kappa.jsonl timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/${T}_pytest.log 2>&1 || exit $?
+PT_KAPPA_LOG=$PWD/gpurun_out/${T}_kappa.jsonl timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/${T}_pytest.log 2>&1 || exit $?
 TAG=$T LIBS="${LIBS:-prod nt1024}" WLS="${WLS:-c3 c4 c5}" bash tools_gpu/ab_libs.sh || exit $?
 for w in c3 c4; do
   timeout -k 10 300 python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --deterministic-timing 0 > gpurun_out/${T}_dropin_$w.log 2>&1 || exit $?
