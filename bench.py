@@ -589,6 +589,9 @@ def main():
                     help="universe workloads on one GPU: also time each rank's LPT share of a PLACE_WORLD-way job")
     ap.add_argument("--deterministic-timing", type=int, default=1,
                     help="also time the reference-order (deterministic) mode (1: yes)")
+    ap.add_argument("--step-apply", type=int, default=0,
+                    help="C2 / C1: 1 = the fused step + apply kernel where it applies (opt-in, measured slower), 0 = "
+                         "the step + apply pair (default; pt_trainer_set_step_apply)")
     ap.add_argument("--no-dropin", action="store_true",
                     help="universe workloads: skip the drop-in Parallel_Universe_Config timing")
     args = ap.parse_args()
@@ -644,6 +647,7 @@ def main():
     tr = Trainer(model=ns, data_loader=dl, train_times=0, alpha=lr, use_gpu=True, opt_method=opt)
     tr.run()   # moves the tables to HBM and builds the native trainer; no steps
     L = _native.lib()
+    _native.check(L.pt_trainer_set_step_apply(tr._native, args.step_apply))
     sampler = dl.device_sampler()
     dev = torch.device("cuda", torch.cuda.current_device())
     seq = bs * (1 + neg)
@@ -705,7 +709,9 @@ def main():
                                          _native.stream()))
     # the sampling kernels of the path the library took for this chunking (pt_trainer_last_path)
     spath = L.pt_trainer_last_path(tr._native)
-    step_names = ["k_step_csr", "k_apply_buf"] if spath != _native.PT_PATH_SAMPLED else ["k_step_sampled", "k_apply"]
+    fused_sa = bool(L.pt_trainer_step_apply(tr._native))
+    step_names = (["k_step_apply", "k_loss_calls"] if fused_sa else
+                  ["k_step_csr", "k_apply_buf"] if spath != _native.PT_PATH_SAMPLED else ["k_step_sampled", "k_apply"])
     names = list(_native.PATH_KERNELS.get(spath, ("sampling", "bucket scan"))) + step_names
     per_kernel = {n: float(v) for n, v in zip(names, ms4) if n and v > 0}
     bytes_step = algorithmic_bytes_per_slot(model, opt, dim) * seq
@@ -760,6 +766,7 @@ def main():
                      "per_kernel": kernel_detail,
                      "lib_sha256": library_sha256(), "counters_lib_sha256": pmc_sha,
                      "counters_match_build": pmc is not None,
+                     "step_apply_fused": fused_sa,
                      "contrib_roundtrip_bytes": contrib_rt if spath != _native.PT_PATH_SAMPLED else 0,
                      "contrib_share_of_counted": None if traffic is None or spath == _native.PT_PATH_SAMPLED
                      else contrib_rt / traffic,
@@ -770,7 +777,8 @@ def main():
                              "algorithmic count where repeated rows (%.1f MB entity table, hub entities, the "
                              "positive rows shared by 25 negatives) hit in L2; counted_frac = that traffic over the "
                              "same kernel time vs 8 TB/s. contrib_roundtrip_bytes: the corrupted entities' gradient "
-                             "rows written by the step kernel and read back by the apply pass" %
+                             "rows written by the step kernel and read back by the apply pass (fused step + apply: by each row's last "
+                             "arriving wave, in the same kernel)" %
                              (args.workload, 4e-6 * dl.get_ent_tot() * dim)},
         "loss_last_step": loss_last,
     }

@@ -137,6 +137,15 @@ int pt_trainer_run_timed(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t
  * k_sample_csr + k_scan_counts; PT_PATH_SAMPLED: none (small neg: the step kernel samples). -1 before any. */
 enum { PT_PATH_TWO_PASS = 0, PT_PATH_FUSED = 1, PT_PATH_PART = 2, PT_PATH_SAMPLED = 3 };
 int pt_trainer_last_path(const pt_trainer *t);
+/* The large-neg TransE step as ONE launch that also updates the table rows (step_apply.hip: each row
+ * updated inside the step by the wave delivering its last gradient contribution, same operations and
+ * order as the separate apply pass), for float4 rows of 33-256 chunks (dim 132-1024, dim % 4 == 0);
+ * on = 0 keeps the step + apply pair. Default off (measured slower at C2: DESIGN.md section 4). Results
+ * equal the pair's up to float-atomic order. */
+int pt_trainer_set_step_apply(pt_trainer *t, int32_t on);
+/* whether the last enqueued in-kernel-sampled steps took the fused step + apply (ms4[2] of
+ * pt_trainer_run_timed is then that kernel, ms4[3] the chunks' loss reduction) */
+int pt_trainer_step_apply(const pt_trainer *t);
 /* Sample `calls` consecutive steps into the counting-sort batch layout the large-neg step kernels read,
  * by path `path` (PT_PATH_FUSED / PT_PATH_PART / PT_PATH_TWO_PASS, or -1 = the automatic choice), advance
  * the sampler streams, and copy the batches to HOST arrays (synchronizes): h_pos [calls][bs][3] (h, r, t

@@ -10,8 +10,8 @@
 #include <mutex>
 #include <thread>
 #include <tuple>
-#include <unordered_map>
 #include <queue>
+#include <unordered_map>
 #include <vector>
 
 #include "tuning.h"
@@ -20,6 +20,7 @@
 #include "kernels.h"
 #include "ordered.h"
 #include "rng.h"
+#include "step_apply.h"
 #include "universe.h"
 #include "universes.h"
 
@@ -69,6 +70,11 @@ struct pt_trainer {
     pt::CsrWork csr{};
     int64_t csr_bs = 0, csr_neg = 0, csr_chunk = 0;   // layout the workspace was carved for
     bool csr_fused = false;                             // k_sample_sort plan fits LDS
+    // the fused step + apply (step_apply.hip) for TransE with 33-256 float4 chunks per row: its rows and
+    // arrival words live in the counting-sort workspace (fr.gent == nullptr: not carved for it)
+    pt::FusedRows fr{};
+    bool step_apply_on = false;                         // pt_trainer_set_step_apply (opt-in: measured slower)
+    bool last_step_apply = false;                       // the last enqueued in-kernel-sampled steps took it
     bool csr_part = false;                              // k_sample_part prepared (its LDS limit raised)
     int last_path = -1;                                 // sampling path of the last enqueued chunk (PT_PATH_*)
     int64_t lpart_cap = 0;                             // W.lpart capacity (positives)
@@ -341,16 +347,25 @@ static int choose_path(const pt_trainer *t, int64_t calls, int64_t bs, int64_t n
 // (bs, neg) re-carves it (and drops captured graphs, whose kernels hold the old pointers).
 static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     if (t->csr_block && t->csr_bs == bs && t->csr_neg == neg) return PT_OK;
-    const int64_t E = t->P.ent_total, D = t->P.dim;
+    const int64_t E = t->P.ent_total, R = t->P.rel_total, D = t->P.dim;
     const int64_t cs = (E + 3) & ~int64_t(3), ss = (E + 4) & ~int64_t(3);
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t per_call = 16 * bs + 8 * bs * neg + 4 * cs + 4 * ss + 4 + 1024;
+    // the fused step + apply's extra state: per call the rows' uses and the loss partials; padded gradient
+    // rows and arrival words; contribution rows at the padded stride
+    pt::StepParams Q = t->P;
+    Q.batch_size = bs;
+    Q.neg = neg;
+    const bool sa = pt::step_apply_supported(Q, bs, neg);
+    const int64_t dp = sa ? pt::step_apply_row_stride(D) : D, us = (E + R + 63) & ~int64_t(63);
+    const size_t per_call = 16 * bs + 8 * bs * neg + 4 * cs + 4 * ss + 4 + 1024 + (sa ? 4 * us + 4 * bs : 0);
     int64_t chunk = (int64_t)std::max<size_t>(1, ((size_t)512 << 20) / per_call);
     chunk = std::min(chunk, kCsrChunk);
+    const size_t a_use = sa ? al(4 * us * chunk) : 0, a_lp = sa ? al(4 * bs * chunk) : 0,
+                 a_gent = sa ? al(4 * E * dp) : 0, a_grel = sa ? al(4 * R * dp) : 0, a_arr = sa ? al(8 * (E + R)) : 0;
     const size_t a_pos = al(16 * bs * chunk), a_neg = al(4 * bs * neg * chunk), a_off = a_neg,
                  a_cnt = al(4 * cs * chunk), a_start = al(4 * ss * chunk), a_tick = al(4 * chunk + 4),
-                 a_con = al(4 * bs * neg * D);
-    const size_t need = a_pos + a_neg + a_off + a_cnt + a_start + a_tick + a_con;
+                 a_con = al(4 * bs * neg * dp);
+    const size_t need = a_use + a_lp + a_gent + a_grel + a_arr + a_pos + a_neg + a_off + a_cnt + a_start + a_tick + a_con;
     PT_HIP(hipDeviceSynchronize());   // queued work may still use the old carving
     t->drop_graphs();
     if (need > t->csr_cap) {
@@ -362,6 +377,15 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     }
     PT_HIP(hipMemset(t->csr_block, 0, need));   // bucket counts start at zero; the scan re-zeroes them
     char *b = (char *)t->csr_block;
+    // the per-chunk memset's block (row uses) first, at the allocation's start
+    t->csr.uses = sa ? (int32_t *)b : nullptr; b += a_use;
+    t->csr.use_stride = us;
+    t->csr.rel_base = E;
+    t->csr.lpart = sa ? (float *)b : nullptr; b += a_lp;
+    t->fr.gent = sa ? (float *)b : nullptr; b += a_gent;
+    t->fr.grel = sa ? (float *)b : nullptr; b += a_grel;
+    t->fr.arrive = sa ? (uint64_t *)b : nullptr; b += a_arr;
+    t->fr.dp = (int32_t)dp;
     t->csr.pos = (int4 *)b; b += a_pos;
     t->csr.neg = (int32_t *)b; b += a_neg;
     t->csr.off = (int32_t *)b; b += a_off;
@@ -439,6 +463,7 @@ static int enqueue_sample_chunk(pt_trainer *t, pt_sampler *s, pt::CsrWork &w, in
     const int64_t dpp = 1 + 2 * neg;
     const int path = choose_path(t, calls, bs, neg, forced);
     t->last_path = path;
+    if (w.uses) PT_HIP(hipMemsetAsync(w.uses, 0, 4 * (size_t)(w.use_stride * calls), st));   // counted by the sampler
     w.rank_only = path == PT_PATH_PART;   // the split sampler leaves bucket ranks (the step resolves them)
     if (path == PT_PATH_FUSED) {
         PT_TIMED(0, pt::launch_sample_sort(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls,
@@ -461,6 +486,16 @@ static int enqueue_sample_chunk(pt_trainer *t, pt_sampler *s, pt::CsrWork &w, in
     return PT_OK;
 }
 
+// whether in-kernel-sampled steps of P take the fused step + apply (carved for in ensure_csr)
+static bool step_apply_on(const pt_trainer *t, const pt::StepParams &P) {
+    static const int forced = [] {
+        const char *v = pt_tuning_env("PT_STEP_APPLY");
+        return v ? atoi(v) : -1;
+    }();
+    if (forced == 0) return false;
+    return t->step_apply_on && t->fr.gent && t->csr.uses && pt::step_apply_supported(P, P.batch_size, P.neg);
+}
+
 // Enqueue `steps` in-kernel-sampled steps; step i adds its loss to d_losses[i]. Large neg takes the
 // counting-sort path: one sampling + one scan launch per chunk of up to kCsrChunk steps (the batch
 // stream does not depend on the tables, so it is drawn ahead), then k_step + k_apply per step.
@@ -476,10 +511,23 @@ static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, in
     if (use_csr(neg)) {
         PT_CHECK(t->csr_block, PT_ESTATE, "counting-sort workspace not allocated");
         const int64_t chunk = t->csr_chunk;
+        const bool sa = step_apply_on(t, P);
+        t->last_step_apply = sa;
+        pt::CsrWork w = t->csr;
+        if (!sa) w.uses = nullptr;   // (the sampler counts row uses only for the fused kernel)
         for (int64_t c0 = 0; c0 < steps; c0 += chunk) {
             const int64_t calls = std::min(chunk, steps - c0);
-            int rc = enqueue_sample_chunk(t, s, t->csr, bs, neg, bern, filter, calls, sample_mode(t), st, tm);
+            int rc = enqueue_sample_chunk(t, s, w, bs, neg, bern, filter, calls, sample_mode(t), st, tm);
             if (rc) return rc;
+            t->csr.rank_only = w.rank_only;   // (read by pt_trainer_run_timed's re-timing of the last batch)
+            if (sa) {   // one launch per step, then the chunk's losses
+                for (int64_t j = 0; j < calls; ++j)
+                    PT_TIMED(2, pt::launch_step_apply(P, pt::csr_view(w, j, bs, neg), t->fr, st));
+                if (d_losses)
+                    PT_TIMED(3, pt::launch_loss_calls(w.lpart, bs, calls, P.inv_count, P.margin, d_losses + c0,
+                                                      P.loss_assign, st));
+                continue;
+            }
             for (int64_t j = 0; j < calls; ++j) {
                 const pt::CsrWork v = pt::csr_view(t->csr, j, bs, neg);
                 float *loss = d_losses ? d_losses + c0 + j : nullptr;
@@ -490,6 +538,7 @@ static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, in
         }
     } else {
         t->last_path = PT_PATH_SAMPLED;
+        t->last_step_apply = false;
         for (int64_t i = 0; i < steps; ++i) {
             float *loss = d_losses ? d_losses + i : nullptr;
             PT_TIMED(2, pt::launch_step(P, dg, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr,
@@ -730,7 +779,13 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
     hipEvent_t ev[4] = {tm.pool[0], tm.pool[1], tm.pool[2], tm.pool[3]};
     int erc = PT_OK;
     if (pt::launch_spin(20000, st) != hipSuccess || hipEventRecord(ev[0], st) != hipSuccess) erc = PT_EHIP;
+    // the fused step + apply: loop 1 only (ms4[3] keeps the chunks' loss kernels from the pass above)
+    const bool sa = t->last_step_apply;
     for (int64_t i = 0; i < steps && !erc; ++i) {
+        if (sa) {
+            if (pt::launch_step_apply(P, v, t->fr, st) != hipSuccess) erc = PT_EHIP;
+            continue;
+        }
         if (pt::launch_step(P, dg, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr, nullptr, t->W,
                             nullptr, st, &v) != hipSuccess ||
             pt::launch_apply(P, t->W, nullptr, 0, bs, dpp, nullptr, st, &v) != hipSuccess)
@@ -739,7 +794,7 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
     if (!erc && (hipEventRecord(ev[1], st) != hipSuccess || pt::launch_spin(20000, st) != hipSuccess ||
                  hipEventRecord(ev[2], st) != hipSuccess))
         erc = PT_EHIP;
-    for (int64_t i = 0; i < steps && !erc; ++i) {
+    for (int64_t i = 0; i < steps && !erc && !sa; ++i) {
         if (pt::launch_step(P, dg, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr, nullptr, t->W,
                             nullptr, st, &v) != hipSuccess)
             erc = PT_EHIP;
@@ -759,10 +814,22 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
     float t_sa = 0, t_s = 0;
     PT_HIP(hipEventElapsedTime(&t_sa, ev[0], ev[1]));
     PT_HIP(hipEventElapsedTime(&t_s, ev[2], ev[3]));
-    ms4[2] = t_s / (float)steps;
-    ms4[3] = (t_sa - t_s) / (float)steps;
+    if (sa) {
+        ms4[2] = t_sa / (float)steps;
+    } else {
+        ms4[2] = t_s / (float)steps;
+        ms4[3] = (t_sa - t_s) / (float)steps;
+    }
     return PT_OK;
 }
+
+extern "C" int pt_trainer_set_step_apply(pt_trainer *t, int32_t on) {
+    PT_CHECK(t, PT_EINVAL, "null trainer");
+    t->step_apply_on = on != 0;
+    t->drop_graphs();   // captured epochs hold the previous choice
+    return PT_OK;
+}
+extern "C" int pt_trainer_step_apply(const pt_trainer *t) { return t && t->last_step_apply ? 1 : 0; }
 
 extern "C" int pt_trainer_last_path(const pt_trainer *t) { return t ? t->last_path : -1; }
 

@@ -42,41 +42,6 @@ __device__ __forceinline__ float gsum(float v) {
     return v;
 }
 
-// gsum of N independent values at once: each butterfly stage issues the N values' DPP adds back to back, so one
-// value's DPP hazard wait is the others' issue slots (the same per-value operations and order as gsum: the
-// results are bit-identical)
-template <int G, int N>
-__device__ __forceinline__ void gsum_n(float (&v)[N]) {
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-        if constexpr (G >= 2) v[i] += dpp_f<0xB1>(v[i]);
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-        if constexpr (G >= 4) v[i] += dpp_f<0x4E>(v[i]);
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-        if constexpr (G >= 8) v[i] += dpp_f<0x141>(v[i]);
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-        if constexpr (G >= 16) v[i] += dpp_f<0x140>(v[i]);
-    if constexpr (G >= 32) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            const unsigned x = __float_as_uint(v[i]);
-            const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-            v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-        }
-    }
-    if constexpr (G >= 64) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            const unsigned x = __float_as_uint(v[i]);
-            const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-            v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-        }
-    }
-}
-
 template <int G, int VEC, int KCH>
 struct V {
     static constexpr int N = VEC * KCH;
@@ -336,56 +301,6 @@ __device__ __forceinline__ float vnormalize(const V<G, VEC, KCH> &x, V<G, VEC, K
 #pragma unroll
     for (int i = 0; i < V<G, VEC, KCH>::N; ++i) out.x[i] = x.x[i] * inv;
     return n;
-}
-
-// vnormalize of several rows at once (in place): the sums of squares reduced together (gsum_n), then the
-// square roots and reciprocals - each row's operations and their order are vnormalize's, so the results are
-// bit-identical; the rows' dependent chains overlap. Norms into n.
-template <bool FAST = false, int G, int VEC, int KCH, int M>
-__device__ __forceinline__ void vnormalize_rows(V<G, VEC, KCH> *const (&x)[M], float (&n)[M]) {
-    float s[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-        s[m] = 0.f;
-#pragma unroll
-        for (int i = 0; i < V<G, VEC, KCH>::N; ++i) s[m] += x[m]->x[i] * x[m]->x[i];
-    }
-    gsum_n<G, M>(s);
-    float inv[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-        n[m] = fsqrt<FAST>(s[m]);
-        inv[m] = frcp<FAST>(n[m] > kEps ? n[m] : kEps);
-    }
-#pragma unroll
-    for (int m = 0; m < M; ++m)
-#pragma unroll
-        for (int i = 0; i < V<G, VEC, KCH>::N; ++i) x[m]->x[i] = x[m]->x[i] * inv[m];
-}
-
-// vpnorm of two vectors at once (bit-identical to two vpnorm calls)
-template <bool FAST = false, int G, int VEC, int KCH>
-__device__ __forceinline__ void vpnorm2(const V<G, VEC, KCH> &a, const V<G, VEC, KCH> &b, int p, float &na, float &nb) {
-    float s[2] = {0.f, 0.f};
-    if (p == 1) {
-#pragma unroll
-        for (int i = 0; i < V<G, VEC, KCH>::N; ++i) {
-            s[0] += fabsf(a.x[i]);
-            s[1] += fabsf(b.x[i]);
-        }
-        gsum_n<G, 2>(s);
-        na = s[0];
-        nb = s[1];
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < V<G, VEC, KCH>::N; ++i) {
-        s[0] += a.x[i] * a.x[i];
-        s[1] += b.x[i] * b.x[i];
-    }
-    gsum_n<G, 2>(s);
-    na = fsqrt<FAST>(s[0]);
-    nb = fsqrt<FAST>(s[1]);
 }
 
 // backward of F.normalize at raw x with norm n: (g - x (x.g)/n^2) / n   (clamp_min branch: g / eps)

@@ -48,6 +48,12 @@ struct CsrWork {
     int dbg = 0;                // timing experiments only (PT_PART_DBG; results then wrong): bit 0 no run
                                 // search, bit 1 no stream jump, bit 2 no 64-bit modulo
     int64_t cnt_stride = 0, start_stride = 0;
+    // fused step + apply (step_apply.hip): per call, the positives' uses of every table row - entity rows
+    // [0, E) as h or t, relation rows [rel_base, rel_base + R) - counted by the sampler ([calls][use_stride],
+    // zeroed before each chunk's sampling); per call the positives' loss partials ([calls][bs])
+    int32_t *uses = nullptr;
+    int64_t use_stride = 0, rel_base = 0;
+    float *lpart = nullptr;
 };
 
 inline CsrWork csr_view(const CsrWork &w, int64_t call, int64_t bs, int64_t neg) {
@@ -57,6 +63,8 @@ inline CsrWork csr_view(const CsrWork &w, int64_t call, int64_t bs, int64_t neg)
     v.off = w.off + call * bs * neg;
     v.cnt = w.cnt + call * w.cnt_stride;
     v.start = w.start + call * w.start_stride;
+    if (w.uses) v.uses = w.uses + call * w.use_stride;
+    if (w.lpart) v.lpart = w.lpart + call * bs;
     return v;
 }
 

@@ -91,6 +91,15 @@ __global__ void k_advance(uint64_t *states, int64_t threads, int64_t bs, int64_t
 // place in its corrupted entity's bucket. Thread k == neg of a positive records the positive.
 using pt::CsrWork;
 
+// the fused step + apply's row-use counts (CsrWork::uses): the positive's h and t rows and its relation row
+__device__ __forceinline__ void count_uses(const CsrWork &w, int64_t call, const PosDraw &pd) {
+    if (!w.uses) return;
+    int32_t *u = w.uses + call * w.use_stride;
+    atomicAdd(u + pd.h, 1);
+    atomicAdd(u + pd.t, 1);
+    atomicAdd(u + w.rel_base + pd.r, 1);
+}
+
 __global__ __launch_bounds__(256) void k_sample_csr(DeviceGraph g, const uint64_t *__restrict__ states,
                                                     int64_t threads, int64_t bs, int64_t neg, int bern, int filter,
                                                     int64_t calls, CsrWork w) {
@@ -102,6 +111,7 @@ __global__ __launch_bounds__(256) void k_sample_csr(DeviceGraph g, const uint64_
     const PosDraw pd = draw_positive(g, states, threads, bs, b, 1 + 2 * neg, call);
     if (k == neg) {
         w.pos[call * bs + b] = make_int4((int)pd.h, (int)pd.r, (int)pd.t, 0);
+        count_uses(w, call, pd);
         return;
     }
     int side;
@@ -243,6 +253,7 @@ __global__ __launch_bounds__(1024) void k_sample_sort(DeviceGraph g, const uint6
         }
         *reinterpret_cast<uint64_t *>(q + 10) = pd.s1;
         w.pos[call * bs + b] = make_int4((int)pd.h, (int)pd.r, (int)pd.t, 0);
+        count_uses(w, call, pd);
     }
     __syncthreads();
     const int64_t slots = bs * neg;
@@ -363,6 +374,7 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
         }
         *reinterpret_cast<uint64_t *>(q + 10) = pd.s1;
         w.pos[call * bs + b] = make_int4((int)pd.h, (int)pd.r, (int)pd.t, 0);
+        count_uses(w, call, pd);
     }
     __syncthreads();
     PT_PHASE(1);

@@ -26,7 +26,7 @@ struct UniverseDev {
     int32_t shape;                                  // universe_shape_id(dim)
 };
 
-// workgroup size of each (model, shape class) kernel. TransE's classes below PT_UNI_NT_CLS run 1,024
+// workgroup size of each (model, shape class) kernel. TransE's narrow classes (<= 8 floats per lane) run 1,024
 // threads (16 waves, 4 per SIMD, 128 VGPRs: twice the lane groups, so a step's positives take half the rounds
 // and twice the waves hide each other's latency; measured C3 57.4 -> 52.5 ms, its longest universe 135 -> 100
 // Mcycles); the 16-float class and TransH (whose step keeps more rows live: at 128 VGPRs it spills, C5 37 -> 89
@@ -34,10 +34,7 @@ struct UniverseDev {
 #ifndef PT_UNI_NT
 #define PT_UNI_NT 1024
 #endif
-#ifndef PT_UNI_NT_CLS
-#define PT_UNI_NT_CLS 3
-#endif
-constexpr int universe_class_threads(int model, int cls) { return model == 0 && cls < PT_UNI_NT_CLS ? PT_UNI_NT : 512; }
+constexpr int universe_class_threads(int model, int cls) { return model == 0 && cls < 2 ? PT_UNI_NT : 512; }
 
 // launch configuration of one group of universes (host-chosen for the largest universe of the group)
 struct UniverseLaunch {

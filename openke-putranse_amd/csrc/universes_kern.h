@@ -95,16 +95,23 @@ constexpr bool exact_kch_shape(int G, int VEC) { return G >= (VEC == 4 ? 2 : 4) 
 // takes (pick_universe_shape: D in ((KCH - 1) G VEC, KCH G VEC]), so those chunks load unconditionally; the
 // last (and every chunk of the power-of-two shapes) loads from a clamped in-row address and selects zero past
 // the row's end, instead of an exec-masked branch per chunk. Stores skip only lanes past the end.
-// PT_UNI_GLOBAL=0 keeps the generic (flat, masked) vload / vstore of device.h.
+// Used by the classes of at most 8 floats per lane (same-box A/B, r04: C5 37.2 -> 36.6 ms); the 16-float
+// class keeps the generic (flat, masked) vload / vstore of device.h (C4 105.6 ms flat vs 121 ms typed: its
+// longer branch-free chunk sequences raised its register allocation). PT_UNI_GLOBAL (measurement builds):
+// 0 = flat everywhere, 1 = typed everywhere, 2 = typed up to 8 floats per lane (default).
 #ifndef PT_UNI_GLOBAL
-#define PT_UNI_GLOBAL 1
+#define PT_UNI_GLOBAL 2
 #endif
+constexpr bool uni_global(int floats) { return PT_UNI_GLOBAL == 1 || (PT_UNI_GLOBAL == 2 && floats <= 8); }
 template <int G, int VEC, int KCH>
 constexpr int full_chunks() { return exact_kch_shape(G, VEC) ? KCH - 1 : 0; }
 
 template <int G, int VEC, int KCH>
 __device__ __forceinline__ void uload(V<G, VEC, KCH> &o, const float *row_, int D, int lane) {
-#if PT_UNI_GLOBAL
+    if constexpr (!uni_global(VEC * KCH)) {
+        vload(o, row_, D, lane);
+        return;
+    }
     const gfloat *row = (const gfloat *)(const void *)row_;
     constexpr int F = full_chunks<G, VEC, KCH>();
 #pragma unroll
@@ -124,14 +131,14 @@ __device__ __forceinline__ void uload(V<G, VEC, KCH> &o, const float *row_, int 
             }
         }
     }
-#else
-    vload(o, row_, D, lane);
-#endif
 }
 
 template <int G, int VEC, int KCH>
 __device__ __forceinline__ void ustore(const V<G, VEC, KCH> &o, float *row_, int D, int lane) {
-#if PT_UNI_GLOBAL
+    if constexpr (!uni_global(VEC * KCH)) {
+        vstore(o, row_, D, lane);
+        return;
+    }
     gfloat *row = (gfloat *)(void *)row_;
     constexpr int F = full_chunks<G, VEC, KCH>();
 #pragma unroll
@@ -147,9 +154,6 @@ __device__ __forceinline__ void ustore(const V<G, VEC, KCH> &o, float *row_, int
             }
         }
     }
-#else
-    vstore(o, row_, D, lane);
-#endif
 }
 
 // Gradient sink of one universe.
@@ -243,13 +247,10 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     // long wide rows (16 floats per lane over >= 16 lanes, D > 128): the first negative's row loads
     // with the positive's, the rest one at a time in the loop (measured: C4, D = 200, 129 -> 108 ms; for
     // the short rows of C3 the extra live row costs more than the round trip it hides, 66 -> 74 ms)
-    constexpr bool kPrefetch = VEC * KCH >= 16 && G >= 16;   // (for every shape: C3 / C4 / C5 unchanged, r03)
-    // rows of at most 8 floats per lane: the first negative's row loads with the positive's too, and the four
-    // rows are normalized together (vnormalize_rows: their reductions overlap), the positive's and the first
-    // negative's score norms too (vpnorm2) - a round's chain of dependent reductions is then 2 long instead of 5
-    // (with HBM-typed branch-free row loads, uload; the extra live row fits the 1,024-thread budget)
-    constexpr bool kJoint = VEC * KCH <= 6;
-    constexpr bool kPre = kPrefetch || kJoint;
+    // (for every shape: C3 / C4 / C5 unchanged, r03; measured r04 and removed: also prefetching for the rows
+    // of at most 6 floats per lane with the four rows' normalizations and the two score norms reduced
+    // together (grouped DPP reductions) - C3 53.7 -> 55.5 ms, C5 (TransH counterpart) 36.6 -> 37.5 ms)
+    constexpr bool kPrefetch = VEC * KCH >= 16 && G >= 16;
     int e[NP];
     bool tail_side[NP];
     Vec x[NP];
@@ -257,38 +258,23 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     for (int q = 0; q < NP; ++q) {
         e[q] = 0;
         tail_side[q] = false;
-        if (kPre && neg > 0) {
+        if (kPrefetch && neg > 0) {
             get_neg(q, 0, e[q], tail_side[q]);
             uload(x[q], P.ent + e[q] * D, D, lane);
         }
     }
-    float ps[NP], csum[NP], lsum[NP], ns0[NP];
+    float ps[NP], csum[NP], lsum[NP];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
-        const bool pre = kPre && neg > 0;
         if (nf) {
-            float nn[4];
-            if (pre) {
-                Vec *const rows[4] = {&hh[q], &rh[q], &th[q], &x[q]};
-                vnormalize_rows<kFm>(rows, nn);
-            } else {
-                Vec *const rows[3] = {&hh[q], &rh[q], &th[q]};
-                float n3[3];
-                vnormalize_rows<kFm>(rows, n3);
-            }
+            vnormalize<kFm>(hh[q], hh[q]);
+            vnormalize<kFm>(rh[q], rh[q]);
+            vnormalize<kFm>(th[q], th[q]);
         }
         Vec vpos;
 #pragma unroll
         for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh[q].x[i] + rh[q].x[i]) - th[q].x[i];
-        if (pre) {   // the first negative's v (as in the loop below) and both score norms at once
-#pragma unroll
-            for (int i = 0; i < Vec::N; ++i)
-                x[q].x[i] = tail_side[q] ? (hh[q].x[i] + rh[q].x[i]) - x[q].x[i] : (x[q].x[i] + rh[q].x[i]) - th[q].x[i];
-            vpnorm2<kFm>(vpos, x[q], p, ps[q], ns0[q]);
-        } else {
-            ps[q] = vpnorm<kFm>(vpos, p);
-            ns0[q] = 0.f;
-        }
+        ps[q] = vpnorm<kFm>(vpos, p);
         csum[q] = lsum[q] = 0.f;
     }
     PT_USTAMP(sk[0].trace, 1);
@@ -302,7 +288,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     }
     const float m = P.margin, inv = P.inv_count;
     for (int k = 0; k < neg; ++k) {
-        if (!kPre || k > 0) {
+        if (!kPrefetch || k > 0) {
 #pragma unroll
             for (int q = 0; q < NP; ++q) {
                 get_neg(q, k, e[q], tail_side[q]);
@@ -311,17 +297,11 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
         }
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
-            float ns;
-            if (kPre && k == 0) {
-                ns = ns0[q];   // normalized, formed and scored with the positive's rows
-            } else {
-                if (nf) vnormalize<kFm>(x[q], x[q]);
+            if (nf) vnormalize<kFm>(x[q], x[q]);
 #pragma unroll
-                for (int i = 0; i < Vec::N; ++i)
-                    x[q].x[i] = tail_side[q] ? (hh[q].x[i] + rh[q].x[i]) - x[q].x[i]
-                                             : (x[q].x[i] + rh[q].x[i]) - th[q].x[i];
-                ns = vpnorm<kFm>(x[q], p);
-            }
+            for (int i = 0; i < Vec::N; ++i)
+                x[q].x[i] = tail_side[q] ? (hh[q].x[i] + rh[q].x[i]) - x[q].x[i] : (x[q].x[i] + rh[q].x[i]) - th[q].x[i];
+            const float ns = vpnorm<kFm>(x[q], p);
             PT_USTAMP(sk[0].trace, 2);
             const float a = ps[q] - ns;
             lsum[q] += a > -m ? a : -m;
@@ -401,79 +381,42 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int hp, int rp
     if (neg > 0) {
         get_neg(0, e, tail_side);
         uload(X, P.ent + e * D, D, lane);
-    } else {
-        vzero(X);
     }
-    // the forward's reductions grouped (vnormalize_rows / gsum_n / vpnorm2: bit-identical per value, their
-    // dependent chains overlapping): n-hat with r-hat; the dots of H, T and the first negative with n-hat; the
-    // three projected rows' normalizations; the positive's and the first negative's score norms
-    if (nf) {
-        Vec *const r2[2] = {&nW, &rh};
-        float n2[2];
-        vnormalize_rows<kFm>(r2, n2);
-    } else {
-        vnormalize<kFm>(nW, nW);
-    }
-    float dd[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < Vec::N; ++i) {
-        dd[0] += H.x[i] * nW.x[i];
-        dd[1] += T.x[i] * nW.x[i];
-        dd[2] += X.x[i] * nW.x[i];
-    }
-    gsum_n<G, 3>(dd);
-    const float hdot = dd[0], tdot = dd[1], ed0 = dd[2];
-    Vec xs0, xh0, vk0;
+    vnormalize<kFm>(nW, nW);
+    const float hdot = vdot(H, nW), tdot = vdot(T, nW);
 #pragma unroll
     for (int i = 0; i < Vec::N; ++i) {
         hh.x[i] = H.x[i] - hdot * nW.x[i];
         th.x[i] = T.x[i] - tdot * nW.x[i];
-        xs0.x[i] = X.x[i] - ed0 * nW.x[i];
     }
-    float hn = 0.f, tn = 0.f, en0 = 0.f;
-    xh0 = xs0;
+    float hn = 0.f, tn = 0.f;
     if (nf) {
-        Vec *const r3[3] = {&hh, &th, &xh0};
-        float n3[3];
-        vnormalize_rows<kFm>(r3, n3);
-        hn = n3[0];
-        tn = n3[1];
-        en0 = n3[2];
+        hn = vnormalize<kFm>(hh, hh);
+        vnormalize<kFm>(rh, rh);
+        tn = vnormalize<kFm>(th, th);
     }
 #pragma unroll
-    for (int i = 0; i < Vec::N; ++i) {
-        vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
-        vk0.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - xh0.x[i] : (xh0.x[i] + rh.x[i]) - th.x[i];
-    }
-    float ps, ns0;
-    vpnorm2<kFm>(vpos, vk0, p, ps, ns0);
+    for (int i = 0; i < Vec::N; ++i) vpos.x[i] = (hh.x[i] + rh.x[i]) - th.x[i];
+    const float ps = vpnorm<kFm>(vpos, p);
     Vec aH, aT, aR, aW;
     vzero(aH); vzero(aT); vzero(aR); vzero(aW);
     float csum = 0.f, lsum = 0.f;
     const float m = P.margin, inv = P.inv_count;
     for (int k = 0; k < neg; ++k) {
-        Vec xs, xh, vk;
-        float ed, en, ns;
-        if (k == 0) {   // formed with the positive's rows above
-            xs = xs0;
-            xh = xh0;
-            vk = vk0;
-            ed = ed0;
-            en = en0;
-            ns = ns0;
-        } else {
+        if (k > 0) {
             get_neg(k, e, tail_side);
             uload(X, P.ent + e * D, D, lane);
-            ed = vdot(X, nW);
-#pragma unroll
-            for (int i = 0; i < Vec::N; ++i) xs.x[i] = X.x[i] - ed * nW.x[i];
-            en = 0.f;
-            if (nf) en = vnormalize<kFm>(xs, xh); else xh = xs;
-#pragma unroll
-            for (int i = 0; i < Vec::N; ++i)
-                vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - xh.x[i] : (xh.x[i] + rh.x[i]) - th.x[i];
-            ns = vpnorm<kFm>(vk, p);
         }
+        Vec xs, xh, vk;
+        const float ed = vdot(X, nW);
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i) xs.x[i] = X.x[i] - ed * nW.x[i];
+        float en = 0.f;
+        if (nf) en = vnormalize<kFm>(xs, xh); else xh = xs;
+#pragma unroll
+        for (int i = 0; i < Vec::N; ++i)
+            vk.x[i] = tail_side ? (hh.x[i] + rh.x[i]) - xh.x[i] : (xh.x[i] + rh.x[i]) - th.x[i];
+        const float ns = vpnorm<kFm>(vk, p);
         const float a = ps - ns;
         lsum += a > -m ? a : -m;
         const float c = a > -m ? inv : (a == -m ? inv * 0.5f : 0.f);
@@ -794,20 +737,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     // ent rows of TransE and every rel / norm_vector row carry normalized-space gradients
                     const bool jac = table == 0 ? (MODEL == 0 && norm_flag) : (table == 1 ? norm_flag != 0 : true);
                     Vec gg;
-                    if (jac) {   // |x| and x.g reduced together (the values of vdot / unormalize_bwd, bit for bit)
-                        float sd[2] = {0.f, 0.f};
-#pragma unroll
-                        for (int j = 0; j < Vec::N; ++j) {
-                            sd[0] += x[u].x[j] * x[u].x[j];
-                            sd[1] += gs[u].x[j] * x[u].x[j];
-                        }
-                        gsum_n<G, 2>(sd);
-                        const float nx = fsqrt<kFastUpd>(sd[0]);
-                        const bool big = nx > kEps;
-                        const float iv = big ? frcp<kFastUpd>(nx) : 1.0f / kEps;
-                        const float cc = big ? sd[1] * (iv * iv) : 0.f;
-#pragma unroll
-                        for (int j = 0; j < Vec::N; ++j) gg.x[j] = (gs[u].x[j] - x[u].x[j] * cc) * iv;
+                    if (jac) {
+                        const float nx = fsqrt<kFastUpd>(vdot(x[u], x[u]));
+                        unormalize_bwd<kFastUpd>(x[u], nx, gs[u], gg);
                     } else {
                         gg = gs[u];
                     }
@@ -877,10 +809,10 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     X(33, 4, 1, 5) X(34, 4, 1, 6) X(35, 4, 1, 7) X(36, 2, 4, 3) X(37, 4, 4, 3) X(38, 8, 4, 3)           \
     X(39, 4, 1, 3) X(40, 8, 1, 3) X(41, 16, 1, 3)
 
-// shape class (one kernel each) by floats per lane: 0 = at most 4, 1 = 5-6, 2 = 7-8, 3 = 9-16 (TransE's wide
-// shapes). 5-6 and 7-8 are separate kernels so the narrower (C3's longest universes, 65-96 dims over 16 lanes)
-// keep their prefetched negative in registers at 1024 threads (one 5-8 kernel spilled ~600 B per lane there)
-#define PT_UCLASS(V_, K_) ((V_) * (K_) <= 4 ? 0 : ((V_) * (K_) <= 6 ? 1 : ((V_) * (K_) <= 8 ? 2 : 3)))
+// shape class (one kernel each): 0 = at most 4 floats per lane, 1 = 8, 2 = 16 (TransE's wide shapes). (Measured
+// r04 and removed: splitting class 1 into 5-6 and 7-8 floats, so the 5-6 kernel - C3's longest universes, 65-96
+// dims over 16 lanes - fits 1,024 threads without spilling: C3 52.3 -> 52.8 ms, the fourth launch costs more.)
+#define PT_UCLASS(V_, K_) ((V_) * (K_) <= 4 ? 0 : ((V_) * (K_) <= 8 ? 1 : 2))
 
 // whether pick_universe_shape can return (G, VEC, KCH) for the model (TransE: wide shapes, TransH: narrow):
 // with p chunks per lane, a group of more than 2 and fewer than 64 lanes holds exactly p, the 2-lane group
@@ -921,8 +853,8 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
         if (u >= n) break;   // every wave of the workgroup reads the same u: the whole group exits
         // the 16-float class reads the descriptor's fields where they are used (fewer live scalars: C4 113 ->
         // 104 ms); the narrower classes keep a register copy (C3 65 vs 68 ms)
-        const UniverseDev Uc = CLS == 3 ? UniverseDev{} : us[u];
-        const UniverseDev &U = CLS == 3 ? us[u] : Uc;
+        const UniverseDev Uc = CLS == 2 ? UniverseDev{} : us[u];
+        const UniverseDev &U = CLS == 2 ? us[u] : Uc;
         switch (U.shape) {
 #define PT_URUN(ID_, G_, V_, K_)                                                                       \
     case ID_:                                                                                          \
@@ -979,11 +911,8 @@ hipError_t launch_universes_plan(const UniverseDev *d_us, int64_t n, int *counte
     if (cls == 1)
         return model == 0 ? launch_q<0, 2, 1, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
                           : launch_q<1, 2, 1, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
-    if (cls == 2)
-        return model == 0 ? launch_q<0, 2, 2, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
-                          : launch_q<1, 2, 2, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
     if (model == 0)
-        return launch_q<0, 2, 3, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
+        return launch_q<0, 2, 2, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
     return hipErrorInvalidValue;   // TransH universes use the narrow shapes
 }
 extern template hipError_t launch_universes_plan<1>(const UniverseDev *, int64_t, int *, int, int64_t, int, int, int,

@@ -25,10 +25,12 @@ re-organised for the GPU:
 """
 import ctypes
 import os
+import pickle
 import random
+import threading
 import time
 from collections import defaultdict
-from copy import deepcopy
+from copy import copy, deepcopy
 from random import randrange, uniform, seed
 
 import numpy as np
@@ -229,10 +231,25 @@ class _KeyStore(object):
         self.rows = torch.full((max(n, 1), max(ent_tot, 1)), float("inf"), dtype=torch.float32, device=device)
         self.tuple = torch.full((max(n, 1),), float("inf"), dtype=torch.float32, device=device)
         self.folded = 0   # universes [0, folded) are MIN-ed into the rows
+        self.rank_inputs = {}   # (known-set handle, side) -> the split's device ranking inputs (_ranks)
 
     def row(self, side, anchor, rel):
         idx = self.keys.get((side, int(anchor), int(rel)))
         return None if idx is None else idx
+
+
+class _Pickled(object):
+    """A checkpoint container serialized with the plain C pickler when wrapped (a snapshot: later changes
+    to the container are not in it) and restored as the container itself on load. torch.save's pickler
+    calls its persistent-id hook once per object, ~1 s for C3's id maps alone (768k entries); the C
+    pickler takes 0.02-0.09 s. The file's layout is unchanged: torch.load returns the plain dicts."""
+    __slots__ = ("data",)
+
+    def __init__(self, obj):
+        self.data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+
+    def __reduce__(self):
+        return (pickle.loads, (self.data,))
 
 
 def universe_dim(dim_param, uid):
@@ -699,7 +716,7 @@ class Parallel_Universe_Config(Tester):
                 print('Save model at universe %d.' % self.next_universe_id)
                 t0 = time.perf_counter()
                 self.save_model("Best_model_Pu{}_{}.ckpt".format(self.embedding_model.__name__,
-                                                                 self.training_identifier))
+                                                                 self.training_identifier), background=True)
                 if tm is not None:
                     tm["checkpoints"] = tm.get("checkpoints", 0) + 1
                     tm["checkpoint_s"] = tm.get("checkpoint_s", 0.0) + time.perf_counter() - t0
@@ -731,6 +748,7 @@ class Parallel_Universe_Config(Tester):
                 training_duration += time.time() - t0
                 if self._after_universe(universe_id):
                     break
+            self.flush_checkpoint()
             print('Time took for creation of embedding spaces: {:5.3f}s'.format(training_duration), end='\n')
             return
         done = 0
@@ -763,6 +781,9 @@ class Parallel_Universe_Config(Tester):
                     break
                 done += 1
                 timing["universes"] += 1
+        t0 = time.time()
+        self.flush_checkpoint()
+        timing["checkpoint_flush_s"] = time.time() - t0
         print('Time took for creation of embedding spaces: {:5.3f}s'.format(training_duration), end='\n')
 
     def wave_size(self):
@@ -869,18 +890,23 @@ class Parallel_Universe_Config(Tester):
         dev = st.rows.device
         n = len(st.h)
         out = []
+        r = np.ascontiguousarray(st.r, dtype=np.int64)
         for side, anchor, truth in ((0, st.t, st.h), (1, st.h, st.t)):
-            off = np.zeros(n + 1, dtype=np.int64)
-            a = np.ascontiguousarray(anchor, dtype=np.int64)
-            r = np.ascontiguousarray(st.r, dtype=np.int64)
-            _native.check(L.pt_known_partners(known, side, n, a.ctypes.data, r.ctypes.data, off.ctypes.data, None))
-            part = np.zeros(max(int(off[-1]), 1), dtype=np.int64)
-            _native.check(L.pt_known_partners(known, side, n, a.ctypes.data, r.ctypes.data, off.ctypes.data,
-                                              part.ctypes.data))
-            d_row = torch.from_numpy(st.q_row[side]).to(dev)
-            d_truth = torch.from_numpy(np.ascontiguousarray(truth, dtype=np.int64)).to(dev)
-            d_off = torch.from_numpy(off).to(dev)
-            d_part = torch.from_numpy(part).to(dev)
+            # the split's queries, truths and known-partner lists do not change between validations: built
+            # and uploaded once per (known set, side)
+            ck = (int(known), side)
+            if ck not in st.rank_inputs:
+                off = np.zeros(n + 1, dtype=np.int64)
+                a = np.ascontiguousarray(anchor, dtype=np.int64)
+                _native.check(L.pt_known_partners(known, side, n, a.ctypes.data, r.ctypes.data, off.ctypes.data,
+                                                  None))
+                part = np.zeros(max(int(off[-1]), 1), dtype=np.int64)
+                _native.check(L.pt_known_partners(known, side, n, a.ctypes.data, r.ctypes.data, off.ctypes.data,
+                                                  part.ctypes.data))
+                st.rank_inputs[ck] = (torch.from_numpy(st.q_row[side]).to(dev),
+                                      torch.from_numpy(np.ascontiguousarray(truth, dtype=np.int64)).to(dev),
+                                      torch.from_numpy(off).to(dev), torch.from_numpy(part).to(dev))
+            d_row, d_truth, d_off, d_part = st.rank_inputs[ck]
             d_repl = st.tuple[d_row].contiguous() if self.missing_embedding_handling == 'null_vector' else None
             raw = torch.zeros(n, dtype=torch.int64, device=dev)
             filt = torch.zeros(n, dtype=torch.int64, device=dev)
@@ -1198,13 +1224,13 @@ class Parallel_Universe_Config(Tester):
         return best
 
     # ------------------------------------------------------------------ state / checkpoints -----
-    def save_model(self, filename=None):
+    def save_model(self, filename=None, background=False):
         save_directory = self.checkpoint_dir
         if not filename:
             filename = "Pu{}_learned_spaces-{}_{}.ckpt".format(self.embedding_model.__name__,
                                                                self.next_universe_id, self.training_identifier)
         os.makedirs(save_directory, exist_ok=True)
-        self.save_parameters(os.path.join("{}{}".format(save_directory, filename)))
+        self.save_parameters(os.path.join("{}{}".format(save_directory, filename)), background=background)
 
     def save_best_state(self):
         self.best_state = self.get_state()
@@ -1331,25 +1357,62 @@ class Parallel_Universe_Config(Tester):
             raise RuntimeError("universes %s are held by no rank" % missing[:8])
         return spaces
 
-    def save_parameters(self, path):
+    def _checkpoint_state(self):
+        """extend_state_dict() as written: the id maps and occurrence sets pre-pickled (_Pickled), the
+        universe dict shallow-copied - a snapshot of this moment (trained universes are not modified later)."""
+        state = dict(self.extend_state_dict())
+        state['trained_embedding_spaces'] = copy(self.trained_embedding_spaces)
+        for k in ('entity_id_mappings', 'relation_id_mappings', 'entity_universes', 'relation_universes'):
+            state[k] = _Pickled(state[k])
+        return state
+
+    def save_parameters(self, path, background=False):
         """One checkpoint file of the whole model, the reference's layout (:890-899). With several ranks
-        every universe is gathered to rank 0, which alone writes; all ranks leave after the file exists."""
+        every universe is gathered to rank 0, which alone writes; all ranks leave after the file exists.
+        background=True (the training loop's best-model saves, one rank, static setting): the state is
+        snapshotted here and the file written by a writer thread while training continues; the next save,
+        load_parameters and the end of train_parallel_universes wait for it (flush_checkpoint)."""
+        self.flush_checkpoint()
         world, rank = _dist()
         if world == 1:
-            torch.save(self.extend_state_dict(), path)
+            state = self._checkpoint_state()
+            if not (background and self.training_setting == "static"):
+                torch.save(state, path)
+                return
+            err = []
+
+            def write():
+                try:
+                    torch.save(state, path)
+                except BaseException as e:   # re-raised by flush_checkpoint on the caller's thread
+                    err.append(e)
+            th = threading.Thread(target=write, name="universe-checkpoint")
+            th.start()
+            self._ckpt_writer = (th, err)
             return
         import torch.distributed as dist
         spaces = self._gather_spaces()
         if rank == 0:
-            state = dict(self.extend_state_dict())
+            state = self._checkpoint_state()
             state['trained_embedding_spaces'] = spaces
             torch.save(state, path)
         dist.barrier()
+
+    def flush_checkpoint(self):
+        """Wait for a background checkpoint write (save_parameters(background=True)); re-raise its error."""
+        w = getattr(self, "_ckpt_writer", None)
+        if w is None:
+            return
+        self._ckpt_writer = None
+        w[0].join()
+        if w[1]:
+            raise w[1][0]
 
     def load_parameters(self, filename):
         """Load a save_parameters checkpoint (from any world size) and re-shard it over this job's ranks:
         the universes are placed by LPT on their evaluation cost (entities x dim) and each rank keeps
         only its own, moved to its GPU when there is one; the id maps stay complete on every rank."""
+        self.flush_checkpoint()
         # checkpoints written by save_parameters (models + python containers): a full unpickle of a
         # file this code wrote
         state_dict = torch.load(self.checkpoint_dir + filename, weights_only=False, map_location="cpu")

@@ -374,6 +374,8 @@ CSR_CASES = [
     ("TransE", 64, 2, True, "sgd", 24, 150),
     ("TransE", 18, 2, True, "sgd", 50, 8),
     ("TransH", 24, 2, True, "adagrad", 40, 6),
+    ("TransE", 136, 2, False, "sgd", 60, 7),     # fused step + apply with one wave per positive
+    ("TransE", 200, 1, True, "sgd", 6, 300),     # fused step + apply, two record windows per wave
 ]
 
 
@@ -414,6 +416,49 @@ def test_counting_sort_step_matches_oracle(case):
     orc = {"ent": ent, "rel": rel, "norm": nv}
     for k, v in got.items():
         assert_tables_close(v, orc[k], 2e-5, ill.get(k) if opt == "adagrad" else None)
+
+
+# The fused step + apply (step_apply.hip: each table row updated inside the step kernel by the wave whose
+# gradient contribution arrives last, pt_trainer_set_step_apply) against the step + apply pair on the same
+# batches and initial tables: the same operations in the same order per row, so the two differ only by the
+# order of the positives' float atomics - per-step losses within 1e-5 relative, tables within 1e-5 absolute
+# after 12 steps. Shapes: one float4 chunk per lane (D = 200), two (D = 300, Adagrad, p = 1), one wave per
+# positive (neg 7, no normalization), two record windows per wave (neg 300).
+SA_CASES = [
+    # dim, p, norm_flag, opt, bs, neg
+    (200, 2, True, "sgd", 128, 25),
+    (300, 1, True, "adagrad", 40, 30),
+    (136, 2, False, "sgd", 60, 7),
+    (200, 1, True, "sgd", 6, 300),
+]
+
+
+@pytest.mark.parametrize("case", SA_CASES, ids=lambda c: "d%d-p%d-nf%d-%s-bs%d-neg%d" % c)
+def test_step_apply_matches_step_and_apply_pair(case):
+    from openke import _native
+    from openke.config import Trainer
+    from openke.module.loss import MarginLoss
+    from openke.module.model import TransE
+    from openke.module.strategy import NegativeSampling
+    dim, p, nf, opt, bs, neg = case
+    steps, lr, margin, seed = 12, (0.5 if opt == "sgd" else 0.1), 4.0, 11
+    runs = {}
+    for fused in (1, 0):
+        dl = _loader_path(KG_SMALL, 8, bs, neg, 1, 1, seed)
+        dl.nbatches = steps
+        torch.manual_seed(dim + neg)
+        kge = TransE(dl.get_ent_tot(), dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=nf)
+        ns = NegativeSampling(model=kge, loss=MarginLoss(margin=margin), batch_size=bs)
+        tr = Trainer(model=ns, data_loader=dl, train_times=1, alpha=lr, use_gpu=True, opt_method=opt)
+        tr._setup()
+        _native.check(_native.lib().pt_trainer_set_step_apply(tr._native, fused))
+        tr.run()
+        assert _native.lib().pt_trainer_step_apply(tr._native) == fused
+        runs[fused] = (tr.last_epoch_loss, _tables(kge))
+    (l1, t1), (l0, t0) = runs[1], runs[0]
+    np.testing.assert_allclose(l1, l0, rtol=1e-5)
+    for k in t1:
+        np.testing.assert_allclose(t1[k], t0[k], atol=1e-5, rtol=0)
 
 
 @pytest.mark.parametrize("path", golden("tc_*.npz"), ids=lambda p: p.split("/")[-1])

@@ -96,3 +96,33 @@ def test_universe_dim_range():
     dims = [universe_dim((20, 100), u) for u in range(200)]
     assert min(dims) >= 20 and max(dims) <= 100 and len(set(dims)) > 30
     assert dims[:3] == [int(np.random.default_rng(1000 + u).integers(20, 101)) for u in range(3)]
+
+
+def test_checkpoint_layout_and_background_write(tmp_path):
+    """save_parameters writes the reference's layout (Parallel_Universe_Config.py:890-899: plain dicts of the
+    id maps and occurrence sets after torch.load) with the containers pre-pickled; a background write is a
+    snapshot of the moment it was asked for (a universe registered afterwards is not in it) and completes at
+    flush_checkpoint."""
+    rng = np.random.default_rng(9)
+    cfg = _config(checkpoint_dir=str(tmp_path) + "/")
+    for uid in range(12):
+        cfg._register_maps(uid, rng.choice(400, 50, replace=False), rng.choice(9, 4, replace=False))
+        cfg.trained_embedding_spaces[uid] = TransE.seeded(uid, 50, 4, dim=8, p_norm=1, norm_flag=True)
+    cfg.next_universe_id = 12
+    want = {k: v for k, v in cfg.get_state().items()}
+    cfg.save_model("bg.ckpt", background=True)
+    cfg._register_maps(12, np.array([3, 4]), np.array([1]))   # after the snapshot
+    cfg.flush_checkpoint()
+    cfg.save_model("fg.ckpt")
+    a = torch.load(str(tmp_path / "bg.ckpt"), weights_only=False)
+    b = torch.load(str(tmp_path / "fg.ckpt"), weights_only=False)
+    for k in ("entity_id_mappings", "relation_id_mappings", "entity_universes", "relation_universes"):
+        assert type(a[k]) is type(want[k]), k
+        assert {u: (dict(m) if isinstance(m, dict) else m) for u, m in a[k].items()} == \
+            {u: (dict(m) if isinstance(m, dict) else m) for u, m in want[k].items()}, k
+    assert 12 not in a["entity_id_mappings"] and 12 in b["entity_id_mappings"]
+    assert a["next_universe_id"] == 12 and sorted(a["trained_embedding_spaces"]) == list(range(12))
+    for u in range(12):
+        sa, sw = a["trained_embedding_spaces"][u].state_dict(), cfg.trained_embedding_spaces[u].state_dict()
+        for k in sw:
+            assert torch.equal(sa[k], sw[k])

@@ -53,8 +53,9 @@ if len(sys.argv) > 2 and sys.argv[2].endswith("_uni.json"):   # universe workloa
 # warmup, graph capture run, timed run, measurement run; the isolation re-timing loops sample nothing).
 if len(sys.argv) > 2:
     sampled = float(sys.argv[3]) if len(sys.argv) > 3 else None
-    samplers = ("k_sample_csr", "k_scan_counts", "k_sample_sort", "k_advance", "k_sample_part")
-    per_step = ("k_step_csr", "k_step_sampled", "k_apply")
+    # (per chunk of sampled steps: the samplers and the fused path's chunk loss reduction)
+    samplers = ("k_sample_csr", "k_scan_counts", "k_sample_sort", "k_advance", "k_sample_part", "k_loss_calls")
+    per_step = ("k_step_csr", "k_step_sampled", "k_step_apply", "k_apply")
     def kb(d):
         return 2.0 * sum(d.get("FETCH_SIZE", [])) + sum(d.get("WRITE_SIZE", []))
     total = 0.0
