@@ -285,8 +285,17 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
     if prof_on:
         prof = np.zeros(64 * max(len(jobs), 1), dtype=np.uint64)
         _native.check(L.pt_universe_set_profile(uset, prof.ctypes.data))
-        prof = prof.reshape(-1, 64).astype(np.float64)
+        prof = prof.reshape(-1, 64)
+        # the set's schedule: each universe's start (100 MHz wall clock, low 32 bits) and duration, in ms
+        w_start = (prof[:, 7] >> np.uint64(32)).astype(np.int64)
+        w_start = ((w_start - w_start.min()) % (1 << 32)).astype(np.float64) * 1e-5
+        w_dur = (prof[:, 7] & np.uint64(0xffffffff)).astype(np.float64) * 1e-5
+        prof = prof.astype(np.float64)
         span = prof[:, :3].sum(axis=1)
+        il = int(np.argmax(span))
+        print("universe-prof schedule: last end %.2f ms after the first start; the longest universe starts at %.2f ms "
+              "and runs %.2f ms; universes starting after 1 ms: %d" % ((w_start + w_dur).max(), w_start[il], w_dur[il],
+                                                                       int((w_start > 1.0).sum())), file=sys.stderr)
         longest = float(span.max())
         for i in np.argsort(-span)[:6]:   # the longest universes (cycles of the last run)
             steps = max(prof[i, 3], 1)
@@ -296,7 +305,8 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
         if os.environ.get("PT_UNI_PROF_DUMP"):   # every universe's phase cycles + its job (time-model fits)
             np.savez(os.environ["PT_UNI_PROF_DUMP"], prof=prof, dims=np.array([int(j.dim) for j in jobs]),
                      bs=np.array([int(j.batch_size) for j in jobs]), epochs=np.array([int(j.epochs) for j in jobs]),
-                     E=np.array([u["ent"].shape[0] for u in unis]), run_s=el / args.c3_steps)
+                     E=np.array([u["ent"].shape[0] for u in unis]), run_s=el / args.c3_steps,
+                     start_ms=w_start, dur_ms=w_dur)
         tot_p = prof[:, :3].sum(axis=0) / max(prof[:, 3].sum(), 1)
         print("universe-prof all: cycles/step presample %.0f A %.0f B %.0f" % tuple(tot_p), file=sys.stderr)
         print("universe-prof longest universe: %.1f Mcycles (%.1f ms at 2.4 GHz); run %.1f ms" %

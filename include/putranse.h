@@ -217,7 +217,8 @@ int pt_universe_set_train(pt_universe_set *s, float *d_losses, void *stream);
 int pt_universe_set_free(pt_universe_set *s);
 /* per-universe cycle counters of the fast kernel (on = 1; off by default) and their readout: out[n][64], per
  * universe (in the set's launch order) shader-clock cycles spent in epoch presampling, phase A, phase B, the
- * step count, batch size, dim and entity count (last train call; out[.][7] unused); out[.][8..63]: phase stamps
+ * step count, batch size, dim and entity count (last train call); out[.][7]: the universe's start on the 100 MHz
+ * wall clock (low 32 bits, in the high word) and its duration in those ticks (low word); out[.][8..63]: phase stamps
  * of one step of lane group 0 in the measurement build (make TUNING=1), zero otherwise */
 int pt_universe_set_profiling(pt_universe_set *s, int32_t on);
 int pt_universe_set_profile(pt_universe_set *s, uint64_t *out);
@@ -226,6 +227,9 @@ int pt_universe_set_states(pt_universe_set *s, int64_t job, uint64_t *out);
 /* every job's LCG states back to their values at pt_universe_set_create (re-running the same trainings from the
  * same start, e.g. a benchmark's repeats; the caller restores tables and optimizer state) */
 int pt_universe_set_reset(pt_universe_set *s);
+/* 1 when universes of embedding dim `dim` train on the fast universe kernels (model PT_TRANSE / PT_TRANSH),
+ * else 0 (pt_universe_set_create then fails with PT_EINVAL). No device call. */
+int pt_universe_dim_supported(int64_t dim, int32_t model);
 /* reference-order (deterministic) mode of a set (see pt_trainer_set_deterministic): one workgroup per
  * universe runs its steps with the ordered per-row sums; its workspace is allocated on first use */
 int pt_universe_set_deterministic(pt_universe_set *s, int32_t on);

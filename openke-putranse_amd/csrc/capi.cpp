@@ -1412,6 +1412,11 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
 
 // the sampler streams back to the jobs' creation states (a benchmark re-runs the same training from the same
 // start: the caller restores the tables and optimizer state)
+// whether universes of this dim train on the fast path (its row shape is compiled into its class kernel)
+extern "C" int pt_universe_dim_supported(int64_t dim, int32_t model) {
+    return (model == PT_TRANSE || model == PT_TRANSH) && pt::universe_shape_supported(dim, model) ? 1 : 0;
+}
+
 extern "C" int pt_universe_set_reset(pt_universe_set *set) {
     PT_CHECK(set, PT_EINVAL, "null universe set");
     if (!set->host.empty())   // the states block at the arena's start, in set order

@@ -51,6 +51,12 @@ struct UniverseLaunch {
 
 // lane-group shape of the universe kernel for dim D (narrower groups than pick_shape) and its id in
 // the kernel's shape switch (-1: unsupported)
+// chunks of VEC floats per lane of a universe row shape: 8 floats per lane for TransE's scalar rows (wide:
+// twice the lane groups, half the rounds of a step's positives), 4 for TransH's; float4 rows 2 chunks (8 floats)
+// for both. (r04, same box: float4 TransE rows at 8 instead of 16 floats per lane moved them from the 512-thread
+// 16-float class kernel, whose CU share finished last, to the 1,024-thread 8-float one: C3 52.5 -> 40.2 ms,
+// C4 105.8 -> 104.0 ms; only TransE rows over 512 floats still take the 16-float class.)
+constexpr int universe_chunks_per_lane(int model, int vec) { return vec == 4 ? 2 : (model == 0 ? 8 : 4); }
 Shape pick_universe_shape(int64_t D, bool wide);
 int universe_shape_id(int64_t D, int model);
 bool universe_shape_supported(int64_t D, int model);

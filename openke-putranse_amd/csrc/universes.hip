@@ -7,7 +7,7 @@ namespace pt {
 Shape pick_universe_shape(int64_t D, bool wide) {
     const int VEC = D % 4 == 0 ? 4 : 1;
     const int64_t chunks = (D + VEC - 1) / VEC;
-    const int64_t per_lane = (VEC == 4 ? 2 : 4) * (wide ? 2 : 1);
+    const int64_t per_lane = wide ? universe_chunks_per_lane(0, VEC) : universe_chunks_per_lane(1, VEC);
     int G = 2;
     while (G < 64 && (int64_t)G * per_lane < chunks) G <<= 1;
     int KCH = 1;
@@ -25,8 +25,9 @@ int universe_shape_id(int64_t D, int model) {
         return v && atoi(v) != 0;
     }();
     const Shape s = pick_universe_shape(D, model == 0 && !narrow);
+    // (a shape its class kernel does not compile would leave the universe untrained: unsupported instead)
 #define PT_USUP(ID_, G_, V_, K_) \
-    if (s.G == G_ && s.VEC == V_ && s.KCH == K_) return ID_;
+    if (s.G == G_ && s.VEC == V_ && s.KCH == K_) return dev::shape_reachable(model, G_, V_, K_) ? ID_ : -1;
     PT_USHAPES(PT_USUP)
 #undef PT_USUP
     return -1;

@@ -64,11 +64,11 @@ __device__ __forceinline__ void phase_barrier(bool agent) {
 
 // Hardware sqrt / reciprocal (1 ulp, v_sqrt_f32 / v_rcp_f32), as in the C2 training step, for the row
 // shapes of at most 8 floats per lane: a correctly rounded division or square root is ~10 VALU
-// instructions in a kernel bound by instruction issue. The 16-float class (long TransE rows, C4) keeps the
-// IEEE forms: its register allocation with the hardware forms slowed its phase A by 25% (C4 105 -> 120 ms),
-// and there a 1-ulp difference in a normalization was seen amplified by a cancelling gradient sum to
-// 5.3e-6 (one component, above the teacher-forced tolerance). The reference-order kernel (ordered.hip)
-// keeps IEEE forms throughout.
+// instructions in a kernel bound by instruction issue. The 16-float class (TransE rows over 512 floats since
+// r04; C4's D = 200 before) keeps the IEEE forms: with the hardware forms its register allocation slowed its
+// phase A by 25% (r03, C4 105 -> 120 ms). (A 1-ulp difference amplified by a cancelling gradient sum, 5.3e-6
+// on one C4 component in r03, is within the forward-error bound the parity tests use since r04.) The
+// reference-order kernel (ordered.hip) keeps IEEE forms throughout.
 constexpr bool kUF = true;
 
 // backward of F.normalize (vnormalize_bwd) without a branch on the norm: the rows of a wave's lane groups
@@ -244,8 +244,9 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
         uload(th[q], P.ent + tp[q] * D, D, lane);
         uload(rh[q], P.rel + rp[q] * D, D, lane);
     }
-    // long wide rows (16 floats per lane over >= 16 lanes, D > 128): the first negative's row loads
-    // with the positive's, the rest one at a time in the loop (measured: C4, D = 200, 129 -> 108 ms; for
+    // long wide rows (16 floats per lane over >= 16 lanes: TransE rows over 512 floats since r04): the first
+    // negative's row loads with the positive's, the rest one at a time in the loop (measured r02 on C4's then
+    // 16-float rows, D = 200: 129 -> 108 ms; for
     // the short rows of C3 the extra live row costs more than the round trip it hides, 66 -> 74 ms)
     // (for every shape: C3 / C4 / C5 unchanged, r03; measured r04 and removed: also prefetching for the rows
     // of at most 6 floats per lane with the four rows' normalizations and the two score norms reduced
@@ -568,6 +569,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     const int per = bs % threads == 0 ? bs / threads : bs / threads + 1;
     float epoch_loss = 0.f;
     uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0;
+    const uint64_t w_start = U.prof ? wall_clock64() : 0;   // (100 MHz wall clock: the set's schedule)
     __syncthreads();
     for (int epoch = 0; epoch < epochs; ++epoch) {
         for (int step = 0; step < nbatches; ++step) {
@@ -793,6 +795,8 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
         U.prof[4] = (uint64_t)bs;
         U.prof[5] = (uint64_t)D;
         U.prof[6] = (uint64_t)E;
+        // the universe's start on the 100 MHz wall clock (low 32 bits) and its duration in those ticks
+        U.prof[7] = (w_start << 32) | ((wall_clock64() - w_start) & 0xffffffffull);
     }
     if (tid < threads) U.states[tid] = s_states[tid];
 }
@@ -820,7 +824,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
 // register allocation for fewer of them); TransH rows above 512 floats (class 2) are not supported.
 constexpr bool shape_reachable(int model, int G, int VEC, int KCH) {
     // (exact_kch_shape: G in (2, 64), so the 2-lane VEC=4 exact shape is the KCH <= p case below)
-    const int p = (VEC == 4 ? 2 : 4) * (model == 0 ? 2 : 1);
+    const int p = universe_chunks_per_lane(model, VEC);
     if (model == 1 && VEC * KCH > 8) return false;
     if (G > 2 && G < 64 && KCH > p / 2 && KCH < p) return exact_kch_shape(G, VEC);   // see pick_universe_shape
     return G == 2 ? KCH <= p : (G == 64 ? KCH >= p : KCH == p);

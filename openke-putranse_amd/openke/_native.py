@@ -83,6 +83,7 @@ SIGNATURES = {
     "pt_trainer_set_deterministic": (ctypes.c_int, [c_vp, c_i32]),
     "pt_trainer_set_sampling": (ctypes.c_int, [c_vp, c_i32, c_i64]),
     "pt_trainer_set_step_apply": (ctypes.c_int, [c_vp, c_i32]),
+    "pt_universe_dim_supported": (ctypes.c_int, [c_i64, c_i32]),
     "pt_trainer_step_apply": (ctypes.c_int, [c_vp]),
     "pt_trainer_get_deterministic": (ctypes.c_int, [c_vp]),
     "pt_trainer_sample_csr": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, ctypes.c_int32, c_vp,

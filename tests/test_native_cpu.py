@@ -355,3 +355,17 @@ def test_host_sanitizers(san):
     assert r.returncode == 0, out[-4000:]
     assert "san_driver: ok (0 failed checks)" in out
     assert "Sanitizer" not in out and "runtime error" not in out, out[-4000:]
+
+
+def test_universe_dims_supported():
+    """Every universe dim the fast kernels accept has its row shape compiled into its class kernel (the host's
+    shape choice and the kernels' shape_reachable agree; a mismatch would leave a universe untrained, so the
+    library reports the dim unsupported instead): TransE and TransH 1-512, TransE float4 rows up to 1,024."""
+    from openke import _native
+    L = _native.lib()
+    for d in range(1, 513):
+        assert L.pt_universe_dim_supported(d, _native.PT_TRANSE) == 1, d
+        assert L.pt_universe_dim_supported(d, _native.PT_TRANSH) == 1, d
+    for d in range(516, 1025, 4):
+        assert L.pt_universe_dim_supported(d, _native.PT_TRANSE) == 1, d
+    assert L.pt_universe_dim_supported(0, _native.PT_TRANSE) == 0
