@@ -738,6 +738,11 @@ def main():
     contrib_rt = 2 * bs * neg * dim * 4   # gradient rows of the corrupted entities: stored by the step, read by apply
 
     c3 = None if args.no_c3 else run_universes(args, ws, rank, dev, "c3", cpu=True)
+    if c3 is not None and ws == 1 and not args.no_dropin:
+        # the drop-in universe path on the same C3 set, as experiments/static_experiment_PuTransE_on_WN18.py
+        # drives it (Parallel_Universe_Config.train_parallel_universes), beside the kernel-only time above
+        c3["dropin"] = run_dropin(args, ws, rank, dev, "c3")
+        c3["dropin"]["over_kernel_only"] = c3["dropin"]["train_parallel_universes_s"] / c3["s_per_step"]
     # universe weak scaling (512 universes per GPU, no collective): at N = 1 it is the strong line
     c3w = None if args.no_c3 or ws == 1 else run_universes(args, ws, rank, dev, "c3", cpu=False, per_gpu=True)
     if rank != 0:

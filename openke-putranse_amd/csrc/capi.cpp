@@ -1504,10 +1504,11 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
         PT_CHECK(p.side == 0 || p.side == 1, PT_EINVAL, "pair side must be 0 or 1");
         PT_CHECK(pt::shape_supported(U.dim), PT_ENOTSUP, "dim not supported");
     }
-    // Jobs = (embedding dim, key batch): a key batch's score rows (keys x global_ent_total floats) are
-    // sized to stay resident in the Infinity Cache while its pairs' atomicMins land (PT_LP_BATCH_MB,
-    // default 192); inside a job the pairs are sorted by universe so each universe's entity rows are
-    // read once per job.
+    // Jobs = (lane-group row shape of the universes' dims, key batch): one launch pair per job covers every
+    // dim of that shape (C3's ~80 dims take ~10 shapes: one launch pair per dim left most of the GPU idle). A
+    // key batch's score rows (keys x global_ent_total floats) are sized to stay resident in the Infinity
+    // Cache while its pairs' atomicMins land (PT_LP_BATCH_MB, default 192); inside a job the pairs are
+    // sorted by universe so each universe's entity rows are read once per job.
     int64_t n_keys = 0;
     for (int64_t i = 0; i < n_pairs; ++i) n_keys = std::max<int64_t>(n_keys, (int64_t)pairs[i].key + 1);
     int64_t batch_mb = 192;
@@ -1515,10 +1516,14 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
     const int64_t keys_per_batch =
         std::max<int64_t>(1, (batch_mb << 20) / (4 * std::max<int64_t>(global_ent_total, 1)));
     const int64_t n_batches = (n_keys + keys_per_batch - 1) / keys_per_batch;
-    std::map<std::pair<int64_t, int64_t>, std::vector<std::vector<pt::LpPair>>> jobs_pairs;   // (dim, batch)
+    auto shape_key = [](int64_t dim) {
+        const pt::Shape s = pt::pick_shape(dim);
+        return (int64_t)s.G * 10000 + (int64_t)s.VEC * 100 + s.KCH;
+    };
+    std::map<std::pair<int64_t, int64_t>, std::vector<std::vector<pt::LpPair>>> jobs_pairs;   // (shape, batch)
     for (int64_t i = 0; i < n_pairs; ++i) {
         const pt_lp_pair &p = pairs[i];
-        auto &per_u = jobs_pairs[{us[p.universe].dim, p.key / keys_per_batch}];
+        auto &per_u = jobs_pairs[{shape_key(us[p.universe].dim), p.key / keys_per_batch}];
         if (per_u.empty()) per_u.resize((size_t)n_universes);
         per_u[p.universe].push_back(pt::LpPair{p.key, p.universe, p.anchor, p.rel, p.side});
     }
@@ -1538,7 +1543,7 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
     };
     std::vector<DimJob> dj;
     for (auto &kv : jobs_pairs) {
-        DimJob d{kv.first.first, (int64_t)hp.size(), 0, (int64_t)uids.size(), 0, 0, (int64_t)uoff.size()};
+        DimJob d{0, (int64_t)hp.size(), 0, (int64_t)uids.size(), 0, 0, (int64_t)uoff.size()};   // dim: the largest
         uoff.resize(uoff.size() + 2 * (size_t)n_universes, 0);
         for (int64_t u = 0; u < n_universes; ++u) {
             const auto &v = kv.second[u];
@@ -1548,6 +1553,7 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
             uoff[d.uoff_begin + 2 * u + 1] = (int64_t)hp.size() - d.p_begin;
             uids.push_back((int32_t)u);
             d.max_ent = std::max(d.max_ent, us[u].ent_total);
+            d.dim = std::max(d.dim, us[u].dim);
         }
         d.p_end = (int64_t)hp.size();
         d.u_end = (int64_t)uids.size();
@@ -1555,6 +1561,7 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
     }
     int64_t max_dim = 0;
     for (auto &d : dj) max_dim = std::max(max_dim, d.dim);
+    max_dim = (max_dim + 3) & ~int64_t(3);   // every job's scratch region 16-byte aligned (float4 rows)
     const size_t scratch = (size_t)n_pairs * (size_t)max_dim * (model == 1 ? 2 : 1);
     char *blk = nullptr;
     const size_t bytes = sizeof(pt::LpUniverseDev) * hu.size() + sizeof(pt::LpPair) * hp.size() +
@@ -1584,7 +1591,7 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
         const hipError_t e = pt::launch_lp_min(du, dp + d.p_begin, np, duoff + d.uoff_begin, duids + d.u_begin,
                                                d.u_end - d.u_begin,
                                                d.dim, d.max_ent, model, p_norm, norm_flag, global_ent_total,
-                                               b, nrm, d_key_rows, d_key_tuple, st);
+                                               d.dim, b, nrm, d_key_rows, d_key_tuple, st);
         if (e != hipSuccess) {
             rc = pt::fail(PT_EHIP, std::string("launch_lp_min: ") + hipGetErrorString(e));
             break;

@@ -141,11 +141,12 @@ hipError_t launch_score(const StepParams &P, int mode, const int64_t *h, const i
 hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh, const int64_t *qt, const int64_t *qr,
                                 int64_t nq, int64_t E, float *out, hipStream_t st, int global_order = 0);
 // pairs sorted by universe; universe u's pairs are pairs[uoff[2u] .. uoff[2u+1]); uids = the n_active
-// universes with pairs; base / normal: scratch [n_pairs][dim]
+// universes with pairs, all of dims that take dim's lane-group shape (pick_shape); base / normal: scratch
+// [n_pairs][ds], ds >= every such dim
 hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, const int64_t *uoff,
                          const int32_t *uids, int64_t n_active, int64_t dim, int64_t max_ent, int model, int p_norm,
-                         int norm_flag, int64_t global_E, float *base, float *normal, float *rows, float *tuple_min,
-                         hipStream_t st);
+                         int norm_flag, int64_t global_E, int64_t ds, float *base, float *normal, float *rows,
+                         float *tuple_min, hipStream_t st);
 
 hipError_t launch_rank_rows(const float *rows, int64_t E, const int64_t *row_of, const int64_t *truth,
                             const float *repl, const int64_t *part_off, const int64_t *part, int64_t nq, int64_t *raw,

@@ -720,10 +720,13 @@ __global__ __launch_bounds__(256) void k_score_queries(StepParams P, int side, c
 // k_lp_scan: one workgroup per (entity chunk, universe): each entity row is loaded (and, for TransE,
 //   normalized) ONCE and scored against every pair of its universe - the universe's rows are read once
 //   per chunk instead of once per pair.
+// One launch pair covers every universe whose dim takes the same lane-group shape (each universe's own dim
+// at run time); the pairs' base / normal rows are `ds` floats apart (the largest dim of the launch).
 template <int MODEL, int G, int VEC, int KCH>
 __global__ __launch_bounds__(256) void k_lp_bases(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
-                                                  int64_t n_pairs, int p_norm, int norm_flag, float *__restrict__ base,
-                                                  float *__restrict__ normal, float *__restrict__ tuple_min) {
+                                                  int64_t n_pairs, int p_norm, int norm_flag, int64_t ds,
+                                                  float *__restrict__ base, float *__restrict__ normal,
+                                                  float *__restrict__ tuple_min) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = 256 / G;
     const int lane = threadIdx.x % G;
@@ -751,18 +754,18 @@ __global__ __launch_bounds__(256) void k_lp_bases(const LpUniverseDev *__restric
         const float ad = vdot(A, nW);
 #pragma unroll
         for (int k = 0; k < Vec::N; ++k) A.x[k] = A.x[k] - ad * nW.x[k];
-        vstore(nW, normal + pi * D, D, lane);
+        vstore(nW, normal + pi * ds, D, lane);
     }
     if (norm_flag) vnormalize(A, ah); else ah = A;
 #pragma unroll
     for (int k = 0; k < Vec::N; ++k) b.x[k] = pr.side == 0 ? rh.x[k] - ah.x[k] : ah.x[k] + rh.x[k];
-    vstore(b, base + pi * D, D, lane);
+    vstore(b, base + pi * ds, D, lane);
 }
 
 template <int MODEL, int G, int VEC, int KCH>
 __global__ __launch_bounds__(256) void k_lp_scan(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
                                                  const int64_t *__restrict__ uoff, const int32_t *__restrict__ uids,
-                                                 int p_norm, int norm_flag, int64_t global_E,
+                                                 int p_norm, int norm_flag, int64_t global_E, int64_t ds,
                                                  const float *__restrict__ base, const float *__restrict__ normal,
                                                  float *__restrict__ rows) {
     using Vec = V<G, VEC, KCH>;
@@ -793,9 +796,9 @@ __global__ __launch_bounds__(256) void k_lp_scan(const LpUniverseDev *__restrict
         for (int64_t pi = p0; pi < p1; ++pi) {
             const LpPair pr = pairs[pi];
             Vec b;
-            vload(b, base + pi * D, D, lane);
+            vload(b, base + pi * ds, D, lane);
             Vec nW;
-            if constexpr (MODEL == 1) vload(nW, normal + pi * D, D, lane);
+            if constexpr (MODEL == 1) vload(nW, normal + pi * ds, D, lane);
 #pragma unroll
             for (int q = 0; q < EPG; ++q) {
                 if constexpr (MODEL == 1) {
@@ -811,6 +814,95 @@ __global__ __launch_bounds__(256) void k_lp_scan(const LpUniverseDev *__restrict
                 const float sc = vpnorm(v, p_norm);
                 if (lane == 0 && col[q] >= 0)
                     atomicMin(reinterpret_cast<int *>(rows + (int64_t)pr.key * global_E + col[q]), __float_as_int(sc));
+            }
+        }
+    }
+}
+
+// k_lp_scan_t: the scan transposed - one LANE per entity. A workgroup (4 waves) stages a tile of 64
+// consecutive local entity rows in LDS once (row stride D + 1 floats: lane e reading float d of its row hits
+// bank (e + d) mod 64, conflict-free), and each wave walks a quarter of the universe's pairs: for a pair, every
+// lane sums its own entity's |x + b| (or squares) sequentially over d with the pair's base row uniform across
+// the wave - no cross-lane reduction per score - and MINs its score into the key row with one atomic
+// instruction for 64 entities, skipped when the row already holds a score no larger (the rows only decrease,
+// so a stale read can only make an atomic unnecessary, never wrong). TransE rows are normalized once per
+// tile (inverse norm per lane); TransH rows are projected on the pair's normal and normalized per pair.
+// sum over d < D of f(d) in 8 interleaved partial sums, combined pairwise: 8 independent add chains per lane
+// and a rounding error of order (D / 8 + 3) ulp, near the tree reductions of the lane-group kernels
+template <typename F>
+__device__ __forceinline__ float sum8(int D, F f) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int d = 0;
+    for (; d + 8 <= D; d += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] += f(d + k);
+    }
+    for (int k = 0; d + k < D; ++k) a[k] += f(d + k);
+    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+template <int MODEL>
+__global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
+                                                   const int64_t *__restrict__ uoff, const int32_t *__restrict__ uids,
+                                                   int p_norm, int norm_flag, int64_t global_E, int64_t ds,
+                                                   const float *__restrict__ base, const float *__restrict__ normal,
+                                                   float *__restrict__ rows) {
+    extern __shared__ float s_x[];   // [64][D + 1]
+    const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+    const int32_t u = uids[blockIdx.y];
+    const LpUniverseDev U = us[u];
+    const int D = (int)U.dim, S = D + 1;
+    const int64_t p0 = uoff[2 * u], p1 = uoff[2 * u + 1];
+    for (int64_t e0 = (int64_t)blockIdx.x * 64; e0 < U.ent_total; e0 += (int64_t)gridDim.x * 64) {
+        const int ne = U.ent_total - e0 < 64 ? (int)(U.ent_total - e0) : 64;
+        __syncthreads();   // (the previous tile's readers are done)
+        const float *src = U.ent + e0 * D;
+        for (int i = (int)threadIdx.x; i < ne * D; i += 256) {
+            const int r = i / D;
+            s_x[r * S + (i - r * D)] = src[i];
+        }
+        __syncthreads();
+        const bool live = lane < ne;
+        const float *xr = s_x + (live ? lane : 0) * S;
+        const int64_t col = live ? U.remap[e0 + lane] : 0;
+        float inv = 1.f;
+        if (MODEL == 0 && norm_flag) {   // F.normalize's scale of this lane's row
+            const float n = sqrtf(sum8(D, [&](int d) { return xr[d] * xr[d]; }));
+            inv = 1.0f / (n > kEps ? n : kEps);
+        }
+        for (int64_t pi = p0 + wave; pi < p1; pi += 4) {
+            const LpPair pr = pairs[pi];
+            const float *b = base + pi * ds;
+            const float sg = pr.side == 0 ? 1.f : -1.f;   // side 0: x-hat + b; side 1: b - x-hat
+            float acc;
+            if constexpr (MODEL == 0) {
+                acc = p_norm == 1 ? sum8(D, [&](int d) { return fabsf(sg * (xr[d] * inv) + b[d]); })
+                                  : sum8(D, [&](int d) {
+                                        const float v = sg * (xr[d] * inv) + b[d];
+                                        return v * v;
+                                    });
+            } else {
+                const float *nw = normal + pi * ds;
+                const float xd = sum8(D, [&](int d) { return xr[d] * nw[d]; });
+                float sc = 1.f;
+                if (norm_flag) {
+                    const float n = sqrtf(sum8(D, [&](int d) {
+                        const float t = xr[d] - xd * nw[d];
+                        return t * t;
+                    }));
+                    sc = 1.0f / (n > kEps ? n : kEps);
+                }
+                acc = p_norm == 1 ? sum8(D, [&](int d) { return fabsf(sg * ((xr[d] - xd * nw[d]) * sc) + b[d]); })
+                                  : sum8(D, [&](int d) {
+                                        const float v = sg * ((xr[d] - xd * nw[d]) * sc) + b[d];
+                                        return v * v;
+                                    });
+            }
+            const float score = p_norm == 1 ? acc : sqrtf(acc);
+            if (live) {
+                int *cell = reinterpret_cast<int *>(rows + (int64_t)pr.key * global_E + col);
+                const int bits = __float_as_int(score);
+                if (bits < *cell) atomicMin(cell, bits);
             }
         }
     }
@@ -997,12 +1089,26 @@ hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh
     return hipErrorInvalidValue;
 }
 
+// PT_LP_SCAN_T (measurement builds): 1 = the transposed scan k_lp_scan_t (default), 0 = k_lp_scan
+#ifndef PT_LP_SCAN_T
+#define PT_LP_SCAN_T 1
+#endif
 hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, const int64_t *uoff,
                          const int32_t *uids, int64_t n_active, int64_t dim, int64_t max_ent, int model, int p_norm,
-                         int norm_flag, int64_t global_E, float *base, float *normal, float *rows, float *tuple_min,
-                         hipStream_t st) {
+                         int norm_flag, int64_t global_E, int64_t ds, float *base, float *normal, float *rows,
+                         float *tuple_min, hipStream_t st) {
     if (n_pairs <= 0) return hipSuccess;
     const Shape s = pick_shape(dim);
+    // the transposed scan's tile of 64 rows in LDS (row stride dim + 1)
+    const size_t lds_t = sizeof(float) * 64 * (size_t)(dim + 1);
+    if (PT_LP_SCAN_T && lds_t > (64 << 10) && lds_t <= (160 << 10)) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_lp_scan_t<0>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_t);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_lp_scan_t<1>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_t);
+        if (e != hipSuccess) return e;
+    }
     const int64_t gpb = 256 / s.G;
     const dim3 gb((unsigned)((n_pairs + gpb - 1) / gpb)), block(256);
     int64_t bx = (max_ent + gpb * 4 - 1) / (gpb * 4);
@@ -1015,17 +1121,25 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
             if (y0 == 0) {                                                                                         \
                 if (model == 0)                                                                                    \
                     hipLaunchKernelGGL((dev::k_lp_bases<0, G_, V_, K_>), gb, block, 0, st, us, pairs, n_pairs,    \
-                                       p_norm, norm_flag, base, normal, tuple_min);                                \
+                                       p_norm, norm_flag, ds, base, normal, tuple_min);                            \
                 else                                                                                               \
                     hipLaunchKernelGGL((dev::k_lp_bases<1, G_, V_, K_>), gb, block, 0, st, us, pairs, n_pairs,    \
-                                       p_norm, norm_flag, base, normal, tuple_min);                                \
+                                       p_norm, norm_flag, ds, base, normal, tuple_min);                            \
             }                                                                                                      \
-            if (model == 0)                                                                                        \
+            if (PT_LP_SCAN_T && lds_t <= (160 << 10)) {                                                         \
+                const dim3 gt((unsigned)((max_ent + 63) / 64), gs.y);                                               \
+                if (model == 0)                                                                                    \
+                    hipLaunchKernelGGL((dev::k_lp_scan_t<0>), gt, block, lds_t, st, us, pairs, uoff, uids + y0,      \
+                                       p_norm, norm_flag, global_E, ds, base, normal, rows);                        \
+                else                                                                                               \
+                    hipLaunchKernelGGL((dev::k_lp_scan_t<1>), gt, block, lds_t, st, us, pairs, uoff, uids + y0,      \
+                                       p_norm, norm_flag, global_E, ds, base, normal, rows);                        \
+            } else if (model == 0)                                                                                 \
                 hipLaunchKernelGGL((dev::k_lp_scan<0, G_, V_, K_>), gs, block, 0, st, us, pairs, uoff, uids + y0,   \
-                                   p_norm, norm_flag, global_E, base, normal, rows);                                \
+                                   p_norm, norm_flag, global_E, ds, base, normal, rows);                            \
             else                                                                                                   \
                 hipLaunchKernelGGL((dev::k_lp_scan<1, G_, V_, K_>), gs, block, 0, st, us, pairs, uoff, uids + y0,   \
-                                   p_norm, norm_flag, global_E, base, normal, rows);                                \
+                                   p_norm, norm_flag, global_E, ds, base, normal, rows);                            \
         }                                                                                                          \
         return hipGetLastError();                                                                                  \
     }
