@@ -815,7 +815,8 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
 
 // shape class (one kernel each): 0 = at most 4 floats per lane, 1 = 8, 2 = 16 (TransE's wide shapes). (Measured
 // r04 and removed: splitting class 1 into 5-6 and 7-8 floats, so the 5-6 kernel - C3's longest universes, 65-96
-// dims over 16 lanes - fits 1,024 threads without spilling: C3 52.3 -> 52.8 ms, the fourth launch costs more.)
+// dims over 16 lanes - fits 1,024 threads without spilling: C3 52.3 -> 52.8 ms, the fourth launch costs more;
+// splitting it by vector width, scalar and float4 rows: C3 40.3 -> 41.1 ms.)
 #define PT_UCLASS(V_, K_) ((V_) * (K_) <= 4 ? 0 : ((V_) * (K_) <= 8 ? 1 : 2))
 
 // whether pick_universe_shape can return (G, VEC, KCH) for the model (TransE: wide shapes, TransH: narrow):
@@ -837,6 +838,11 @@ constexpr bool shape_reachable(int model, int G, int VEC, int KCH) {
 // kernel is register-allocated for its own widest shape (one kernel over all shapes spills the narrow
 // ones' state too), and two launches still run concurrently (a launch per shape would need more
 // hardware queues than a process gets).
+// PT_UNI_ONLY_SHAPE (measurement builds only: the other shapes' universes are then NOT trained): compile one
+// row shape into the class kernels, to time that shape's chain without the other shapes' register allocation
+#ifndef PT_UNI_ONLY_SHAPE
+#define PT_UNI_ONLY_SHAPE -1
+#endif
 template <int MODEL, int NT, int WPE, int CLS, int PLAN>
 __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__restrict__ us, int64_t n,
                                                        int *__restrict__ next_universe, int p_norm, int norm_flag,
@@ -862,7 +868,8 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
         switch (U.shape) {
 #define PT_URUN(ID_, G_, V_, K_)                                                                       \
     case ID_:                                                                                          \
-        if constexpr (PT_UCLASS(V_, K_) == CLS && shape_reachable(MODEL, G_, V_, K_))                   \
+        if constexpr (PT_UCLASS(V_, K_) == CLS && shape_reachable(MODEL, G_, V_, K_) &&                 \
+                      (PT_UNI_ONLY_SHAPE < 0 || ID_ == PT_UNI_ONLY_SHAPE))                              \
             universe_run<MODEL, G_, V_, K_, NT, PLAN>(U, p_norm, norm_flag, opt, (int)neg, bern, filter, cfg, S); \
         break;
             PT_USHAPES(PT_URUN)

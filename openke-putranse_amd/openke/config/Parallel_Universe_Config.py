@@ -590,7 +590,7 @@ class Parallel_Universe_Config(Tester):
         em = np.ascontiguousarray(ent_remap, dtype=np.int64)
         rm = np.ascontiguousarray(rel_remap, dtype=np.int64)
         self._pending_maps.append((uid, em, rm))
-        self._remap_cache[uid] = self._remaps_from_arrays(em, rm)
+        self._remap_cache[uid] = (em, rm)   # the sorted lookup helpers on first use (_remaps)
 
     def _materialize_maps(self):
         """Register the pending universes' maps in the reference's dictionaries, all at once: the per-universe
@@ -805,7 +805,12 @@ class Parallel_Universe_Config(Tester):
         return em, rm, em[eo], eo, rm[ro], ro
 
     def _remaps(self, uid):
+        """(ent_remap, rel_remap, sorted entity ids, their order, sorted relation ids, their order) of a
+        universe; the sorted helpers are built on first use (the training commit and the LP fold read only the
+        remaps, _remap_arrays)."""
         c = self._remap_cache.get(uid)
+        if c is not None and len(c) == 2:
+            c = self._remap_cache[uid] = self._remaps_from_arrays(*c)
         if c is None:
             emap, rmap = self.entity_id_mappings[uid], self.relation_id_mappings[uid]
             em = np.zeros(len(emap), dtype=np.int64)
@@ -816,6 +821,11 @@ class Parallel_Universe_Config(Tester):
                 rm[l] = g
             c = self._remap_cache[uid] = self._remaps_from_arrays(em, rm)
         return c
+
+    def _remap_arrays(self, uid):
+        """(local -> global entity ids, local -> global relation ids) of a universe."""
+        c = self._remap_cache.get(uid)
+        return (c[0], c[1]) if c is not None else self._remaps(uid)[:2]
 
     def _store(self, eval_mode):
         st = self._stores.get(eval_mode)
@@ -837,7 +847,7 @@ class Parallel_Universe_Config(Tester):
             kge = self.trained_embedding_spaces[u]
             if not next(kge.parameters()).is_cuda:
                 kge.cuda()
-            em, rm, eg, eo, rg, ro = self._remaps(u)
+            em, rm = self._remap_arrays(u)
             dr = self._dev_remaps.get(u)
             if dr is None:
                 dr = self._dev_remaps[u] = torch.from_numpy(em).cuda()

@@ -15,3 +15,9 @@ for w in c3 c4; do
   timeout -k 10 400 python tools_gpu/ablib.py ab/lib_ls0.so bench.py --workload $w --steps 1 --warmup 1 \
     --no-cpu-baseline --deterministic-timing 0 > gpurun_out/${T}_ls0_$w.log 2>&1 || exit $?
 done
+# the D 65-80 scalar-row shape alone in its class kernel (ab/lib_solo27.so: no other shape's registers; the
+# other universes are NOT trained - a chain measurement only) vs the product, per-universe cycles
+PT_UNI_PROF=1 timeout -k 10 300 python bench.py --workload c3 --steps 2 --warmup 1 --no-cpu-baseline --no-dropin \
+  --deterministic-timing 0 > gpurun_out/${T}_prof_prod_c3.log 2>&1 || exit $?
+PT_UNI_PROF=1 timeout -k 10 300 python tools_gpu/ablib.py ab/lib_solo27.so bench.py --workload c3 --steps 2 --warmup 1 \
+  --no-cpu-baseline --no-dropin --deterministic-timing 0 > gpurun_out/${T}_prof_solo_c3.log 2>&1 || exit $?
