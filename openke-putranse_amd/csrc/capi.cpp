@@ -11,6 +11,7 @@
 #include <thread>
 #include <tuple>
 #include <queue>
+#include <set>
 #include <unordered_map>
 #include <vector>
 
@@ -1130,7 +1131,43 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     };
     std::vector<int64_t> order((size_t)n);
     for (int64_t i = 0; i < n; ++i) order[i] = i;
-    auto cls_of = [&](int64_t i) { return pt::universe_shape_class(pt::universe_shape_id(jobs[i].dim, model)); };
+    // Kernel (class) per universe: its row shape's class kernel, or - for up to three "hot" shapes of class 1
+    // (TransE), those holding the set's longest universes - a kernel compiled for that shape alone. A class
+    // kernel is register-allocated for all its shapes at once: the longest C3 universe's shape alone runs its
+    // chain in 78 instead of 94 Mcycles. At most four launches in all (the hardware queues a process gets).
+    std::vector<int> cls_v((size_t)n);
+    {
+        std::vector<int> shape_v((size_t)n);
+        std::map<int, double> hot_cost;   // class-1 shape -> its longest universe (steps x (4 + rounds))
+        for (int64_t i = 0; i < n; ++i) {
+            shape_v[i] = pt::universe_shape_id(jobs[i].dim, model);
+            cls_v[i] = pt::universe_shape_class(shape_v[i]);
+            if (model != PT_TRANSE || cls_v[i] != 1) continue;
+            const int64_t gpb = pt::universe_shape_groups(shape_v[i], model);
+            const double c = (double)jobs[i].epochs * (double)jobs[i].nbatches *
+                             (4.0 + (double)((std::max<int64_t>(jobs[i].batch_size, 1) + gpb - 1) / gpb));
+            hot_cost[shape_v[i]] = std::max(hot_cost[shape_v[i]], c);
+        }
+        std::vector<std::pair<double, int>> cand;
+        for (auto &kv : hot_cost) cand.push_back({kv.second, kv.first});
+        std::sort(cand.begin(), cand.end(), std::greater<std::pair<double, int>>());
+        std::set<int> hot;
+        for (auto &c : cand) {
+            if (hot.size() >= 3) break;
+            std::set<int> h2 = hot;
+            h2.insert(c.second);
+            std::set<int> launches;
+            for (int64_t i = 0; i < n; ++i)
+                launches.insert(h2.count(shape_v[i]) ? pt::kUniHotBase + shape_v[i] : cls_v[i]);
+            if (launches.size() > 4) break;
+            hot = h2;
+        }
+        if (const char *v = pt_tuning_env("PT_UNI_HOT"))   // tuning: 0 = class kernels only
+            if (atoi(v) == 0) hot.clear();
+        for (int64_t i = 0; i < n; ++i)
+            if (hot.count(shape_v[i])) cls_v[i] = pt::kUniHotBase + shape_v[i];
+    }
+    auto cls_of = [&](int64_t i) { return cls_v[(size_t)i]; };
     std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
         const int sa = cls_of(a), sb = cls_of(b);
         if (sa != sb) return sa < sb;

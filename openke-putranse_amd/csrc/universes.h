@@ -35,6 +35,9 @@ struct UniverseDev {
 #define PT_UNI_NT 1024
 #endif
 constexpr int universe_class_threads(int model, int cls) { return model == 0 && cls < 2 ? PT_UNI_NT : 512; }
+// class ids from kUniHotBase on: a "hot" class-1 shape (id - kUniHotBase) run by a kernel compiled for that shape
+// alone (its own register allocation; see pt_universe_set_create)
+constexpr int kUniHotBase = 64;
 
 // launch configuration of one group of universes (host-chosen for the largest universe of the group)
 struct UniverseLaunch {

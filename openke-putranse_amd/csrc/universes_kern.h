@@ -838,11 +838,6 @@ constexpr bool shape_reachable(int model, int G, int VEC, int KCH) {
 // kernel is register-allocated for its own widest shape (one kernel over all shapes spills the narrow
 // ones' state too), and two launches still run concurrently (a launch per shape would need more
 // hardware queues than a process gets).
-// PT_UNI_ONLY_SHAPE (measurement builds only: the other shapes' universes are then NOT trained): compile one
-// row shape into the class kernels, to time that shape's chain without the other shapes' register allocation
-#ifndef PT_UNI_ONLY_SHAPE
-#define PT_UNI_ONLY_SHAPE -1
-#endif
 template <int MODEL, int NT, int WPE, int CLS, int PLAN>
 __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__restrict__ us, int64_t n,
                                                        int *__restrict__ next_universe, int p_norm, int norm_flag,
@@ -868,8 +863,8 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
         switch (U.shape) {
 #define PT_URUN(ID_, G_, V_, K_)                                                                       \
     case ID_:                                                                                          \
-        if constexpr (PT_UCLASS(V_, K_) == CLS && shape_reachable(MODEL, G_, V_, K_) &&                 \
-                      (PT_UNI_ONLY_SHAPE < 0 || ID_ == PT_UNI_ONLY_SHAPE))                              \
+        if constexpr ((CLS < kUniHotBase ? PT_UCLASS(V_, K_) == CLS : ID_ == CLS - kUniHotBase) &&     \
+                      shape_reachable(MODEL, G_, V_, K_))                                               \
             universe_run<MODEL, G_, V_, K_, NT, PLAN>(U, p_norm, norm_flag, opt, (int)neg, bern, filter, cfg, S); \
         break;
             PT_USHAPES(PT_URUN)
@@ -887,7 +882,8 @@ namespace detail {
 template <int MODEL, int WPE, int CLS, int PLAN>
 hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int64_t cus, int p_norm, int norm_flag, int opt,
                     int64_t neg, int bern, int filter, const UniverseLaunch &cfg, hipStream_t st) {
-    constexpr int NT = universe_class_threads(MODEL, CLS);
+    // (a hot single-shape kernel runs a class-1 shape: that class's workgroup size)
+    constexpr int NT = universe_class_threads(MODEL, CLS < kUniHotBase ? CLS : 1);
     auto kern = dev::k_universes<MODEL, NT, WPE * NT / 512, CLS, PLAN>;
     if (cfg.lds_bytes > (64 << 10)) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -916,6 +912,26 @@ hipError_t launch_universes_plan(const UniverseDev *d_us, int64_t n, int *counte
                                  int p_norm, int norm_flag, int opt, int64_t neg, int bern, int filter,
                                  const UniverseLaunch &cfg, hipStream_t st) {
     using detail::launch_q;
+    if (cls >= kUniHotBase) {
+        // a hot shape's own kernel (plans 1 and 2, TransE); otherwise its universes run in their class kernel
+        if constexpr (PLAN != 0) {
+            if (model == 0) {
+                switch (cls - kUniHotBase) {
+#define PT_UHOT(ID_, G_, V_, K_)                                                                                  \
+    case ID_:                                                                                                      \
+        if constexpr (PT_UCLASS(V_, K_) == 1 && dev::shape_reachable(0, G_, V_, K_))                                \
+            return launch_q<0, 2, kUniHotBase + ID_, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, \
+                                                          filter, cfg, st);                                        \
+        break;
+                    PT_USHAPES(PT_UHOT)
+#undef PT_UHOT
+                    default:
+                        break;
+                }
+            }
+        }
+        cls = 1;
+    }
     if (cls == 0)
         return model == 0 ? launch_q<0, 2, 0, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st)
                           : launch_q<1, 2, 0, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, filter, cfg, st);
