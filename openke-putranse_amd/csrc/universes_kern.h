@@ -102,18 +102,22 @@ constexpr bool exact_kch_shape(int G, int VEC) { return G >= (VEC == 4 ? 2 : 4) 
 #ifndef PT_UNI_GLOBAL
 #define PT_UNI_GLOBAL 2
 #endif
+#ifndef PT_UNI_BSPLIT
+#define PT_UNI_BSPLIT 0
+#endif
 constexpr bool uni_global(int floats) { return PT_UNI_GLOBAL == 1 || (PT_UNI_GLOBAL == 2 && floats <= 8); }
 template <int G, int VEC, int KCH>
 constexpr int full_chunks() { return exact_kch_shape(G, VEC) ? KCH - 1 : 0; }
 
-template <int G, int VEC, int KCH>
+// (EX = false: no chunk assumed full - a lane shape used for a dim range its pick_universe_shape did not make)
+template <bool EX = true, int G, int VEC, int KCH>
 __device__ __forceinline__ void uload(V<G, VEC, KCH> &o, const float *row_, int D, int lane) {
     if constexpr (!uni_global(VEC * KCH)) {
         vload(o, row_, D, lane);
         return;
     }
     const gfloat *row = (const gfloat *)(const void *)row_;
-    constexpr int F = full_chunks<G, VEC, KCH>();
+    constexpr int F = EX ? full_chunks<G, VEC, KCH>() : 0;
 #pragma unroll
     for (int k = 0; k < KCH; ++k) {
         const int c = k * G + lane;
@@ -133,14 +137,14 @@ __device__ __forceinline__ void uload(V<G, VEC, KCH> &o, const float *row_, int 
     }
 }
 
-template <int G, int VEC, int KCH>
+template <bool EX = true, int G, int VEC, int KCH>
 __device__ __forceinline__ void ustore(const V<G, VEC, KCH> &o, float *row_, int D, int lane) {
     if constexpr (!uni_global(VEC * KCH)) {
         vstore(o, row_, D, lane);
         return;
     }
     gfloat *row = (gfloat *)(void *)row_;
-    constexpr int F = full_chunks<G, VEC, KCH>();
+    constexpr int F = EX ? full_chunks<G, VEC, KCH>() : 0;
 #pragma unroll
     for (int k = 0; k < KCH; ++k) {
         const int c = k * G + lane;
@@ -227,7 +231,7 @@ struct UniverseSink {
 // per-negative row-role bookkeeping). get_neg(q, k, &e, &tail_side). Gradients in normalized space, like
 // group_step for TransE; a corrupted row equal to a positive row is simply a separate contribution.
 // Positive q's gradient rows go to sink sk[q] (its own contribution slots). Returns the summed losses.
-template <int NP, int G, int VEC, int KCH, typename Sink, typename NegFn>
+template <int NP, int G, int VEC, int KCH, bool PF = false, typename Sink, typename NegFn>
 __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp)[NP], const int (&rp)[NP],
                                              const int (&tp)[NP], int neg, NegFn get_neg, const Sink (&sk)[NP],
                                              int lane) {
@@ -251,7 +255,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     // (for every shape: C3 / C4 / C5 unchanged, r03; measured r04 and removed: also prefetching for the rows
     // of at most 6 floats per lane with the four rows' normalizations and the two score norms reduced
     // together (grouped DPP reductions) - C3 53.7 -> 55.5 ms, C5 (TransH counterpart) 36.6 -> 37.5 ms)
-    constexpr bool kPrefetch = VEC * KCH >= 16 && G >= 16;
+    constexpr bool kPrefetch = PF || (VEC * KCH >= 16 && G >= 16);   // PF: see universe_run
     int e[NP];
     bool tail_side[NP];
     Vec x[NP];
@@ -495,11 +499,15 @@ struct UniShared {
 //   2 = every row as a contribution list (relation rows too many for LDS: C5), presampled batches;
 //   0 = the launch configuration's choices at run time (fallbacks: global float atomics, global flags,
 //       per-step sampling).
-template <int MODEL, int G, int VEC, int KCH, int NT, int PLAN>
+template <int MODEL, int G, int VEC, int KCH, int NT, int PLAN, bool HOT = false>
 __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, int norm_flag, int opt, int neg,
                                              int bern, int filter, const UniverseLaunch &cfg, const UniShared &S) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = NT / G;
+    // the first negative's row loaded with the positive's (transe_step's kPrefetch) also for the hot kernels'
+    // rows over 128 floats (32 or 64 lanes; r04 same-box A/B: C4 99.4 -> 91.0 ms, its longest universe's phase
+    // A 27.9k -> 24.4k cycles/step; for C3's 16-lane hot shapes the set was 1 ms slower, so they do not)
+    constexpr bool PF = HOT && G >= 32;
     int32_t *s_dyn = S.dyn;
     uint64_t *s_states = S.states;
     int &s_count = *S.count;
@@ -629,7 +637,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                         // reading gives the same gradients)
                         const int hq[1] = {hp}, rq[1] = {rp}, tq[1] = {tp};
                         const UniverseSink<PLAN> sk[1] = {sink};
-                        lsum = transe_step<1, G, VEC, KCH>(
+                        lsum = transe_step<1, G, VEC, KCH, PF>(
                             P, hq, rq, tq, neg,
                             [&](int, int k, int &e, bool &tail_side) {
                                 const int o = (k + 1) * bs + b;
@@ -652,7 +660,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     if constexpr (MODEL == 0) {
                         const int hq[1] = {(int)pd.h}, rq[1] = {(int)pd.r}, tq[1] = {(int)pd.t};
                         const UniverseSink<PLAN> sk[1] = {sink};
-                        lsum = transe_step<1, G, VEC, KCH>(
+                        lsum = transe_step<1, G, VEC, KCH, PF>(
                             P, hq, rq, tq, neg,
                             [&](int, int k, int &e, bool &tail_side) {
                                 int side;
@@ -685,13 +693,22 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             const int n = s_count;
             // (TransH: 2 rows of 8 floats per lane in flight spill its step's registers; TransE keeps 2)
             // (1024-thread workgroups: half the rows per lane group, twice the lane groups; 128 VGPRs per lane)
-            constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? (MODEL == 1 || NT > 512 ? 1 : 2) : (NT > 512 ? 2 : 4));
+            // (r04: two rows per lane group in the hot kernels' 5-6-float shapes spill 28-68 B per lane, phase B
+            // of C3's D = 69 universe 5.9k -> 8.2k cycles per step)
+            // PT_UNI_BSPLIT: the hot kernels' phase B on lane groups of half the width (twice the floats per lane,
+            // twice the rows per round) - phase B's rounds are latency chains of a few dependent memory round trips
+            constexpr bool kSplitB = HOT && PT_UNI_BSPLIT != 0 && G >= 16 && VEC * KCH <= 8;
+            constexpr int GB = kSplitB ? G / 2 : G, KB = kSplitB ? 2 * KCH : KCH, GPBB = NT / GB;
+            constexpr bool EXB = !kSplitB;   // (the half-width shape's chunks are not all full for every dim)
+            using VecB = V<GB, VEC, KB>;
+            const int laneB = tid % GB, grpB = tid / GB;
+            constexpr int RB = VEC * KB >= 16 ? 1 : (VEC * KB > 4 ? (MODEL == 1 || NT > 512 ? 1 : 2) : (NT > 512 ? 2 : 4));
             constexpr bool kFastUpd = kUF && VEC * KCH <= 8;
             // (guards, not breaks, inside the unrolled loops: the row arrays must stay in registers)
             PT_USTAMP(tr, 47);
-            for (int i0 = grp * RB; i0 < n; i0 += GPB * RB) {
-                if (i0 / (GPB * RB) < 14) PT_USTAMP(tr, 48 + i0 / (GPB * RB));
-                Vec x[RB], gs[RB], a[RB], y[RB];
+            for (int i0 = grpB * RB; i0 < n; i0 += GPBB * RB) {
+                if (i0 / (GPBB * RB) < 14) PT_USTAMP(tr, 48 + i0 / (GPBB * RB));
+                VecB x[RB], gs[RB], a[RB], y[RB];
                 int32_t code[RB], c1[RB];
 #pragma unroll
                 for (int u = 0; u < RB; ++u) {
@@ -702,18 +719,18 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                         const int row = code[u] >> 2;
                         const float *wp = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
                         const float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
-                        uload(x[u], wp, (int)D, lane);
-                        if (opt != 0) uload(a[u], ap, (int)D, lane);
+                        uload<EXB>(x[u], wp, (int)D, laneB);
+                        if (opt != 0) uload<EXB>(a[u], ap, (int)D, laneB);
                         if ((table == 0 && contrib) || (table > 0 && rel_list)) {
                             // the row's contributions (linked in LDS): the first two loads issued with the
                             // row's own, the rest walked below; summed in list order
                             const int32_t c0 = s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row];
-                            uload(gs[u], U.contrib + c0 * D, (int)D, lane);
+                            uload<EXB>(gs[u], U.contrib + c0 * D, (int)D, laneB);
                             c1[u] = s_next[c0];
-                            if (c1[u] >= 0) uload(y[u], U.contrib + c1[u] * D, (int)D, lane);
+                            if (c1[u] >= 0) uload<EXB>(y[u], U.contrib + c1[u] * D, (int)D, laneB);
                         } else {
                             vload(gs[u], (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D,
-                                  (int)D, lane);
+                                  (int)D, laneB);
                         }
                     }
                 }
@@ -721,11 +738,11 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                 for (int u = 0; u < RB; ++u) {
                     if (code[u] >= 0 && c1[u] >= 0) {
 #pragma unroll
-                        for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
+                        for (int j = 0; j < VecB::N; ++j) gs[u].x[j] += y[u].x[j];
                         for (int32_t c = s_next[c1[u]]; c >= 0; c = s_next[c]) {
-                            uload(y[u], U.contrib + c * D, (int)D, lane);
+                            uload<EXB>(y[u], U.contrib + c * D, (int)D, laneB);
 #pragma unroll
-                            for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
+                            for (int j = 0; j < VecB::N; ++j) gs[u].x[j] += y[u].x[j];
                         }
                     }
                 }
@@ -738,7 +755,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
                     // ent rows of TransE and every rel / norm_vector row carry normalized-space gradients
                     const bool jac = table == 0 ? (MODEL == 0 && norm_flag) : (table == 1 ? norm_flag != 0 : true);
-                    Vec gg;
+                    VecB gg;
                     if (jac) {
                         const float nx = fsqrt<kFastUpd>(vdot(x[u], x[u]));
                         unormalize_bwd<kFastUpd>(x[u], nx, gs[u], gg);
@@ -747,27 +764,27 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     }
                     if (opt == 0) {
 #pragma unroll
-                        for (int j = 0; j < Vec::N; ++j) x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j];
+                        for (int j = 0; j < VecB::N; ++j) x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j];
                     } else {
 #pragma unroll
-                        for (int j = 0; j < Vec::N; ++j) {
+                        for (int j = 0; j < VecB::N; ++j) {
                             a[u].x[j] = a[u].x[j] + gg.x[j] * gg.x[j];
                             if constexpr (kFastUpd)
                                 x[u].x[j] = x[u].x[j] + (-U.lr) * (gg.x[j] * frcp<true>(fsqrt<true>(a[u].x[j]) + 1e-10f));
                             else
                                 x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j] / (sqrtf(a[u].x[j]) + 1e-10f);
                         }
-                        ustore(a[u], ap, (int)D, lane);
+                        ustore<EXB>(a[u], ap, (int)D, laneB);
                     }
-                    ustore(x[u], wp, (int)D, lane);
+                    ustore<EXB>(x[u], wp, (int)D, laneB);
                     if ((table == 0 && contrib) || (table > 0 && rel_list)) {
-                        if (lane == 0) s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row] = -1;
+                        if (laneB == 0) s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row] = -1;
                     } else {
-                        Vec z;
+                        VecB z;
                         vzero(z);
                         vstore(z, (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D, (int)D,
-                               lane);
-                        if (lane == 0) (table == 0 ? sink.fent : (table == 1 ? sink.frel : sink.fnorm))[row] = 0;
+                               laneB);
+                        if (laneB == 0) (table == 0 ? sink.fent : (table == 1 ? sink.frel : sink.fnorm))[row] = 0;
                     }
                 }
             }
@@ -865,7 +882,8 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
     case ID_:                                                                                          \
         if constexpr ((CLS < kUniHotBase ? PT_UCLASS(V_, K_) == CLS : ID_ == CLS - kUniHotBase) &&     \
                       shape_reachable(MODEL, G_, V_, K_))                                               \
-            universe_run<MODEL, G_, V_, K_, NT, PLAN>(U, p_norm, norm_flag, opt, (int)neg, bern, filter, cfg, S); \
+            universe_run<MODEL, G_, V_, K_, NT, PLAN, (CLS >= kUniHotBase)>(U, p_norm, norm_flag, opt, \
+                                                                                   (int)neg, bern, filter, cfg, S); \
         break;
             PT_USHAPES(PT_URUN)
 #undef PT_URUN
