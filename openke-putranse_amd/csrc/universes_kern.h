@@ -102,22 +102,18 @@ constexpr bool exact_kch_shape(int G, int VEC) { return G >= (VEC == 4 ? 2 : 4) 
 #ifndef PT_UNI_GLOBAL
 #define PT_UNI_GLOBAL 2
 #endif
-#ifndef PT_UNI_BSPLIT
-#define PT_UNI_BSPLIT 0
-#endif
 constexpr bool uni_global(int floats) { return PT_UNI_GLOBAL == 1 || (PT_UNI_GLOBAL == 2 && floats <= 8); }
 template <int G, int VEC, int KCH>
 constexpr int full_chunks() { return exact_kch_shape(G, VEC) ? KCH - 1 : 0; }
 
-// (EX = false: no chunk assumed full - a lane shape used for a dim range its pick_universe_shape did not make)
-template <bool EX = true, int G, int VEC, int KCH>
+template <int G, int VEC, int KCH>
 __device__ __forceinline__ void uload(V<G, VEC, KCH> &o, const float *row_, int D, int lane) {
     if constexpr (!uni_global(VEC * KCH)) {
         vload(o, row_, D, lane);
         return;
     }
     const gfloat *row = (const gfloat *)(const void *)row_;
-    constexpr int F = EX ? full_chunks<G, VEC, KCH>() : 0;
+    constexpr int F = full_chunks<G, VEC, KCH>();
 #pragma unroll
     for (int k = 0; k < KCH; ++k) {
         const int c = k * G + lane;
@@ -137,14 +133,14 @@ __device__ __forceinline__ void uload(V<G, VEC, KCH> &o, const float *row_, int 
     }
 }
 
-template <bool EX = true, int G, int VEC, int KCH>
+template <int G, int VEC, int KCH>
 __device__ __forceinline__ void ustore(const V<G, VEC, KCH> &o, float *row_, int D, int lane) {
     if constexpr (!uni_global(VEC * KCH)) {
         vstore(o, row_, D, lane);
         return;
     }
     gfloat *row = (gfloat *)(void *)row_;
-    constexpr int F = EX ? full_chunks<G, VEC, KCH>() : 0;
+    constexpr int F = full_chunks<G, VEC, KCH>();
 #pragma unroll
     for (int k = 0; k < KCH; ++k) {
         const int c = k * G + lane;
@@ -695,20 +691,15 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // (1024-thread workgroups: half the rows per lane group, twice the lane groups; 128 VGPRs per lane)
             // (r04: two rows per lane group in the hot kernels' 5-6-float shapes spill 28-68 B per lane, phase B
             // of C3's D = 69 universe 5.9k -> 8.2k cycles per step)
-            // PT_UNI_BSPLIT: the hot kernels' phase B on lane groups of half the width (twice the floats per lane,
-            // twice the rows per round) - phase B's rounds are latency chains of a few dependent memory round trips
-            constexpr bool kSplitB = HOT && PT_UNI_BSPLIT != 0 && G >= 16 && VEC * KCH <= 8;
-            constexpr int GB = kSplitB ? G / 2 : G, KB = kSplitB ? 2 * KCH : KCH, GPBB = NT / GB;
-            constexpr bool EXB = !kSplitB;   // (the half-width shape's chunks are not all full for every dim)
-            using VecB = V<GB, VEC, KB>;
-            const int laneB = tid % GB, grpB = tid / GB;
-            constexpr int RB = VEC * KB >= 16 ? 1 : (VEC * KB > 4 ? (MODEL == 1 || NT > 512 ? 1 : 2) : (NT > 512 ? 2 : 4));
+            // (r04: the hot kernels' phase B on lane groups of half the width - twice the floats per lane, twice the
+            // rows per round: phase B of C3's D = 68 universe 4.3k -> 14.2k, of C4's longest 23k -> 89k cycles per step)
+            constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? (MODEL == 1 || NT > 512 ? 1 : 2) : (NT > 512 ? 2 : 4));
             constexpr bool kFastUpd = kUF && VEC * KCH <= 8;
             // (guards, not breaks, inside the unrolled loops: the row arrays must stay in registers)
             PT_USTAMP(tr, 47);
-            for (int i0 = grpB * RB; i0 < n; i0 += GPBB * RB) {
-                if (i0 / (GPBB * RB) < 14) PT_USTAMP(tr, 48 + i0 / (GPBB * RB));
-                VecB x[RB], gs[RB], a[RB], y[RB];
+            for (int i0 = grp * RB; i0 < n; i0 += GPB * RB) {
+                if (i0 / (GPB * RB) < 14) PT_USTAMP(tr, 48 + i0 / (GPB * RB));
+                Vec x[RB], gs[RB], a[RB], y[RB];
                 int32_t code[RB], c1[RB];
 #pragma unroll
                 for (int u = 0; u < RB; ++u) {
@@ -719,18 +710,18 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                         const int row = code[u] >> 2;
                         const float *wp = (table == 0 ? U.ent : (table == 1 ? U.rel : U.normv)) + row * D;
                         const float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
-                        uload<EXB>(x[u], wp, (int)D, laneB);
-                        if (opt != 0) uload<EXB>(a[u], ap, (int)D, laneB);
+                        uload(x[u], wp, (int)D, lane);
+                        if (opt != 0) uload(a[u], ap, (int)D, lane);
                         if ((table == 0 && contrib) || (table > 0 && rel_list)) {
                             // the row's contributions (linked in LDS): the first two loads issued with the
                             // row's own, the rest walked below; summed in list order
                             const int32_t c0 = s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row];
-                            uload<EXB>(gs[u], U.contrib + c0 * D, (int)D, laneB);
+                            uload(gs[u], U.contrib + c0 * D, (int)D, lane);
                             c1[u] = s_next[c0];
-                            if (c1[u] >= 0) uload<EXB>(y[u], U.contrib + c1[u] * D, (int)D, laneB);
+                            if (c1[u] >= 0) uload(y[u], U.contrib + c1[u] * D, (int)D, lane);
                         } else {
                             vload(gs[u], (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D,
-                                  (int)D, laneB);
+                                  (int)D, lane);
                         }
                     }
                 }
@@ -738,11 +729,11 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                 for (int u = 0; u < RB; ++u) {
                     if (code[u] >= 0 && c1[u] >= 0) {
 #pragma unroll
-                        for (int j = 0; j < VecB::N; ++j) gs[u].x[j] += y[u].x[j];
+                        for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
                         for (int32_t c = s_next[c1[u]]; c >= 0; c = s_next[c]) {
-                            uload<EXB>(y[u], U.contrib + c * D, (int)D, laneB);
+                            uload(y[u], U.contrib + c * D, (int)D, lane);
 #pragma unroll
-                            for (int j = 0; j < VecB::N; ++j) gs[u].x[j] += y[u].x[j];
+                            for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
                         }
                     }
                 }
@@ -755,7 +746,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     float *ap = (table == 0 ? U.ent_acc : (table == 1 ? U.rel_acc : U.norm_acc)) + row * D;
                     // ent rows of TransE and every rel / norm_vector row carry normalized-space gradients
                     const bool jac = table == 0 ? (MODEL == 0 && norm_flag) : (table == 1 ? norm_flag != 0 : true);
-                    VecB gg;
+                    Vec gg;
                     if (jac) {
                         const float nx = fsqrt<kFastUpd>(vdot(x[u], x[u]));
                         unormalize_bwd<kFastUpd>(x[u], nx, gs[u], gg);
@@ -764,27 +755,27 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     }
                     if (opt == 0) {
 #pragma unroll
-                        for (int j = 0; j < VecB::N; ++j) x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j];
+                        for (int j = 0; j < Vec::N; ++j) x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j];
                     } else {
 #pragma unroll
-                        for (int j = 0; j < VecB::N; ++j) {
+                        for (int j = 0; j < Vec::N; ++j) {
                             a[u].x[j] = a[u].x[j] + gg.x[j] * gg.x[j];
                             if constexpr (kFastUpd)
                                 x[u].x[j] = x[u].x[j] + (-U.lr) * (gg.x[j] * frcp<true>(fsqrt<true>(a[u].x[j]) + 1e-10f));
                             else
                                 x[u].x[j] = x[u].x[j] + (-U.lr) * gg.x[j] / (sqrtf(a[u].x[j]) + 1e-10f);
                         }
-                        ustore<EXB>(a[u], ap, (int)D, laneB);
+                        ustore(a[u], ap, (int)D, lane);
                     }
-                    ustore<EXB>(x[u], wp, (int)D, laneB);
+                    ustore(x[u], wp, (int)D, lane);
                     if ((table == 0 && contrib) || (table > 0 && rel_list)) {
-                        if (laneB == 0) s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row] = -1;
+                        if (lane == 0) s_head[(table == 0 ? 0 : (table == 1 ? E : E + R)) + row] = -1;
                     } else {
-                        VecB z;
+                        Vec z;
                         vzero(z);
                         vstore(z, (table == 0 ? sink.gent : (table == 1 ? sink.grel : sink.gnorm)) + row * D, (int)D,
-                               laneB);
-                        if (laneB == 0) (table == 0 ? sink.fent : (table == 1 ? sink.frel : sink.fnorm))[row] = 0;
+                               lane);
+                        if (lane == 0) (table == 0 ? sink.fent : (table == 1 ? sink.frel : sink.fnorm))[row] = 0;
                     }
                 }
             }
