@@ -1126,8 +1126,10 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     const int64_t lds_budget = std::min<int64_t>(max_lds, 80 << 10) - 1024;
     // one persistent launch per row shape, its universes longest dependent step chain first (the work
     // queue then approximates longest-processing-time scheduling over the launch's workgroups)
+    // (the CU-share model below: a step costs a fixed part worth ~64 positives plus one unit per positive)
     auto work = [&](int64_t i) {
-        return (double)jobs[i].epochs * (double)jobs[i].nbatches * (double)std::max<int64_t>(jobs[i].batch_size, 1);
+        return (double)jobs[i].epochs * (double)jobs[i].nbatches *
+               (64.0 + (double)std::max<int64_t>(jobs[i].batch_size, 1));
     };
     std::vector<int64_t> order((size_t)n);
     for (int64_t i = 0; i < n; ++i) order[i] = i;
@@ -1180,26 +1182,25 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         set->groups.back().work += work(order[k]);
     }
     PT_CHECK(set->groups.size() <= 64, PT_EINVAL, "too many universe shape classes");
-    // CU shares: model a universe's time as steps x (fixed + rounds of its step's positives over the shape's
-    // lane groups); give every group one CU, then each further CU to the group whose LPT makespan over
-    // its current share is longest (the launches run concurrently, so the slowest group ends the set)
+    // CU shares: model a universe's time as steps x (fixed + its step's positives); give every group one CU,
+    // then each further CU to the group whose LPT makespan over its current share is longest (the launches run
+    // concurrently, so the slowest group ends the set)
     {
         int cus = 0;
         PT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, set->device));
-        // a step's cost in rounds of its positives: its fixed part (presampling, the two barriers, phase B)
-        // is worth ~4 rounds (per-universe phase cycles, PT_UNI_PROF: a one-round step costs ~3/4 of a
-        // four-round one); 1 -> 4 moved C3 from 62.1 to 53.9 ms (8: 54.3; one workgroup per universe with
-        // the dispatcher interleaving the class launches, PT_UNI_GRID=1: 59.8)
-        double uni_fixed = 4.0;
+        // a step's cost: a fixed part plus one unit per positive. Fitted to every universe's measured cycles per
+        // step (r04, PT_UNI_PROF dumps of C3 / C4: cycles/step = a + b x bs, a/b = 70 and 24 positives; the residual
+        // spread 15 %, against 21 % for the earlier fixed + rounds-of-positives model, whose shares left C3's float4
+        // hot launch ending 2 ms after the longest universe). PT_UNI_FIXED (tuning builds) overrides the fixed part.
+        double uni_fixed = 64.0;
         if (const char *v = pt_tuning_env("PT_UNI_FIXED")) uni_fixed = atof(v);
         std::vector<std::vector<double>> tg(set->groups.size());
         for (size_t k = 0; k < set->groups.size(); ++k) {
             const auto &gr = set->groups[k];
             for (int64_t q = gr.off; q < gr.off + gr.n; ++q) {
                 const pt_universe_job &J = jobs[order[q]];
-                const int64_t gpb = pt::universe_shape_groups(pt::universe_shape_id(J.dim, model), model);
-                const int64_t rounds = (std::max<int64_t>(J.batch_size, 1) + gpb - 1) / gpb;
-                tg[k].push_back((double)J.epochs * (double)J.nbatches * (double)(uni_fixed + rounds));
+                tg[k].push_back((double)J.epochs * (double)J.nbatches *
+                                (uni_fixed + (double)std::max<int64_t>(J.batch_size, 1)));
             }
             std::sort(tg[k].begin(), tg[k].end(), std::greater<double>());
         }
