@@ -1126,10 +1126,14 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     const int64_t lds_budget = std::min<int64_t>(max_lds, 80 << 10) - 1024;
     // one persistent launch per row shape, its universes longest dependent step chain first (the work
     // queue then approximates longest-processing-time scheduling over the launch's workgroups)
-    // (the CU-share model below: a step costs a fixed part worth ~64 positives plus one unit per positive)
+    // A universe's time (the CU-share model and the queue order): steps x cycles per step, a fixed part plus a
+    // per-positive part that grows with the padded row (lanes x floats per lane) - fitted to every universe's
+    // measured cycles per step (r04, PT_UNI_PROF dumps of C3 and C4: 6,587 + bs x (63.3 + 0.681 x row slots);
+    // residual spread 18 % / 14 %, against 21 % / 20 % for the earlier fixed + rounds-of-positives model)
     auto work = [&](int64_t i) {
+        const int rs = pt::universe_shape_row_slots(pt::universe_shape_id(jobs[i].dim, model));
         return (double)jobs[i].epochs * (double)jobs[i].nbatches *
-               (64.0 + (double)std::max<int64_t>(jobs[i].batch_size, 1));
+               (6587.0 + (double)std::max<int64_t>(jobs[i].batch_size, 1) * (63.3 + 0.681 * rs));
     };
     std::vector<int64_t> order((size_t)n);
     for (int64_t i = 0; i < n; ++i) order[i] = i;
@@ -1182,26 +1186,18 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         set->groups.back().work += work(order[k]);
     }
     PT_CHECK(set->groups.size() <= 64, PT_EINVAL, "too many universe shape classes");
-    // CU shares: model a universe's time as steps x (fixed + its step's positives); give every group one CU,
+    // CU shares: a universe's time by the step-cost model (`work`); give every group one CU,
     // then each further CU to the group whose LPT makespan over its current share is longest (the launches run
     // concurrently, so the slowest group ends the set)
     {
         int cus = 0;
         PT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, set->device));
-        // a step's cost: a fixed part plus one unit per positive. Fitted to every universe's measured cycles per
-        // step (r04, PT_UNI_PROF dumps of C3 / C4: cycles/step = a + b x bs, a/b = 70 and 24 positives; the residual
-        // spread 15 %, against 21 % for the earlier fixed + rounds-of-positives model, whose shares left C3's float4
-        // hot launch ending 2 ms after the longest universe). PT_UNI_FIXED (tuning builds) overrides the fixed part.
-        double uni_fixed = 64.0;
-        if (const char *v = pt_tuning_env("PT_UNI_FIXED")) uni_fixed = atof(v);
+        // (the step-cost model of `work`: with it the shares no longer leave C3's float4 hot launch ending 2 ms after
+        // the longest universe, which the rounds-of-positives model did)
         std::vector<std::vector<double>> tg(set->groups.size());
         for (size_t k = 0; k < set->groups.size(); ++k) {
             const auto &gr = set->groups[k];
-            for (int64_t q = gr.off; q < gr.off + gr.n; ++q) {
-                const pt_universe_job &J = jobs[order[q]];
-                tg[k].push_back((double)J.epochs * (double)J.nbatches *
-                                (uni_fixed + (double)std::max<int64_t>(J.batch_size, 1)));
-            }
+            for (int64_t q = gr.off; q < gr.off + gr.n; ++q) tg[k].push_back(work(order[q]));
             std::sort(tg[k].begin(), tg[k].end(), std::greater<double>());
         }
         auto makespan = [&](size_t k, int64_t s) {

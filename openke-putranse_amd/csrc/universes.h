@@ -72,5 +72,6 @@ hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, in
                             const UniverseLaunch &cfg, hipStream_t st);
 int universe_shape_class(int shape);
 int universe_shape_groups(int shape, int model);
+int universe_shape_row_slots(int shape);
 
 }  // namespace pt

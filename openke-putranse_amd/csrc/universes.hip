@@ -53,6 +53,15 @@ int universe_shape_groups(int shape, int model) {
     return 1;
 }
 
+// padded row length of a row shape (lanes x floats per lane: the floats a lane group touches per row)
+int universe_shape_row_slots(int shape) {
+#define PT_URS(ID_, G_, V_, K_) \
+    if (shape == ID_) return G_ * V_ * K_;
+    PT_USHAPES(PT_URS)
+#undef PT_URS
+    return 1;
+}
+
 // the LDS plan the launch configuration amounts to (universe_run's PLAN): 1 and 2 are compiled apart with
 // their choices fixed, anything else takes the general kernel
 static int universe_plan(const UniverseLaunch &cfg) {
