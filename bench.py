@@ -6,7 +6,10 @@ batch 2000, 25 negatives per positive, L2 norm, SGD (alpha 1.0, margin 5), bern 
 of 2000 positives x (1 + 25) slots, NegativeSampling + MarginLoss forward, backward, SGD update of the
 touched rows. Inputs (graph, tables) are resident in HBM before timing starts.
 
-  python bench.py [--gpus N --steps K --warmup W]       (N > 1 under torch.distributed.run)
+  python bench.py [--gpus N --steps K --warmup W]
+
+N > 1: bench.py runs as one rank per GPU; started without a torch.distributed environment it launches the N
+ranks itself (torch.distributed.run, 127.0.0.1) before touching the GPU and relays rank 0's line.
 
 C2 is a single model, so N > 1 runs N independent replicas (one per GPU, "replicas only", weak
 scaling, no collective in the data path); value = slots of all ranks / max-over-ranks time.
@@ -64,6 +67,42 @@ def dist_setup():
     else:
         torch.cuda.set_device(0)
     return ws, rank, local
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` (N > 1) started without a torch.distributed environment: start N fresh ranks under
+    torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) with the same arguments, relay their output
+    and return their exit status. Runs before anything in this process touches the GPU (the parent only counts
+    devices), and starts the ranks as children: a GPU-initialised process is never replaced."""
+    import socket
+    import subprocess
+    backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
+    if backend == "nccl":
+        have = torch.cuda.device_count()
+        if have < n:
+            print("bench.py: --gpus %d needs %d visible GPUs, found %d" % (n, n, have), file=sys.stderr)
+            return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    line = None
+    for ln in p.stdout.splitlines():
+        print(ln, flush=True)
+        if ln.startswith("{"):
+            line = ln
+    if p.returncode != 0:
+        return p.returncode
+    try:
+        got = json.loads(line)["n_gpus"] if line else None
+    except ValueError:
+        got = None
+    if got != n:
+        print("bench.py: --gpus %d but the ranks reported n_gpus %s" % (n, got), file=sys.stderr)
+        return 3
+    return 0
 
 
 def barrier(ws):
@@ -162,6 +201,8 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
     from openke import _native
     L = _native.lib()
     shape, n_univ, model, dim_spec, p_norm, tc_range, margin_range, do_lp = PU_WORKLOADS[name]
+    if getattr(args, "universes", 0):   # --universes: the reference experiment's own count (e.g. 6,000)
+        n_univ = args.universes
     if per_gpu:   # weak scaling: the workload's universe count on EVERY GPU (universes 4+k continue the seeds)
         n_univ *= ws
         do_lp = False
@@ -270,9 +311,30 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
         assert torch.isfinite(losses).all(), "non-finite universe loss"
         return el
 
+    def launch_times(us):
+        """The set's concurrent class launches in its last training (pt_universe_set_launch_times): per launch
+        start / end (ms after the first start) and universes, and their overlap = summed launch time over the span
+        (the launch count when all run side by side from the start, 1.0 when they run one after another)."""
+        if not hasattr(L, "pt_universe_set_launch_times"):
+            return None
+        n = ctypes.c_int64(0)
+        _native.check(L.pt_universe_set_launch_times(us, 0, None, ctypes.byref(n)))
+        if n.value == 0:
+            return None
+        buf = np.zeros(3 * n.value, dtype=np.float32)
+        _native.check(L.pt_universe_set_launch_times(us, n.value, buf.ctypes.data, ctypes.byref(n)))
+        rows = buf.reshape(-1, 3)
+        span = float(rows[:, 1].max() - rows[:, 0].min())
+        return {"launches": [[round(float(a), 3), round(float(b), 3), int(c)] for a, b, c in rows],
+                "span_ms": span, "overlap": float((rows[:, 1] - rows[:, 0]).sum()) / max(span, 1e-9),
+                "latest_start_ms": float(rows[:, 0].max()),
+                "note": "[start ms, end ms, universes] per class launch of the last timed training (HIP events on "
+                        "each launch's stream); overlap = summed launch time / span"}
+
     every = list(range(len(jobs)))
     uset, reset = make_set(every)
     el = time_set(uset, reset, every, args.c3_steps, args.c3_warmup)
+    class_launches = launch_times(uset)
     tot = torch.tensor([el, float(slots_step), float(bytes_step)], dtype=torch.float64, device=dev)
     if ws > 1:
         import torch.distributed as dist
@@ -359,6 +421,8 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
                                 "measurement: a universe's working set (tables, Adagrad state, contribution rows, "
                                 "a few hundred KB) is cache-resident and its work lists, relation gradient rows and "
                                 "presampled batches live in LDS, so frac > 1 (C4) means on-chip service"}}
+    if class_launches is not None:
+        out["class_launches"] = class_launches
     if det_s is not None:
         out["deterministic_s_per_step"] = det_s
         out["deterministic_triples_per_s"] = slots_step / det_s
@@ -390,6 +454,9 @@ def run_dropin(args, ws, rank, dev, name="c3"):
     from openke.data import TestDataLoader, TrainDataLoader
     from openke.module.model import TransE, TransH
     shape, n_univ, model, dim_spec, p_norm, tc_range, margin_range, do_lp = PU_WORKLOADS[name]
+    if getattr(args, "universes", 0):
+        n_univ = args.universes
+    valid_steps = args.valid_steps if getattr(args, "valid_steps", 0) else max(n_univ // 4, 1)
     path = synth_kg.ensure_dataset(os.path.join(args.data_dir, "rank%d" % rank), shape)
     t0 = time.perf_counter()
     train_dl = TrainDataLoader(in_path=path, nbatches=20, threads=8, sampling_mode="normal", bern_flag=0,
@@ -403,7 +470,7 @@ def run_dropin(args, ws, rank, dev, name="c3"):
         max_triple_constraint=tc_range[1], min_balance=0.25, max_balance=0.5,
         embedding_model=TransE if model == "TransE" else TransH,
         embedding_model_param={"dim": dim_spec, "p_norm": p_norm, "norm_flag": 1},
-        checkpoint_dir=ck, valid_steps=max(n_univ // 4, 1), save_steps=10000, training_setting="static",
+        checkpoint_dir=ck, valid_steps=valid_steps, save_steps=10000, training_setting="static",
         incremental_strategy=None)
     setup_s = time.perf_counter() - t0
     torch.cuda.synchronize()
@@ -413,7 +480,7 @@ def run_dropin(args, ws, rank, dev, name="c3"):
     torch.cuda.synchronize()
     barrier(ws)
     train_s = time.perf_counter() - t0
-    out = {"setup_s": setup_s, "train_parallel_universes_s": train_s, "wave_size": cfg.wave_size(),
+    out = {"universes": n_univ, "setup_s": setup_s, "train_parallel_universes_s": train_s, "wave_size": cfg.wave_size(),
            "valid_steps": cfg.valid_steps, "universes_committed": cfg.next_universe_id,
            "breakdown_s": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in cfg.last_train_timing.items()}}
     if do_lp:
@@ -602,9 +669,39 @@ def main():
     ap.add_argument("--step-apply", type=int, default=0,
                     help="C2 / C1: 1 = the fused step + apply kernel where it applies (opt-in, measured slower), 0 = "
                          "the step + apply pair (default; pt_trainer_set_step_apply)")
+    ap.add_argument("--universes", type=int, default=0,
+                    help="universe workloads: this many universes instead of the config's (the reference experiment "
+                         "trains 6,000: experiments/static_experiment_PuTransE_on_WN18.py:84-91)")
+    ap.add_argument("--valid-steps", type=int, default=0,
+                    help="drop-in leg: validate every this many universes (default: a quarter of the universes; the "
+                         "reference experiment uses 100)")
     ap.add_argument("--no-dropin", action="store_true",
                     help="universe workloads: skip the drop-in Parallel_Universe_Config timing")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, check the world size against --gpus, print it and stop (no GPU work)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        print("bench.py: WORLD_SIZE %s differs from --gpus %d" % (os.environ.get("WORLD_SIZE", "1"), args.gpus),
+              file=sys.stderr)
+        sys.exit(3)
+    if args.launch_check:
+        ws = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        if ws > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            ws_seen = int(t.item())
+            dist.destroy_process_group()
+        else:
+            ws_seen = 1
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": ws_seen, "world_size_env": ws}), flush=True)
+        return
 
     ws, rank, local = dist_setup()
     if args.workload in PU_WORKLOADS:
@@ -624,7 +721,7 @@ def main():
                 rec["link_prediction"] = c3["link_prediction"]
             if dropin is not None:
                 rec["dropin"] = dropin
-            for k in ("placement", "deterministic_s_per_step", "deterministic_triples_per_s", "longest_universe_cycles",
+            for k in ("placement", "class_launches", "deterministic_s_per_step", "deterministic_triples_per_s", "longest_universe_cycles",
                       "note_runs", "host_universe_build_s"):
                 if k in c3:
                     rec[k] = c3[k]

@@ -227,6 +227,11 @@ int pt_universe_set_states(pt_universe_set *s, int64_t job, uint64_t *out);
 /* every job's LCG states back to their values at pt_universe_set_create (re-running the same trainings from the
  * same start, e.g. a benchmark's repeats; the caller restores tables and optimizer state) */
 int pt_universe_set_reset(pt_universe_set *s);
+/* the concurrent class launches of the last fast-path train call: *n_out = their count; out (when not NULL,
+ * cap >= count): per launch {start ms, end ms, universes}, times relative to the earliest start (HIP timing events
+ * on each launch's stream). The launches run on process-wide streams with hardware queues of their own, so they
+ * overlap regardless of the caller's own streams. */
+int pt_universe_set_launch_times(pt_universe_set *s, int64_t cap, float *out, int64_t *n_out);
 /* 1 when universes of embedding dim `dim` train on the fast universe kernels (model PT_TRANSE / PT_TRANSH),
  * else 0 (pt_universe_set_create then fails with PT_EINVAL). No device call. */
 int pt_universe_dim_supported(int64_t dim, int32_t model);

@@ -343,6 +343,16 @@ static int choose_path(const pt_trainer *t, int64_t calls, int64_t bs, int64_t n
     return PT_PATH_TWO_PASS;
 }
 
+// whether the fused step + apply is wanted for this trainer (opt-in, pt_trainer_set_step_apply; the tuning build's
+// PT_STEP_APPLY=0 vetoes it): only then does ensure_csr carve its extra state
+static bool step_apply_wanted(const pt_trainer *t) {
+    static const int forced = [] {
+        const char *v = pt_tuning_env("PT_STEP_APPLY");
+        return v ? atoi(v) : -1;
+    }();
+    return t->step_apply_on && forced != 0;
+}
+
 // Workspace of the counting-sort path, carved once per (bs, neg): room for a chunk of pre-sampled
 // steps (<= kCsrChunk, fewer when a step's arrays are large) plus one step's gradient rows. A new
 // (bs, neg) re-carves it (and drops captured graphs, whose kernels hold the old pointers).
@@ -356,7 +366,7 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     pt::StepParams Q = t->P;
     Q.batch_size = bs;
     Q.neg = neg;
-    const bool sa = pt::step_apply_supported(Q, bs, neg);
+    const bool sa = step_apply_wanted(t) && pt::step_apply_supported(Q, bs, neg);
     const int64_t dp = sa ? pt::step_apply_row_stride(D) : D, us = (E + R + 63) & ~int64_t(63);
     const size_t per_call = 16 * bs + 8 * bs * neg + 4 * cs + 4 * ss + 4 + 1024 + (sa ? 4 * us + 4 * bs : 0);
     int64_t chunk = (int64_t)std::max<size_t>(1, ((size_t)512 << 20) / per_call);
@@ -489,12 +499,7 @@ static int enqueue_sample_chunk(pt_trainer *t, pt_sampler *s, pt::CsrWork &w, in
 
 // whether in-kernel-sampled steps of P take the fused step + apply (carved for in ensure_csr)
 static bool step_apply_on(const pt_trainer *t, const pt::StepParams &P) {
-    static const int forced = [] {
-        const char *v = pt_tuning_env("PT_STEP_APPLY");
-        return v ? atoi(v) : -1;
-    }();
-    if (forced == 0) return false;
-    return t->step_apply_on && t->fr.gent && t->csr.uses && pt::step_apply_supported(P, P.batch_size, P.neg);
+    return step_apply_wanted(t) && t->fr.gent && t->csr.uses && pt::step_apply_supported(P, P.batch_size, P.neg);
 }
 
 // Enqueue `steps` in-kernel-sampled steps; step i adds its loss to d_losses[i]. Large neg takes the
@@ -522,6 +527,9 @@ static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, in
             if (rc) return rc;
             t->csr.rank_only = w.rank_only;   // (read by pt_trainer_run_timed's re-timing of the last batch)
             if (sa) {   // one launch per step, then the chunk's losses
+                // arrival words back to zero every chunk (the last arriver of a row also clears its word): a step
+                // whose arrivals ever miss a row (an aborted launch) cannot carry over past its chunk
+                PT_HIP(hipMemsetAsync(t->fr.arrive, 0, 8 * (size_t)(t->P.ent_total + t->P.rel_total), st));
                 for (int64_t j = 0; j < calls; ++j)
                     PT_TIMED(2, pt::launch_step_apply(P, pt::csr_view(w, j, bs, neg), t->fr, st));
                 if (d_losses)
@@ -826,6 +834,7 @@ extern "C" int pt_trainer_run_timed(pt_trainer *t, pt_sampler *s, int64_t bs, in
 
 extern "C" int pt_trainer_set_step_apply(pt_trainer *t, int32_t on) {
     PT_CHECK(t, PT_EINVAL, "null trainer");
+    if (t->step_apply_on != (on != 0)) t->csr_bs = 0;   // re-carve the workspace: the fused kernel's state only when on
     t->step_apply_on = on != 0;
     t->drop_graphs();   // captured epochs hold the previous choice
     return PT_OK;
@@ -1032,6 +1041,60 @@ extern "C" int pt_universe_seeds(const pt_universe *u, uint64_t *seeds) {
     return PT_OK;
 }
 
+// Streams of the universe trainer's concurrent class launches: created once per device for the whole process
+// and shared by every set. Each is created with a CU mask that covers every CU: the runtime gives such a stream
+// a hardware queue of its own instead of sharing one of the process's GPU_MAX_HW_QUEUES (4) queues with the
+// caller's streams. With plain streams, a process that already held streams of its own (torch's, the C2 trainer's
+// capture stream) got two class launches on one queue, where they ran one after the other (round 4: the C3 set
+// 58.7 ms in the default bench process against 35.7 ms standalone).
+namespace {
+struct ClassStreamPool {
+    std::mutex mu;
+    std::map<std::pair<int, int>, std::vector<hipStream_t>> by_dev;   // (device, mode) -> streams
+};
+ClassStreamPool &class_stream_pool() {
+    static ClassStreamPool *p = new ClassStreamPool();   // never destroyed: streams outlive every set
+    return *p;
+}
+// mode 1: full-CU-mask streams (dedicated hardware queues; the product's choice); tuning builds also take
+// PT_UNI_STREAMS = 0 (round 4: per-set plain side streams, class 0 on the caller's stream), 2 (highest-priority
+// streams: their own queue pool), 3 (plain library streams)
+int class_stream_mode() {
+    static const int m = [] {
+        const char *v = pt_tuning_env("PT_UNI_STREAMS");
+        return v ? atoi(v) : 1;
+    }();
+    return m;
+}
+hipError_t class_streams(int device, int mode, size_t n, std::vector<hipStream_t> *out) {
+    ClassStreamPool &P = class_stream_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto &v = P.by_dev[{device, mode}];
+    while (v.size() < n) {
+        hipStream_t q = nullptr;
+        hipError_t e = hipSuccess;
+        if (mode == 1) {
+            int cus = 0;
+            e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+            if (e != hipSuccess) return e;
+            std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+            for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+            e = hipExtStreamCreateWithCUMask(&q, (uint32_t)mask.size(), mask.data());
+        } else if (mode == 2) {
+            int lo = 0, hi = 0;
+            e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+            if (e == hipSuccess) e = hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi);
+        } else {
+            e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
+        }
+        if (e != hipSuccess) return e;
+        v.push_back(q);
+    }
+    out->assign(v.begin(), v.begin() + (std::ptrdiff_t)n);
+    return hipSuccess;
+}
+}  // namespace
+
 // Train many universes with the persistent multi-universe kernel (universes.hip).
 struct pt_universe_set {
     int32_t model = 0, p_norm = 1, norm_flag = 1, opt = PT_ADAGRAD;
@@ -1047,8 +1110,10 @@ struct pt_universe_set {
         int64_t share = 1;   // workgroups (= CUs) of its launch
     };
     std::vector<Group> groups;            // runs of d_us with one shape class (one kernel launch each)
-    std::vector<hipStream_t> streams;     // side streams of the group launches (created on first train)
+    std::vector<hipStream_t> streams;     // PT_UNI_STREAMS=0 only: per-set side streams (else the process pool's)
     std::vector<hipEvent_t> events;
+    std::vector<hipEvent_t> t_start, t_stop;   // per group launch: timing events of the last train call
+    bool timed = false;                        // the last train call recorded them
     pt::UniverseLaunch cfg;
     std::vector<pt::UniverseDev> host;    // same order; loss pointers patched per train call
     std::vector<int64_t> host_loss_off;
@@ -1062,6 +1127,8 @@ struct pt_universe_set {
     int64_t ord_max_seq = 0;
     ~pt_universe_set() {
         for (auto e : events) (void)hipEventDestroy(e);
+        for (auto e : t_start) (void)hipEventDestroy(e);
+        for (auto e : t_stop) (void)hipEventDestroy(e);
         for (auto q : streams) (void)hipStreamDestroy(q);
         if (arena) (void)hipFree(arena);
         if (prof) (void)hipFree(prof);
@@ -1123,7 +1190,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     // slower: C5 37.6 -> 352 ms, C4 104 -> 107 ms, C3 unchanged.)
     int max_lds = 64 << 10;
     (void)hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, set->device);
-    const int64_t lds_budget = std::min<int64_t>(max_lds, 80 << 10) - 1024;
+    const int64_t lds_budget = std::min<int64_t>(max_lds, 80 << 10) - 1024 - 2048;   // (2 KB: the static PreTables)
     // one persistent launch per row shape, its universes longest dependent step chain first (the work
     // queue then approximates longest-processing-time scheduling over the launch's workgroups)
     // A universe's time (the CU-share model and the queue order): steps x cycles per step, a fixed part plus a
@@ -1404,25 +1471,42 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
         PT_HIP(hipStreamSynchronize(st));
         return PT_OK;
     }
-    // one launch per shape class, concurrently on a side stream, each over its share of the CUs (set at
-    // creation); joined back into `st`
+    // one launch per shape class, concurrently, each over its share of the CUs (set at creation): forked from `st`
+    // onto the process's class streams (each on a hardware queue of its own, class_streams) and joined back, so
+    // the launches overlap whatever streams the caller's process already holds
     const size_t ng = set->groups.size();
-    while (set->streams.size() + 1 < ng) {
-        hipStream_t q;
-        PT_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-        set->streams.push_back(q);
+    const int smode = class_stream_mode();
+    std::vector<hipStream_t> qs(ng);
+    if (smode == 0) {   // round 4's scheme (tuning A/B): class 0 on `st`, the others on per-set side streams
+        while (set->streams.size() + 1 < ng) {
+            hipStream_t q;
+            PT_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+            set->streams.push_back(q);
+        }
+        for (size_t k = 0; k < ng; ++k) qs[k] = k == 0 ? st : set->streams[k - 1];
+    } else {
+        PT_HIP(class_streams(set->device, smode, ng, &qs));
     }
-    while (set->events.size() < ng) {
+    while (set->events.size() < ng + 1) {
         hipEvent_t ev;
         PT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         set->events.push_back(ev);
     }
+    while (set->t_start.size() < ng) {
+        hipEvent_t a, b;
+        PT_HIP(hipEventCreate(&a));
+        PT_HIP(hipEventCreate(&b));
+        set->t_start.push_back(a);
+        set->t_stop.push_back(b);
+    }
     PT_HIP(hipEventRecord(set->events[0], st));
-    for (size_t k = 1; k < ng; ++k) PT_HIP(hipStreamWaitEvent(set->streams[k - 1], set->events[0], 0));
+    for (size_t k = 0; k < ng; ++k)
+        if (qs[k] != st) PT_HIP(hipStreamWaitEvent(qs[k], set->events[0], 0));
     for (size_t k = 0; k < ng; ++k) {
         const auto &gr = set->groups[k];
         const int64_t share = gr.share;
-        hipStream_t q = k == 0 ? st : set->streams[k - 1];
+        hipStream_t q = qs[k];
+        PT_HIP(hipEventRecord(set->t_start[k], q));
         // PT_UNI_GRID=1 (tuning): one workgroup per universe in every launch, the hardware dispatcher
         // interleaving the class launches as CUs free up, instead of a CU share per launch
         static const bool per_universe = [] {
@@ -1434,13 +1518,41 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
                                                   set->model, set->p_norm, set->norm_flag, set->opt, set->neg,
                                                   (int)set->bern, (int)set->filter, set->cfg, q);
         if (e != hipSuccess) return pt::fail(PT_EHIP, std::string("launch_universes: ") + hipGetErrorString(e));
+        PT_HIP(hipEventRecord(set->t_stop[k], q));
     }
-    for (size_t k = 1; k < ng; ++k) {
-        PT_HIP(hipEventRecord(set->events[k], set->streams[k - 1]));
-        PT_HIP(hipStreamWaitEvent(st, set->events[k], 0));
+    for (size_t k = 0; k < ng; ++k) {
+        if (qs[k] == st) continue;
+        PT_HIP(hipEventRecord(set->events[k + 1], qs[k]));
+        PT_HIP(hipStreamWaitEvent(st, set->events[k + 1], 0));
     }
     // the host array must outlive the async copy: this call returns only after it has been consumed
     PT_HIP(hipStreamSynchronize(st));
+    set->timed = true;
+    return PT_OK;
+}
+
+// the class launches of the last fast-path train call: per launch its start and end (ms after the earliest start,
+// HIP events on the launch's stream) and its universe count; the launches overlap when they run concurrently
+extern "C" int pt_universe_set_launch_times(pt_universe_set *set, int64_t cap, float *out, int64_t *n_out) {
+    PT_CHECK(set && n_out, PT_EINVAL, "pt_universe_set_launch_times: null argument");
+    const int64_t ng = set->timed ? (int64_t)set->groups.size() : 0;
+    *n_out = ng;
+    if (!out || ng == 0) return PT_OK;
+    PT_CHECK(cap >= ng, PT_EINVAL, "pt_universe_set_launch_times: cap below the launch count");
+    for (int64_t k = 0; k < ng; ++k) {
+        float a = 0.f, b = 0.f;
+        PT_HIP(hipEventElapsedTime(&a, set->t_start[0], set->t_start[(size_t)k]));
+        PT_HIP(hipEventElapsedTime(&b, set->t_start[0], set->t_stop[(size_t)k]));
+        out[3 * k] = a;
+        out[3 * k + 1] = b;
+        out[3 * k + 2] = (float)set->groups[(size_t)k].n;
+    }
+    float lo = out[0];
+    for (int64_t k = 1; k < ng; ++k) lo = std::min(lo, out[3 * k]);
+    for (int64_t k = 0; k < ng; ++k) {
+        out[3 * k] -= lo;
+        out[3 * k + 1] -= lo;
+    }
     return PT_OK;
 }
 

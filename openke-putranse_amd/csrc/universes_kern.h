@@ -475,6 +475,32 @@ __device__ __forceinline__ float transh_step(const StepParams &P, int hp, int rp
     return lsum;
 }
 
+// Exact x mod d for 64-bit x and a divisor fixed for a universe (its trainTotal, entTotal - 1): one 64 x 64 -> high
+// 64 multiply by m = floor((2^64 - 1) / d) estimates the quotient q with floor(x / d) - 2 <= q <= floor(x / d), two
+// selects correct the remainder. Replaces the generic 64-bit urem (a long VALU sequence) of rand_max (Random.h:
+// 23-25: randd % x) in the presampler, whose draws are otherwise all 64-bit divisions.
+struct FastMod {
+    uint64_t m, d;
+};
+__device__ __forceinline__ FastMod fastmod_make(uint64_t d) { return FastMod{d ? ~0ull / d : 0ull, d}; }
+__device__ __forceinline__ uint64_t fastmod(uint64_t x, const FastMod &f) {
+    const uint64_t q = __umul64hi(x, f.m);
+    uint64_t r = x - q * f.d;
+    r = r >= f.d ? r - f.d : r;
+    r = r >= f.d ? r - f.d : r;
+    return r;
+}
+
+// The presampler's stream jumps from LDS tables (built once per universe): positive b of sampler call c starts at
+// position (c * len + j) * dpp of its thread slice's stream (Base.cpp:200-207: slice id = b / per, j = b - id * per,
+// len the slice's size), i.e. LCG^((c * len + j) * dpp) = TC[c][len == per ? 0 : 1] o TJ[j] applied to the slice's
+// chunk-start state - two affine maps instead of an O(log n) jump of 64-bit multiplies per draw.
+constexpr int kPreJ = 64, kPreC = 32;
+struct PreTables {
+    Affine j[kPreJ];        // LCG^(j * dpp)
+    Affine c[kPreC][2];     // LCG^(c * per * dpp), LCG^(c * rem * dpp) (rem: the last non-empty slice's size)
+};
+
 // Dynamic LDS layout (int32 units; the host sizes it for the largest universe of the launch):
 //   list[list_cap] | flags[E + 2R] or [2R] | head[E] + next[ccap] (contrib) |
 //   batch h, r, t [3][pchunk * bs * (1 + neg)] (pchunk > 0) | rel (+ norm) gradient rows [R][D] floats
@@ -484,6 +510,7 @@ struct UniShared {
     uint64_t *states;   // [64]
     int *count, *ccount;
     float *loss;
+    PreTables *pre;
 };
 
 // One universe's whole training run (all epochs x nbatches steps) by the calling workgroup.
@@ -540,6 +567,21 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     const int nrelg = (PLAN == 1 || (PLAN == 0 && cfg.lds_relgrad)) && !rel_list ? R * D * (MODEL == 1 ? 2 : 1) : 0;
 
     if (tid < threads) s_states[tid] = U.states[tid];
+    // presampler jump tables (PreTables): positives per thread slice `per`, the last non-empty slice's size `rem`
+    const int per = bs % threads == 0 ? bs / threads : bs / threads + 1;
+    const int rem = per > 0 ? bs - (bs / per) * per : 0;
+    const int dpp = 1 + 2 * neg;
+    const bool fastpre = presampled && per <= kPreJ && pchunk <= kPreC;
+    if (fastpre) {
+        PreTables &T = *S.pre;
+        if (tid < kPreJ) {
+            T.j[tid] = lcg_power((uint64_t)tid * (uint64_t)dpp);
+        } else if (tid < kPreJ + 2 * kPreC) {
+            const int c = (tid - kPreJ) >> 1, w = (tid - kPreJ) & 1;
+            T.c[c][w] = lcg_power((uint64_t)c * (uint64_t)(w ? rem : per) * (uint64_t)dpp);
+        }
+    }
+    const FastMod fm_n = fastmod_make((uint64_t)U.g.train_total), fm_e = fastmod_make((uint64_t)(E - 1));
     for (int i = tid; i < nflags; i += NT) s_flags[i] = 0;
     for (int i = tid; i < nheads; i += NT) s_head[i] = -1;
     for (int i = tid; i < nrelg; i += NT) s_grel[i] = 0.f;
@@ -568,9 +610,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
         sink.grel = s_grel;
         sink.gnorm = s_grel + R * D;
     }
-    const int dpp = 1 + 2 * neg;
     const DeviceGraph &g = U.g;
-    const int per = bs % threads == 0 ? bs / threads : bs / threads + 1;
     float epoch_loss = 0.f;
     uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0;
     const uint64_t w_start = U.prof ? wall_clock64() : 0;   // (100 MHz wall clock: the set's schedule)
@@ -587,6 +627,33 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                 const int nb = nbatches - step < pchunk ? nbatches - step : pchunk;
                 for (int q = tid; q < nb * bs; q += NT) {
                     const int s = q / bs, b = q - s * bs;
+                    if (fastpre && !filter) {
+                        // the same draws as draw_positive / draw_negative (bit-identical streams and values):
+                        // table jumps, 32-bit slice arithmetic, rand_max by fastmod
+                        const int id = b / per, j = b - id * per;
+                        const PreTables &T = *S.pre;
+                        const Affine m1 = T.j[j], m2 = T.c[s][bs - id * per >= per ? 0 : 1];
+                        uint64_t st = m1.a * s_states[id] + m1.c;
+                        st = m2.a * st + m2.c;
+                        const int i = (int)fastmod(lcg_next(st), fm_n);
+                        i32x4 ra, rc;
+                        graph_rec(g, i, ra, rc);
+                        int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
+                        bh[b] = ra.x; br[b] = ra.y; bt[b] = ra.z;
+                        const float prob = bern ? g.bern_prob[ra.y] : 500.f;
+                        for (int k = 0; k < neg; ++k) {
+                            // coin, then the corruption (Corrupt.h:18-25, 68-74: skips the passed entity)
+                            const bool tail = (float)(lcg_next(st) % 1000ULL) < prob;
+                            const int tmp = (int)fastmod(lcg_next(st), fm_e);
+                            const int skip = tail ? ra.x : ra.z;
+                            const int e = tmp < skip ? tmp : tmp + 1;
+                            const int o = (k + 1) * bs + b;
+                            bh[o] = tail ? ra.x : e;
+                            bt[o] = tail ? e : ra.z;
+                            br[o] = ra.y;
+                        }
+                        continue;
+                    }
                     const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp, s);
                     int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
                     bh[b] = (int32_t)pd.h; br[b] = (int32_t)pd.r; bt[b] = (int32_t)pd.t;
@@ -855,7 +922,8 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
     __shared__ uint64_t s_states[64];
     __shared__ int s_count, s_ccount, s_u;
     __shared__ float s_loss;
-    const UniShared S{s_dyn, s_states, &s_count, &s_ccount, &s_loss};
+    __shared__ PreTables s_pre;
+    const UniShared S{s_dyn, s_states, &s_count, &s_ccount, &s_loss, &s_pre};
     for (;;) {
         if (threadIdx.x == 0) s_u = atomicAdd(next_universe, 1);
         __syncthreads();

@@ -110,6 +110,7 @@ SIGNATURES = {
     "pt_universe_set_profiling": (ctypes.c_int, [c_vp, c_i32]),
     "pt_universe_set_states": (ctypes.c_int, [c_vp, c_i64, c_vp]),
     "pt_universe_set_reset": (ctypes.c_int, [c_vp]),
+    "pt_universe_set_launch_times": (ctypes.c_int, [c_vp, ctypes.c_int64, c_vp, c_vp]),
     "pt_universes_train": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
                                           c_i64, c_vp, c_vp]),
     "pt_universes_train_ex": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,

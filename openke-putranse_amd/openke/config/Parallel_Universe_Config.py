@@ -1343,11 +1343,19 @@ class Parallel_Universe_Config(Tester):
         if rank != 0:
             return None
         # a universe held by several ranks (the one-universe protocol, add_embedding_space, registers every
-        # universe on every rank): the owner's copy, else the lowest rank's
+        # universe on every rank): the owner's copy, else the lowest rank's - after checking that every copy is
+        # the same universe (sizes and tables equal), so a placement bug cannot pick one of two diverged copies
         chosen = {}
         for r, part in enumerate(got):
             for x in part:
                 uid = x[0]
+                if uid in chosen:
+                    y = chosen[uid][1]
+                    same = (x[1], x[2]) == (y[1], y[2]) and x[3].keys() == y[3].keys() and all(
+                        x[3][k].shape == y[3][k].shape and torch.equal(x[3][k], y[3][k]) for k in x[3])
+                    if not same:
+                        raise RuntimeError("universe %d is held by ranks %d and %d with different tables"
+                                           % (uid, chosen[uid][0], r))
                 if uid not in chosen or (chosen[uid][0] != self.owner(uid) and r == self.owner(uid)):
                     chosen[uid] = (r, x)
         spaces = defaultdict(Model)
@@ -1392,10 +1400,18 @@ class Parallel_Universe_Config(Tester):
             err = []
 
             def write():
+                # written next to the target and renamed onto it: a crash or kill while the writer runs leaves the
+                # previous checkpoint intact
+                tmp = "%s.tmp%d" % (path, os.getpid())
                 try:
-                    torch.save(state, path)
+                    torch.save(state, tmp)
+                    os.replace(tmp, path)
                 except BaseException as e:   # re-raised by flush_checkpoint on the caller's thread
                     err.append(e)
+                    try:
+                        os.remove(tmp)
+                    except OSError:
+                        pass
             th = threading.Thread(target=write, name="universe-checkpoint")
             th.start()
             self._ckpt_writer = (th, err)

@@ -305,3 +305,34 @@ def test_multi_rank_checkpoint_with_every_rank_holding_every_universe(tmp_path):
     _assert_same_spaces(_ck_summary(single),
                         {u: {n: t.numpy() for n, t in m.state_dict().items()}
                          for u, m in b["trained_embedding_spaces"].items()})
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_spawns_gpus_ranks(n):
+    """`bench.py --gpus N` started without a torch.distributed environment launches N ranks itself
+    (torch.distributed.run, 127.0.0.1) and their world size equals --gpus (gloo rehearsal, no GPU work)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env["PT_BENCH_BACKEND"] = "gloo"
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(n), "--launch-check"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == n and rec["world_size_env"] == n
+
+
+def test_bench_rejects_world_size_mismatch():
+    """A rank whose WORLD_SIZE differs from --gpus exits non-zero instead of printing a line."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--launch-check"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and not p.stdout.strip().startswith("{")
