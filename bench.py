@@ -203,6 +203,8 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
     shape, n_univ, model, dim_spec, p_norm, tc_range, margin_range, do_lp = PU_WORKLOADS[name]
     if getattr(args, "universes", 0):   # --universes: the reference experiment's own count (e.g. 6,000)
         n_univ = args.universes
+    if getattr(args, "dim", 0):         # --dim: one fixed dim (the reference experiment's 20)
+        dim_spec = args.dim
     if per_gpu:   # weak scaling: the workload's universe count on EVERY GPU (universes 4+k continue the seeds)
         n_univ *= ws
         do_lp = False
@@ -434,7 +436,8 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
         out["link_prediction"] = universe_link_prediction(L, path, unis, mid, p_norm, ws, dev)
     L.pt_graph_free(g)
     if cpu and ws == 1 and rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = universe_cpu_baseline(path, name, args.cpu_seconds)
+        out["cpu_baseline"] = universe_cpu_baseline(path, name, args.cpu_seconds, getattr(args, "dim", 0),
+                                                    getattr(args, "universes", 0))
     return out
 
 
@@ -456,6 +459,9 @@ def run_dropin(args, ws, rank, dev, name="c3"):
     shape, n_univ, model, dim_spec, p_norm, tc_range, margin_range, do_lp = PU_WORKLOADS[name]
     if getattr(args, "universes", 0):
         n_univ = args.universes
+    if getattr(args, "dim", 0):
+        dim_spec = args.dim
+    do_lp = do_lp or getattr(args, "link_prediction", False)
     valid_steps = args.valid_steps if getattr(args, "valid_steps", 0) else max(n_univ // 4, 1)
     path = synth_kg.ensure_dataset(os.path.join(args.data_dir, "rank%d" % rank), shape)
     t0 = time.perf_counter()
@@ -496,7 +502,7 @@ def run_dropin(args, ws, rank, dev, name="c3"):
     return out
 
 
-def universe_cpu_baseline(path, name, seconds):
+def universe_cpu_baseline(path, name, seconds, dim_override=0, n_override=0):
     """The CPU restatement training whole universes of the same workload on `cpu_workers()` threads (one
     universe per thread at a time, taken in id order; the reference trains them one after another on one
     process, Parallel_Universe_Config.py:316-327): construction + epochs x 20 Adagrad steps each, new
@@ -505,6 +511,10 @@ def universe_cpu_baseline(path, name, seconds):
     sys.path.insert(0, HERE)
     import oracle
     shape, n_univ, model, dim_spec, p_norm, tc_range, margin_range, _ = PU_WORKLOADS[name]
+    if dim_override:
+        dim_spec = dim_override
+    if n_override:
+        n_univ = n_override
     workers = cpu_workers()
     kg = oracle.KG.load(path)
     lock = threading.Lock()
@@ -672,6 +682,11 @@ def main():
     ap.add_argument("--universes", type=int, default=0,
                     help="universe workloads: this many universes instead of the config's (the reference experiment "
                          "trains 6,000: experiments/static_experiment_PuTransE_on_WN18.py:84-91)")
+    ap.add_argument("--dim", type=int, default=0,
+                    help="universe workloads: one fixed embedding dim instead of the config's (the reference experiment: 20)")
+    ap.add_argument("--link-prediction", action="store_true",
+                    help="universe workloads: the drop-in leg ends with run_link_prediction() (as the reference "
+                         "experiment does; C4 always does)")
     ap.add_argument("--valid-steps", type=int, default=0,
                     help="drop-in leg: validate every this many universes (default: a quarter of the universes; the "
                          "reference experiment uses 100)")

@@ -1051,10 +1051,18 @@ namespace {
 struct ClassStreamPool {
     std::mutex mu;
     std::map<std::pair<int, int>, std::vector<hipStream_t>> by_dev;   // (device, mode) -> streams
+    // destroyed when the library is unloaded (process exit): the HIP runtime, loaded before this library, is
+    // finalized after it, so the queues are released while it still runs
+    ~ClassStreamPool() {
+        for (auto &kv : by_dev) {
+            if (hipSetDevice(kv.first.first) != hipSuccess) continue;
+            for (hipStream_t q : kv.second) (void)hipStreamDestroy(q);
+        }
+    }
 };
 ClassStreamPool &class_stream_pool() {
-    static ClassStreamPool *p = new ClassStreamPool();   // never destroyed: streams outlive every set
-    return *p;
+    static ClassStreamPool p;
+    return p;
 }
 // mode 1: full-CU-mask streams (dedicated hardware queues; the product's choice); tuning builds also take
 // PT_UNI_STREAMS = 0 (round 4: per-set plain side streams, class 0 on the caller's stream), 2 (highest-priority
