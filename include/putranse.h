@@ -246,6 +246,24 @@ enum { PT_DETERMINISTIC = 1 };
 int pt_universes_train_ex(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm, int32_t norm_flag,
                           int32_t opt, int64_t bern, int64_t filter, int32_t flags, float *d_losses, void *stream);
 
+/* Initial tables of universe models drawn on the GPU, bit-identical to the torch CPU generator after
+ * torch.manual_seed(seed): the reference builds each universe's TransE / TransH on the CPU after
+ * set_random_seed(seed0 + k) (Parallel_Universe_Config.py:157-161, 169-177; nn.Embedding's normal_ draws, then
+ * xavier_uniform_, TransE.py:17-36, TransH.py:17-42). A job skips `skip` 32-bit outputs of MT19937(seed mod 2^32) -
+ * the draws the constructor's normal_ calls consume (the caller counts them) - then fills its `ntab` tables in
+ * order, one output per element: out = (float)((x & 0xffffff) * 2^-24 * ((float)hi - (float)lo) + (float)lo) in
+ * double (torch's float uniform_). Tables are device buffers of numel floats; the call synchronizes `stream`. */
+typedef struct {
+    uint64_t seed;
+    int64_t skip;
+    int32_t ntab;
+    int32_t pad_;
+    int64_t numel[4];
+    double lo[4], hi[4];
+    float *out[4];
+} pt_torch_init_job;
+int pt_torch_init_tables(const pt_torch_init_job *jobs, int64_t n, void *stream);
+
 /* ------------------------------------------------------------------ link prediction --------- */
 /* Per-universe all-entity scoring with a float MIN reduction into per-key rows
  * (obtain_embedding_space_score + transmit_max_scores, Parallel_Universe_Config.py:446-465, :516-543).

@@ -1629,6 +1629,28 @@ extern "C" int pt_universes_train_ex(const pt_universe_job *jobs, int64_t n, int
     return rc;
 }
 
+// initial universe tables, torch-CPU-generator-identical (torch_init.hip)
+extern "C" int pt_torch_init_tables(const pt_torch_init_job *jobs, int64_t n, void *stream) {
+    PT_CHECK(n >= 0 && (jobs || n == 0), PT_EINVAL, "pt_torch_init_tables: null jobs");
+    if (n == 0) return PT_OK;
+    for (int64_t i = 0; i < n; ++i) {
+        const pt_torch_init_job &J = jobs[i];
+        PT_CHECK(J.ntab >= 0 && J.ntab <= 4 && J.skip >= 0, PT_EINVAL, "pt_torch_init_tables: bad job");
+        for (int k = 0; k < J.ntab; ++k)
+            PT_CHECK(J.numel[k] >= 0 && (J.out[k] || J.numel[k] == 0), PT_EINVAL, "pt_torch_init_tables: null table");
+    }
+    hipStream_t st = (hipStream_t)stream;
+    pt_torch_init_job *d = nullptr;
+    PT_HIP(hipMallocAsync((void **)&d, sizeof(pt_torch_init_job) * (size_t)n, st));
+    hipError_t e = hipMemcpyAsync(d, jobs, sizeof(pt_torch_init_job) * (size_t)n, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = pt::launch_torch_init(d, n, st);
+    const hipError_t f = hipFreeAsync(d, st);
+    const hipError_t w = hipStreamSynchronize(st);   // the caller's job array may go away on return
+    if (e == hipSuccess) e = f != hipSuccess ? f : w;
+    if (e != hipSuccess) return pt::fail(PT_EHIP, std::string("pt_torch_init_tables: ") + hipGetErrorString(e));
+    return PT_OK;
+}
+
 extern "C" int pt_universes_train(const pt_universe_job *jobs, int64_t n, int32_t model, int32_t p_norm,
                                   int32_t norm_flag, int32_t opt, int64_t bern, int64_t filter, float *d_losses,
                                   void *stream) {

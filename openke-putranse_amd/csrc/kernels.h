@@ -148,6 +148,7 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
                          int norm_flag, int64_t global_E, int64_t ds, float *base, float *normal, float *rows,
                          float *tuple_min, hipStream_t st);
 
+hipError_t launch_torch_init(const pt_torch_init_job *d_jobs, int64_t n, hipStream_t st);
 hipError_t launch_rank_rows(const float *rows, int64_t E, const int64_t *row_of, const int64_t *truth,
                             const float *repl, const int64_t *part_off, const int64_t *part, int64_t nq, int64_t *raw,
                             int64_t *filt, hipStream_t st);

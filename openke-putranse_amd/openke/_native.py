@@ -45,6 +45,12 @@ class UniverseJob(ctypes.Structure):
                 ("normv", c_vp), ("ent_acc", c_vp), ("rel_acc", c_vp), ("norm_acc", c_vp), ("dim", c_i64)]
 
 
+class TorchInitJob(ctypes.Structure):
+    """pt_torch_init_job: initial tables of one model drawn on the GPU as torch's CPU generator draws them."""
+    _fields_ = [("seed", ctypes.c_uint64), ("skip", c_i64), ("ntab", c_i32), ("pad_", c_i32),
+                ("numel", c_i64 * 4), ("lo", ctypes.c_double * 4), ("hi", ctypes.c_double * 4), ("out", c_vp * 4)]
+
+
 class LpUniverse(ctypes.Structure):
     _fields_ = [("ent", c_vp), ("rel", c_vp), ("normv", c_vp), ("ent_total", c_i64), ("rel_total", c_i64),
                 ("dim", c_i64), ("d_ent_remap", c_vp)]
@@ -113,6 +119,7 @@ SIGNATURES = {
     "pt_universe_set_launch_times": (ctypes.c_int, [c_vp, ctypes.c_int64, c_vp, c_vp]),
     "pt_universes_train": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
                                           c_i64, c_vp, c_vp]),
+    "pt_torch_init_tables": (ctypes.c_int, [ctypes.POINTER(TorchInitJob), c_i64, c_vp]),
     "pt_universes_train_ex": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
                                              c_i64, c_i32, c_vp, c_vp]),
     "pt_lp_min_scores": (ctypes.c_int, [ctypes.POINTER(LpUniverse), c_i64, c_i32, c_i32, c_i32,

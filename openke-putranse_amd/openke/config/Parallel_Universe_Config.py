@@ -517,28 +517,50 @@ class Parallel_Universe_Config(Tester):
             # a private generator, so the wave's modules are built on a thread pool
             mine = [i for i, uid in enumerate(ids) if self.owner(uid) == rank]
             ta = time.perf_counter()
-
-            def build(i):
-                return self.embedding_model.seeded(self.initial_random_seed + ids[i], sizes[i][0], sizes[i][1],
-                                                   **self._model_param(ids[i]))
-            if len(mine) > 1:
-                from concurrent.futures import ThreadPoolExecutor
-                with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1, len(mine))) as ex:
-                    built = list(ex.map(build, mine))
+            if mine and self.embedding_model.device_init_ok(dev):
+                # the same tables drawn on the GPU straight into device tensors (Model.device_seeded: torch's CPU
+                # generator restated, one launch for the wave; checked bit-identical to seeded() once per process)
+                built = self.embedding_model.device_seeded(
+                    [(self.initial_random_seed + ids[i], sizes[i][0], sizes[i][1], self._model_param(ids[i]))
+                     for i in mine], dev)
+                tm["modules_s"] = time.perf_counter() - ta
+                for i, kge in zip(mine, built):
+                    recs[i]["kge"] = kge
+                tm["h2d_s"] = 0.0
             else:
-                built = [build(i) for i in mine]
-            tb = time.perf_counter()
-            tm["modules_s"] = tb - ta
-            for i, kge in zip(mine, built):
-                recs[i]["kge"] = kge.to(dev)
-            tm["h2d_s"] = time.perf_counter() - tb
+                def build(i):
+                    return self.embedding_model.seeded(self.initial_random_seed + ids[i], sizes[i][0], sizes[i][1],
+                                                       **self._model_param(ids[i]))
+                if len(mine) > 1:
+                    from concurrent.futures import ThreadPoolExecutor
+                    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1, len(mine))) as ex:
+                        built = list(ex.map(build, mine))
+                else:
+                    built = [build(i) for i in mine]
+                tb = time.perf_counter()
+                tm["modules_s"] = tb - ta
+                for i, kge in zip(mine, built):
+                    recs[i]["kge"] = kge.to(dev)
+                tm["h2d_s"] = time.perf_counter() - tb
+            # every owned universe's Adagrad state (zero-init, the tables' shapes) carved from one zeroed buffer:
+            # one allocation and one fill for the wave instead of one per table
+            acc_elems = sum(sum(x.numel() for x in recs[i]["kge"].tables() if x is not None) for i in mine)
+            acc_buf = torch.zeros(max(acc_elems, 1), dtype=torch.float32, device=dev)
+            acc_off = 0
             for i in mine:
                 uid, rec, h = ids[i], recs[i], handles[i]
                 tc, balance, margin, epochs, lr = draws[i]
                 bs = rec["batch_size"]
                 kge = rec["kge"]
                 ent, rel, nv = kge.tables()
-                accs = tuple(torch.zeros_like(x) if x is not None else None for x in (ent, rel, nv))
+                accs = []
+                for x in (ent, rel, nv):
+                    if x is None:
+                        accs.append(None)
+                        continue
+                    accs.append(acc_buf[acc_off:acc_off + x.numel()].view(x.shape))
+                    acc_off += x.numel()
+                accs = tuple(accs)
                 st = np.zeros(dl.work_threads, dtype=np.uint64)
                 _native.check(L.pt_universe_seeds(h, st.ctypes.data))
                 j = _native.UniverseJob()

@@ -1,4 +1,5 @@
 import ctypes
+import math
 import threading
 
 import numpy as np
@@ -9,8 +10,30 @@ from ... import _native
 from ..BaseModule import BaseModule
 
 _MODES = {"normal": 0, "head_batch": 1, "tail_batch": 2}
-# per-thread torch.Generator of Model.seeded (None: the default generator, as the reference's constructors use)
+# per-thread torch.Generator of Model.seeded (None: the default generator, as the reference's constructors use);
+# per-thread recording state of Model.device_seeded (plan / dev)
 _INIT = threading.local()
+_DEVICE_INIT_OK = {}
+
+
+def _normal_draws(numels):
+    """32-bit MT19937 outputs torch's CPU normal_ consumes for float tensors of these sizes, in order, from a freshly
+    seeded generator (aten/src/ATen/native/cpu/DistributionTemplates.h, normal_kernel): a contiguous tensor of at
+    least 16 elements draws one uniform float per element plus 16 more when the size is not a multiple of 16
+    (normal_fill recomputes the last 16); a smaller one takes Box-Muller normal_distribution<double> samples, two
+    random64 (4 outputs) per generated pair, the second sample cached in the generator for the next element."""
+    draws, cached = 0, False
+    for n in numels:
+        if n >= 16:
+            draws += n + (16 if n % 16 else 0)
+            continue
+        for _ in range(n):
+            if cached:
+                cached = False
+            else:
+                draws += 4
+                cached = True
+    return draws
 
 
 class Model(BaseModule):
@@ -38,19 +61,101 @@ class Model(BaseModule):
         finally:
             _INIT.gen = None
 
+    @classmethod
+    def device_seeded(cls, specs, device):
+        """[cls.seeded(seed, ent_tot, rel_tot, **param) for (seed, ent_tot, rel_tot, param) in specs] with the same
+        tables bit for bit, drawn on the GPU (pt_torch_init_tables: the torch CPU generator's MT19937 and its float
+        uniform_, one workgroup per model) straight into device tensors: no CPU draws, no host-to-device copy.
+        Each constructor runs in a recording mode - its nn.Embedding tables allocated on `device` uninitialised,
+        its normal_ draws counted (_normal_draws) and its xavier / uniform inits recorded - and one launch fills
+        every model. Verified against seeded() once per process and class (device_init_ok); raises if the
+        constructor's draw order is one the kernel does not express (a uniform init before a normal_)."""
+        models, jobs = [], []
+        for seed, ent_tot, rel_tot, param in specs:
+            _INIT.plan = []
+            _INIT.dev = device
+            try:
+                m = cls(ent_tot, rel_tot, **param)
+                plan = _INIT.plan
+            finally:
+                _INIT.plan = None
+                _INIT.dev = None
+            normals = [x[1] for x in plan if x[0] == "normal"]
+            unis = [x for x in plan if x[0] == "uniform"]
+            first_u = next((i for i, x in enumerate(plan) if x[0] == "uniform"), len(plan))
+            if any(x[0] == "normal" for x in plan[first_u:]) or len(unis) > 4:
+                raise NotImplementedError("device_seeded: %s's init order is not normal_* then uniform_*" % cls.__name__)
+            j = _native.TorchInitJob()
+            j.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+            j.skip = _normal_draws(normals)
+            j.ntab = len(unis)
+            for k, (_, w, lo, hi) in enumerate(unis):
+                j.numel[k] = w.numel()
+                j.lo[k], j.hi[k] = float(lo), float(hi)
+                j.out[k] = w.data_ptr()
+            jobs.append(j)
+            models.append(m.to(device))   # (the small non-table parameters, e.g. a margin; tables are there already)
+        if jobs:
+            arr = (_native.TorchInitJob * len(jobs))(*jobs)
+            with torch.cuda.device(device):
+                _native.check(_native.lib().pt_torch_init_tables(arr, len(jobs), _native.stream()))
+        return models
+
+    @classmethod
+    def device_init_ok(cls, device):
+        """Whether device_seeded reproduces seeded() bit for bit under this torch build: checked once per process
+        and class on two small models (tables of at least and of fewer than 16 elements: torch's two normal_
+        paths), so a torch whose CPU generator differs makes callers keep the CPU construction."""
+        key = (cls, str(device))
+        if key not in _DEVICE_INIT_OK:
+            specs = [(12345, 37, 3, {"dim": 20}), (77, 5, 1, {"dim": 3})]
+            got = cls.device_seeded(specs, device)
+            ok = True
+            for (seed, e, r, param), m in zip(specs, got):
+                ref = cls.seeded(seed, e, r, **param)
+                for a, b in zip(ref.tables(), m.tables()):
+                    if a is not None and not torch.equal(a.detach(), b.detach().cpu()):
+                        ok = False
+            _DEVICE_INIT_OK[key] = ok
+        return _DEVICE_INIT_OK[key]
+
     @staticmethod
     def _generator():
         return getattr(_INIT, "gen", None)
 
     @staticmethod
     def _embedding(rows, dim):
-        """nn.Embedding(rows, dim) with its default N(0, 1) init drawn from the active generator."""
+        """nn.Embedding(rows, dim) with its default N(0, 1) init drawn from the active generator (device_seeded:
+        allocated uninitialised on the device, its draws recorded)."""
+        plan = getattr(_INIT, "plan", None)
+        if plan is not None:
+            w = torch.empty(rows, dim, device=_INIT.dev)
+            plan.append(("normal", rows * dim))
+            return nn.Embedding(rows, dim, _weight=w)
         gen = getattr(_INIT, "gen", None)
         if gen is None:
             return nn.Embedding(rows, dim)
         w = torch.empty(rows, dim)
         w.normal_(generator=gen)
         return nn.Embedding(rows, dim, _weight=w)
+
+    def _xavier_uniform_(self, w):
+        """nn.init.xavier_uniform_(w) from the active generator (device_seeded: recorded with torch's bound)."""
+        plan = getattr(_INIT, "plan", None)
+        if plan is not None:
+            fan_in, fan_out = nn.init._calculate_fan_in_and_fan_out(w)
+            a = math.sqrt(3.0) * (1.0 * math.sqrt(2.0 / float(fan_in + fan_out)))
+            plan.append(("uniform", w, -a, a))
+            return
+        nn.init.xavier_uniform_(w, generator=self._generator())
+
+    def _uniform_(self, w, a, b):
+        """nn.init.uniform_(w, a, b) from the active generator (device_seeded: recorded)."""
+        plan = getattr(_INIT, "plan", None)
+        if plan is not None:
+            plan.append(("uniform", w, a, b))
+            return
+        nn.init.uniform_(tensor=w, a=a, b=b, generator=self._generator())
 
     # -- native plumbing --------------------------------------------------------------------------
     def tables(self):

@@ -23,15 +23,13 @@ class TransE(Model):
         self.ent_embeddings = self._embedding(self.ent_tot, self.dim)
         self.rel_embeddings = self._embedding(self.rel_tot, self.dim)
         if margin is None or epsilon is None:
-            nn.init.xavier_uniform_(self.ent_embeddings.weight.data, generator=self._generator())
-            nn.init.xavier_uniform_(self.rel_embeddings.weight.data, generator=self._generator())
+            self._xavier_uniform_(self.ent_embeddings.weight.data)
+            self._xavier_uniform_(self.rel_embeddings.weight.data)
         else:
             self.embedding_range = nn.Parameter(torch.Tensor([(self.margin + self.epsilon) / self.dim]),
                                                 requires_grad=False)
-            nn.init.uniform_(tensor=self.ent_embeddings.weight.data, a=-self.embedding_range.item(),
-                             b=self.embedding_range.item(), generator=self._generator())
-            nn.init.uniform_(tensor=self.rel_embeddings.weight.data, a=-self.embedding_range.item(),
-                             b=self.embedding_range.item(), generator=self._generator())
+            self._uniform_(self.ent_embeddings.weight.data, -self.embedding_range.item(), self.embedding_range.item())
+            self._uniform_(self.rel_embeddings.weight.data, -self.embedding_range.item(), self.embedding_range.item())
         if margin is not None:
             self.margin = nn.Parameter(torch.Tensor([margin]))
             self.margin.requires_grad = False

@@ -24,15 +24,14 @@ class TransH(Model):
         self.rel_embeddings = self._embedding(self.rel_tot, self.dim)
         self.norm_vector = self._embedding(self.rel_tot, self.dim)
         if margin is None or epsilon is None:
-            nn.init.xavier_uniform_(self.ent_embeddings.weight.data, generator=self._generator())
-            nn.init.xavier_uniform_(self.rel_embeddings.weight.data, generator=self._generator())
-            nn.init.xavier_uniform_(self.norm_vector.weight.data, generator=self._generator())
+            self._xavier_uniform_(self.ent_embeddings.weight.data)
+            self._xavier_uniform_(self.rel_embeddings.weight.data)
+            self._xavier_uniform_(self.norm_vector.weight.data)
         else:
             self.embedding_range = nn.Parameter(torch.Tensor([(self.margin + self.epsilon) / self.dim]),
                                                 requires_grad=False)
             for emb in (self.ent_embeddings, self.rel_embeddings, self.norm_vector):
-                nn.init.uniform_(tensor=emb.weight.data, a=-self.embedding_range.item(),
-                                 b=self.embedding_range.item(), generator=self._generator())
+                self._uniform_(emb.weight.data, -self.embedding_range.item(), self.embedding_range.item())
         if margin is not None:
             self.margin = nn.Parameter(torch.Tensor([margin]))
             self.margin.requires_grad = False
