@@ -27,6 +27,7 @@ import ctypes
 import os
 import pickle
 import random
+import sys
 import threading
 import time
 from collections import defaultdict
@@ -865,14 +866,22 @@ class Parallel_Universe_Config(Tester):
         local = [u for u in universes if u in self.trained_embedding_spaces]
         lp_us, pairs = [], []
         model_id = p_norm = norm_flag = None
+        # the device local -> global entity maps of universes folded for the first time: one host-to-device copy
+        # for all of them (views of one device array) instead of one per universe
+        new = [u for u in local if u not in self._dev_remaps]
+        if new:
+            ems = [self._remap_arrays(u)[0] for u in new]
+            flat = torch.from_numpy(np.concatenate(ems) if ems else np.zeros(0, np.int64)).cuda()
+            off = 0
+            for u, em in zip(new, ems):
+                self._dev_remaps[u] = flat[off:off + len(em)]
+                off += len(em)
         for slot, u in enumerate(local):
             kge = self.trained_embedding_spaces[u]
             if not next(kge.parameters()).is_cuda:
                 kge.cuda()
             em, rm = self._remap_arrays(u)
-            dr = self._dev_remaps.get(u)
-            if dr is None:
-                dr = self._dev_remaps[u] = torch.from_numpy(em).cuda()
+            dr = self._dev_remaps[u]
             ent, rel, nv = kge.tables()
             U = _native.LpUniverse()
             U.ent, U.rel = ent.data_ptr(), rel.data_ptr()
@@ -1412,16 +1421,30 @@ class Parallel_Universe_Config(Tester):
         background=True (the training loop's best-model saves, one rank, static setting): the state is
         snapshotted here and the file written by a writer thread while training continues; the next save,
         load_parameters and the end of train_parallel_universes wait for it (flush_checkpoint)."""
-        self.flush_checkpoint()
         world, rank = _dist()
+        if not (world == 1 and background and self.training_setting == "static"):
+            self.flush_checkpoint()
         if world == 1:
             state = self._checkpoint_state()
             if not (background and self.training_setting == "static"):
                 torch.save(state, path)
                 return
-            err = []
+            prev = getattr(self, "_ckpt_writer", None)
+            err = prev[1] if prev is not None else []
+            seq = self._ckpt_seq = getattr(self, "_ckpt_seq", 0) + 1
+            latest = self.__dict__.setdefault("_ckpt_latest", {})
+            latest[path] = seq
 
             def write():
+                # writes land in save order: a writer first waits for the one before it (off the training thread)
+                if prev is not None:
+                    prev[0].join()
+                if err:
+                    return
+                # a newer save of the same file was requested meanwhile: it writes the newer snapshot (the file only
+                # skips an intermediate state it would have held until then)
+                if latest.get(path) != seq:
+                    return
                 # written next to the target and renamed onto it: a crash or kill while the writer runs leaves the
                 # previous checkpoint intact
                 tmp = "%s.tmp%d" % (path, os.getpid())
@@ -1434,6 +1457,12 @@ class Parallel_Universe_Config(Tester):
                         os.remove(tmp)
                     except OSError:
                         pass
+            # while a writer pickles (holding the GIL), the training thread's every return from a GIL-releasing
+            # call (a ctypes launch, a torch op, a print) would wait up to the 5 ms switch interval for it: a short
+            # interval until the writes are flushed
+            if prev is None:
+                self._switch_interval = sys.getswitchinterval()
+                sys.setswitchinterval(min(self._switch_interval, 2e-4))
             th = threading.Thread(target=write, name="universe-checkpoint")
             th.start()
             self._ckpt_writer = (th, err)
@@ -1452,7 +1481,8 @@ class Parallel_Universe_Config(Tester):
         if w is None:
             return
         self._ckpt_writer = None
-        w[0].join()
+        w[0].join()   # (the last writer joined its predecessors)
+        sys.setswitchinterval(getattr(self, "_switch_interval", 0.005))
         if w[1]:
             raise w[1][0]
 

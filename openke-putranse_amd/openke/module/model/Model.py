@@ -1,3 +1,4 @@
+import copy
 import ctypes
 import math
 import threading
@@ -14,6 +15,71 @@ _MODES = {"normal": 0, "head_batch": 1, "tail_batch": 2}
 # per-thread recording state of Model.device_seeded (plan / dev)
 _INIT = threading.local()
 _DEVICE_INIT_OK = {}
+
+
+_MODULE_CONTAINERS = (dict, set, list)
+
+
+def _clone_module(src):
+    """A new module object with src's attributes: every container (parameter / buffer / submodule / hook dicts)
+    copied, so nothing registered on one is shared with the other. Tensors are replaced by the caller."""
+    m = object.__new__(type(src))
+    m.__dict__.update({k: (type(v)(v) if isinstance(v, _MODULE_CONTAINERS) else v) for k, v in src.__dict__.items()})
+    return m
+
+
+def _named_plan(model, plan):
+    """A recorded init plan with each table named by its submodule (("normal" | "xavier", name) or
+    ("uniform", name, lo, hi)), so it can be replayed on a model of other sizes."""
+    names = {sub.weight.data_ptr(): n for n, sub in model._modules.items() if isinstance(sub, nn.Embedding)}
+    out = []
+    for x in plan:
+        if x[0] == "normal":
+            out.append(("normal", names[x[2].data_ptr()]))
+        else:
+            out.append((x[0], names[x[1].data_ptr()]) + tuple(x[2:4] if x[0] == "uniform" else ()))
+    return out
+
+
+def _clone_model(template, ent_tot, rel_tot, device):
+    """What the constructor builds for (ent_tot, rel_tot) with the template's parameters, assembled from the
+    template (Model.device_seeded: the constructor's Python work per universe was most of a wave's host time):
+    the same attributes and submodules, each nn.Embedding table allocated on `device` (uninitialised: the init
+    kernel fills it) with the rows the constructor gives it (ent_tot for the entity table, rel_tot for the relation
+    tables), every other parameter a copy of the template's (a constant such as the margin). Returns
+    (model, its init plan in device_seeded's recorded form)."""
+    tm, named, t_ent, t_rel = template
+    m = _clone_module(tm)
+    m.ent_tot, m.rel_tot = ent_tot, rel_tot
+    for name, sub in tm._modules.items():
+        if isinstance(sub, nn.Embedding):
+            n_rows = ent_tot if name == "ent_embeddings" else rel_tot
+            e = _clone_module(sub)
+            e.num_embeddings = n_rows
+            e._parameters["weight"] = nn.Parameter(torch.empty(n_rows, sub.embedding_dim, device=device),
+                                                   requires_grad=sub.weight.requires_grad)
+            m._modules[name] = e
+        else:
+            m._modules[name] = copy.deepcopy(sub)
+    for name, p in tm._parameters.items():
+        m._parameters[name] = None if p is None else nn.Parameter(p.detach().clone(), requires_grad=p.requires_grad)
+    plan = []
+    for x in named:
+        w = m._modules[x[1]].weight.data
+        if x[0] == "normal":
+            plan.append(("normal", w.numel(), x[1]))
+        elif x[0] == "xavier":
+            plan.append(("uniform", w) + _xavier_bounds(w))
+        else:
+            plan.append(("uniform", w, x[2], x[3]))
+    return m, plan
+
+
+def _xavier_bounds(w):
+    """nn.init.xavier_uniform_'s (-a, a) for a 2-D tensor (gain 1): a = sqrt(3) * sqrt(2 / (fan_in + fan_out))."""
+    fan_in, fan_out = nn.init._calculate_fan_in_and_fan_out(w)
+    a = math.sqrt(3.0) * (1.0 * math.sqrt(2.0 / float(fan_in + fan_out)))
+    return (-a, a)
 
 
 def _normal_draws(numels):
@@ -71,15 +137,27 @@ class Model(BaseModule):
         every model. Verified against seeded() once per process and class (device_init_ok); raises if the
         constructor's draw order is one the kernel does not express (a uniform init before a normal_)."""
         models, jobs = [], []
+        templates = {}   # constructor parameters -> (a model built by the constructor, its recorded plan)
         for seed, ent_tot, rel_tot, param in specs:
-            _INIT.plan = []
-            _INIT.dev = device
-            try:
-                m = cls(ent_tot, rel_tot, **param)
-                plan = _INIT.plan
-            finally:
-                _INIT.plan = None
-                _INIT.dev = None
+            key = tuple(sorted(param.items()))
+            t = templates.get(key)
+            cloned = False
+            if t is None or ent_tot == rel_tot:
+                _INIT.plan = []
+                _INIT.dev = device
+                try:
+                    m = cls(ent_tot, rel_tot, **param)
+                    plan = [("uniform",) + x[1:] if x[0] == "xavier" else x for x in _INIT.plan]
+                    named = _named_plan(m, _INIT.plan)
+                finally:
+                    _INIT.plan = None
+                    _INIT.dev = None
+                if t is None and ent_tot != rel_tot and {x[1] for x in named} <= {"ent_embeddings", "rel_embeddings",
+                                                                               "norm_vector"}:
+                    templates[key] = (m, named, ent_tot, rel_tot)
+            else:
+                m, plan = _clone_model(t, ent_tot, rel_tot, device)
+                cloned = True
             normals = [x[1] for x in plan if x[0] == "normal"]
             unis = [x for x in plan if x[0] == "uniform"]
             first_u = next((i for i, x in enumerate(plan) if x[0] == "uniform"), len(plan))
@@ -94,7 +172,9 @@ class Model(BaseModule):
                 j.lo[k], j.hi[k] = float(lo), float(hi)
                 j.out[k] = w.data_ptr()
             jobs.append(j)
-            models.append(m.to(device))   # (the small non-table parameters, e.g. a margin; tables are there already)
+            # (a constructed model's small non-table parameters - the constants, a margin - to the device; a clone
+            # copied them from the template, which is there already)
+            models.append(m if cloned else m.to(device))
         if jobs:
             arr = (_native.TorchInitJob * len(jobs))(*jobs)
             with torch.cuda.device(device):
@@ -130,7 +210,7 @@ class Model(BaseModule):
         plan = getattr(_INIT, "plan", None)
         if plan is not None:
             w = torch.empty(rows, dim, device=_INIT.dev)
-            plan.append(("normal", rows * dim))
+            plan.append(("normal", rows * dim, w))
             return nn.Embedding(rows, dim, _weight=w)
         gen = getattr(_INIT, "gen", None)
         if gen is None:
@@ -143,9 +223,7 @@ class Model(BaseModule):
         """nn.init.xavier_uniform_(w) from the active generator (device_seeded: recorded with torch's bound)."""
         plan = getattr(_INIT, "plan", None)
         if plan is not None:
-            fan_in, fan_out = nn.init._calculate_fan_in_and_fan_out(w)
-            a = math.sqrt(3.0) * (1.0 * math.sqrt(2.0 / float(fan_in + fan_out)))
-            plan.append(("uniform", w, -a, a))
+            plan.append(("xavier", w) + _xavier_bounds(w))
             return
         nn.init.xavier_uniform_(w, generator=self._generator())
 

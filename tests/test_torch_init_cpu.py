@@ -90,3 +90,50 @@ def test_normal_draw_rule():
         for _ in range(_normal_draws(sizes)):
             mt.next()
         assert mt.next() & 0xFFFFFF == nxt, sizes
+
+
+@pytest.mark.parametrize("cls,param", [(TransE, {"dim": 20}), (TransH, {"dim": 7, "p_norm": 2}),
+                                       (TransE, {"dim": 10, "margin": 6.0, "epsilon": 2.0})])
+def test_clone_model_matches_constructor(cls, param):
+    """Model.device_seeded builds all but the first model of a parameter set by cloning it (_clone_model): the
+    clone has the constructed model's attributes, submodules, parameter names / shapes / flags, and the init plan
+    the constructor records for those sizes."""
+    from openke.module.model import Model as M
+    mod = __import__("openke.module.model.Model", fromlist=["_INIT"])
+    cpu = torch.device("cpu")
+
+    def record(e, r):
+        mod._INIT.plan, mod._INIT.dev = [], cpu
+        try:
+            m = cls(e, r, **param)
+            return m, list(mod._INIT.plan)
+        finally:
+            mod._INIT.plan, mod._INIT.dev = None, None
+    t, tplan = record(300, 7)
+    tmpl = (t, mod._named_plan(t, tplan), 300, 7)
+    c, cplan = mod._clone_model(tmpl, 41, 3, cpu)
+    ref, rplan = record(41, 3)
+    assert type(c) is type(ref) and c.ent_tot == 41 and c.rel_tot == 3
+    sd_c, sd_r = c.state_dict(), ref.state_dict()
+    assert list(sd_c) == list(sd_r)
+    for k in sd_r:
+        assert sd_c[k].shape == sd_r[k].shape
+        if "embeddings" not in k and "norm_vector" not in k:
+            assert torch.equal(sd_c[k], sd_r[k])
+    for (n1, p1), (n2, p2) in zip(c.named_parameters(), ref.named_parameters()):
+        assert n1 == n2 and p1.requires_grad == p2.requires_grad and p1 is not dict(t.named_parameters()).get(n1)
+    for name, sub in ref._modules.items():
+        assert type(c._modules[name]) is type(sub)
+        if isinstance(sub, torch.nn.Embedding):
+            assert (c._modules[name].num_embeddings, c._modules[name].embedding_dim) == (sub.num_embeddings,
+                                                                                         sub.embedding_dim)
+    for k in ("dim", "p_norm", "norm_flag", "margin_flag", "epsilon"):
+        assert getattr(c, k, None) == getattr(ref, k, None) or k == "margin"
+    # the replayed plan: the same draws and bounds as the constructor records for these sizes
+    norm = lambda p: [(x[0], x[1] if x[0] == "normal" else x[1].shape) + tuple(x[2:4] if x[0] != "normal" else ())
+                      for x in p]
+    rplan = [("uniform",) + x[1:] if x[0] == "xavier" else x for x in rplan]
+    assert norm(cplan) == norm(rplan)
+    # nothing shared with the template
+    assert c._modules is not t._modules and c._parameters is not t._parameters
+    assert c._modules["ent_embeddings"] is not t._modules["ent_embeddings"]
