@@ -690,6 +690,8 @@ def main():
     ap.add_argument("--valid-steps", type=int, default=0,
                     help="drop-in leg: validate every this many universes (default: a quarter of the universes; the "
                          "reference experiment uses 100)")
+    ap.add_argument("--no-ref-scale", action="store_true",
+                    help="default line: skip the pu_c3_ref6000 field (6,000 universes, dim 20, strong scaling)")
     ap.add_argument("--no-dropin", action="store_true",
                     help="universe workloads: skip the drop-in Parallel_Universe_Config timing")
     ap.add_argument("--launch-check", action="store_true",
@@ -857,6 +859,15 @@ def main():
         c3["dropin"]["over_kernel_only"] = c3["dropin"]["train_parallel_universes_s"] / c3["s_per_step"]
     # universe weak scaling (512 universes per GPU, no collective): at N = 1 it is the strong line
     c3w = None if args.no_c3 or ws == 1 else run_universes(args, ws, rank, dev, "c3", cpu=False, per_gpu=True)
+    # the reference experiment's own scale (experiments/static_experiment_PuTransE_on_WN18.py:43-91: 6,000
+    # universes, dim 20), kernel-only, strong scaling over the ranks: enough universes per GPU at N = 8 (750) that
+    # the set is throughput-bound, not bound by its longest universe as the 512-universe C3 set is
+    c3r = None
+    if not args.no_c3 and not args.no_ref_scale:
+        import copy as _copy
+        a2 = _copy.copy(args)
+        a2.universes, a2.dim, a2.place_world, a2.deterministic_timing = 6000, 20, 0, 0
+        c3r = run_universes(a2, ws, rank, dev, "c3", cpu=False)
     if rank != 0:
         if ws > 1:
             import torch.distributed as dist
@@ -916,6 +927,8 @@ def main():
         rec["pu_c3"] = c3
     if c3w is not None:
         rec["pu_c3_weak"] = c3w
+    if c3r is not None:
+        rec["pu_c3_ref6000"] = c3r
     if ws == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(path, wl, args.cpu_seconds)
     print(json.dumps(rec), flush=True)

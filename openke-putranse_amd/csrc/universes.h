@@ -35,6 +35,12 @@ struct UniverseDev {
 #define PT_UNI_NT 1024
 #endif
 constexpr int universe_class_threads(int model, int cls) { return model == 0 && cls < 2 ? PT_UNI_NT : 512; }
+// workgroup size of a hot single-shape kernel for lane groups of G lanes: PT_UNI_HOT_WIDE_NT for the wide rows
+// (G >= 32: C4's D = 200 on 32 lanes x 8 floats), the class size otherwise
+#ifndef PT_UNI_HOT_WIDE_NT
+#define PT_UNI_HOT_WIDE_NT 1024
+#endif
+constexpr int universe_hot_threads(int G) { return G >= 32 ? PT_UNI_HOT_WIDE_NT : PT_UNI_NT; }
 // class ids from kUniHotBase on: a "hot" class-1 shape (id - kUniHotBase) run by a kernel compiled for that shape
 // alone (its own register allocation; see pt_universe_set_create)
 constexpr int kUniHotBase = 64;

@@ -956,11 +956,11 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
 }  // namespace dev
 
 namespace detail {
-template <int MODEL, int WPE, int CLS, int PLAN>
+template <int MODEL, int WPE, int CLS, int PLAN, int HOT_G = 0>
 hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int64_t cus, int p_norm, int norm_flag, int opt,
                     int64_t neg, int bern, int filter, const UniverseLaunch &cfg, hipStream_t st) {
-    // (a hot single-shape kernel runs a class-1 shape: that class's workgroup size)
-    constexpr int NT = universe_class_threads(MODEL, CLS < kUniHotBase ? CLS : 1);
+    // (a hot single-shape kernel runs a class-1 shape: that class's workgroup size, or universe_hot_threads)
+    constexpr int NT = CLS < kUniHotBase ? universe_class_threads(MODEL, CLS) : universe_hot_threads(HOT_G);
     auto kern = dev::k_universes<MODEL, NT, WPE * NT / 512, CLS, PLAN>;
     if (cfg.lds_bytes > (64 << 10)) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -997,8 +997,8 @@ hipError_t launch_universes_plan(const UniverseDev *d_us, int64_t n, int *counte
 #define PT_UHOT(ID_, G_, V_, K_)                                                                                  \
     case ID_:                                                                                                      \
         if constexpr (PT_UCLASS(V_, K_) == 1 && dev::shape_reachable(0, G_, V_, K_))                                \
-            return launch_q<0, 2, kUniHotBase + ID_, PLAN>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg, bern, \
-                                                          filter, cfg, st);                                        \
+            return launch_q<0, 2, kUniHotBase + ID_, PLAN, G_>(d_us, n, counter, cus, p_norm, norm_flag, opt, neg,  \
+                                                              bern, filter, cfg, st);                                \
         break;
                     PT_USHAPES(PT_UHOT)
 #undef PT_UHOT
