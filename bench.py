@@ -630,8 +630,14 @@ def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
     _native.check(L.pt_lp_metrics(ranks[0].ctypes.data, ranks[1].ctypes.data, ranks[2].ctypes.data,
                                   ranks[3].ctypes.data, n, met.ctypes.data))
     L.pt_known_free(known)
-    cand = sum(len(u["em"]) for u in unis)
+    # scored (pair, candidate) cells: every local entity of the pair's universe (k_lp_scan_t: one lane per entity,
+    # the pair's base row uniform across the wave; per cell and dim one LDS read and ~3 VALU lane-operations)
+    ent_of = np.array([len(u["em"]) for u in unis], dtype=np.int64)
+    cells = int(ent_of[pair_arr[:, 1]].sum()) if len(pair_arr) else 0
+    dim_of = np.array([u["dim"] for u in unis], dtype=np.int64)
+    cell_dims = int((ent_of[pair_arr[:, 1]] * dim_of[pair_arr[:, 1]]).sum()) if len(pair_arr) else 0
     return {"queries": int(n), "keys": len(keys), "pairs_this_rank": len(pair_arr), "seconds": el,
+            "scored_cells": cells, "scored_cell_dims": cell_dims,
             "score_s": t_score, "min_combine_s": t_comb, "rank_s": el - t_score - t_comb,
             "mrr_mr_hit10_hit3_hit1": [float(x) for x in met[:5]],
             "note": "universe scoring 4D+4 B per (key, universe entity); ranking 4 B per (query, entity)"}

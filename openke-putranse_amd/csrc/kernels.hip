@@ -841,6 +841,34 @@ __device__ __forceinline__ float sum8(int D, F f) {
     return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
+// NP sums of the sum8 form (the same partial sums and combination order for each) over one pass of d: the
+// caller's function f(q, d) for sum q reads shared operands (the LDS row) once for all of them
+template <int NP, typename F>
+__device__ __forceinline__ void sum8xn(int D, F f, float (&r)[NP]) {
+    float a[NP][8];
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[q][k] = 0.f;
+    int d = 0;
+    for (; d + 8 <= D; d += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int q = 0; q < NP; ++q) a[q][k] += f(q, d + k);
+    }
+    for (int k = 0; d + k < D; ++k)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) a[q][k] += f(q, d + k);
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+        r[q] = ((a[q][0] + a[q][1]) + (a[q][2] + a[q][3])) + ((a[q][4] + a[q][5]) + (a[q][6] + a[q][7]));
+}
+
+#ifndef PT_LP_PAIRS
+#define PT_LP_PAIRS 2   // (measured r05, C4 k_lp_scan_t total: 1 pair 137.9 ms, 2 pairs 99.4, 4 pairs 105.3, 8 pairs 128.5)
+#endif
+
 template <int MODEL>
 __global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
                                                    const int64_t *__restrict__ uoff, const int32_t *__restrict__ uids,
@@ -863,14 +891,58 @@ __global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restri
         }
         __syncthreads();
         const bool live = lane < ne;
-        const float *xr = s_x + (live ? lane : 0) * S;
+        float *xr = s_x + (live ? lane : 0) * S;
         const int64_t col = live ? U.remap[e0 + lane] : 0;
         float inv = 1.f;
         if (MODEL == 0 && norm_flag) {   // F.normalize's scale of this lane's row
             const float n = sqrtf(sum8(D, [&](int d) { return xr[d] * xr[d]; }));
             inv = 1.0f / (n > kEps ? n : kEps);
         }
-        for (int64_t pi = p0 + wave; pi < p1; pi += 4) {
+        int64_t pi = p0 + wave;
+        if constexpr (MODEL == 0) {
+            // TransE: the tile's rows normalized in place once (x * inv: the same rounded products the per-pair form
+            // computed), then the wave's pairs PT_LP_PAIRS at a time - pi, pi + 4, ... share every LDS read of the row. Each
+            // score keeps its expression and its sum8 order, so the scores are bit-identical to one pair at a time.
+            // (the four waves share the tile: every wave has read it for its norm, then wave 0 normalizes it while
+            // the others wait)
+            __syncthreads();
+            if (wave == 0 && live && norm_flag) {
+                for (int d = 0; d < D; ++d) xr[d] = xr[d] * inv;
+            }
+            __syncthreads();
+            constexpr int NPP = PT_LP_PAIRS;   // pairs per pass: pi, pi + 4, ..., pi + 4 (NPP - 1)
+            for (; pi + 4 * (NPP - 1) < p1; pi += 4 * NPP) {
+                LpPair pr[NPP];
+                const float *bq[NPP];
+                float sg[NPP], acc[NPP];
+#pragma unroll
+                for (int q = 0; q < NPP; ++q) {
+                    pr[q] = pairs[pi + 4 * q];
+                    bq[q] = base + (pi + 4 * q) * ds;
+                    sg[q] = pr[q].side == 0 ? 1.f : -1.f;
+                }
+                if (p_norm == 1)
+                    sum8xn<NPP>(D, [&](int q, int d) { return fabsf(sg[q] * xr[d] + bq[q][d]); }, acc);
+                else
+                    sum8xn<NPP>(D,
+                                [&](int q, int d) {
+                                    const float v = sg[q] * xr[d] + bq[q][d];
+                                    return v * v;
+                                },
+                                acc);
+                if (live) {
+#pragma unroll
+                    for (int q = 0; q < NPP; ++q) {
+                        const float sc = p_norm == 1 ? acc[q] : sqrtf(acc[q]);
+                        int *cell = reinterpret_cast<int *>(rows + (int64_t)pr[q].key * global_E + col);
+                        const int bits = __float_as_int(sc);
+                        if (bits < *cell) atomicMin(cell, bits);
+                    }
+                }
+            }
+            inv = 1.f;   // (the row is normalized in LDS now)
+        }
+        for (; pi < p1; pi += 4) {
             const LpPair pr = pairs[pi];
             const float *b = base + pi * ds;
             const float sg = pr.side == 0 ? 1.f : -1.f;   // side 0: x-hat + b; side 1: b - x-hat
