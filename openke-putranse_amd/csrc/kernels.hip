@@ -851,6 +851,8 @@ __device__ __forceinline__ void sum8xn(int D, F f, float (&r)[NP]) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) a[q][k] = 0.f;
     int d = 0;
+    // (two 8-dim groups per iteration: the next group's operand loads issue before the current group's waits)
+#pragma unroll 2
     for (; d + 8 <= D; d += 8) {
 #pragma unroll
         for (int k = 0; k < 8; ++k)
@@ -876,7 +878,9 @@ __global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restri
                                                    const float *__restrict__ base, const float *__restrict__ normal,
                                                    float *__restrict__ rows) {
     extern __shared__ float s_x[];   // [64][D + 1]
-    const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+    // (the wave index made provably uniform: the pair walk, its LpPair records and base rows then live in scalar
+    // registers and load through the scalar cache, instead of every lane loading the same base-row words)
+    const int lane = (int)threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int32_t u = uids[blockIdx.y];
     const LpUniverseDev U = us[u];
     const int D = (int)U.dim, S = D + 1;
@@ -915,11 +919,16 @@ __global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restri
                 LpPair pr[NPP];
                 const float *bq[NPP];
                 float sg[NPP], acc[NPP];
+                int *cell[NPP];
+                int old[NPP];
 #pragma unroll
                 for (int q = 0; q < NPP; ++q) {
                     pr[q] = pairs[pi + 4 * q];
                     bq[q] = base + (pi + 4 * q) * ds;
                     sg[q] = pr[q].side == 0 ? 1.f : -1.f;
+                    // the key-row cells this pass may lower, read before the sums (their latency hidden behind them)
+                    cell[q] = reinterpret_cast<int *>(rows + (int64_t)pr[q].key * global_E + col);
+                    old[q] = live ? __builtin_nontemporal_load(cell[q]) : 0;
                 }
                 if (p_norm == 1)
                     sum8xn<NPP>(D, [&](int q, int d) { return fabsf(sg[q] * xr[d] + bq[q][d]); }, acc);
@@ -934,9 +943,8 @@ __global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restri
 #pragma unroll
                     for (int q = 0; q < NPP; ++q) {
                         const float sc = p_norm == 1 ? acc[q] : sqrtf(acc[q]);
-                        int *cell = reinterpret_cast<int *>(rows + (int64_t)pr[q].key * global_E + col);
                         const int bits = __float_as_int(sc);
-                        if (bits < *cell) atomicMin(cell, bits);
+                        if (bits < old[q]) atomicMin(cell[q], bits);
                     }
                 }
             }
