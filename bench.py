@@ -698,6 +698,9 @@ def main():
                          "reference experiment uses 100)")
     ap.add_argument("--no-ref-scale", action="store_true",
                     help="default line: skip the pu_c3_ref6000 field (6,000 universes, dim 20, strong scaling)")
+    ap.add_argument("--slot-scale", type=int, default=-1,
+                    help="C2 / C1: 1 = slot-scale mode (per-slot records + positive base rows instead of contribution "
+                         "rows; pt_trainer_set_slot_scale), 0 = contribution rows, -1 = the library's default")
     ap.add_argument("--no-dropin", action="store_true",
                     help="universe workloads: skip the drop-in Parallel_Universe_Config timing")
     ap.add_argument("--launch-check", action="store_true",
@@ -778,6 +781,8 @@ def main():
     tr.run()   # moves the tables to HBM and builds the native trainer; no steps
     L = _native.lib()
     _native.check(L.pt_trainer_set_step_apply(tr._native, args.step_apply))
+    if args.slot_scale >= 0:
+        _native.check(L.pt_trainer_set_slot_scale(tr._native, args.slot_scale))
     sampler = dl.device_sampler()
     dev = torch.device("cuda", torch.cuda.current_device())
     seq = bs * (1 + neg)
@@ -840,6 +845,7 @@ def main():
     # the sampling kernels of the path the library took for this chunking (pt_trainer_last_path)
     spath = L.pt_trainer_last_path(tr._native)
     fused_sa = bool(L.pt_trainer_step_apply(tr._native))
+    slot_sc = bool(L.pt_trainer_slot_scale(tr._native)) if hasattr(L, "pt_trainer_slot_scale") else False
     step_names = (["k_step_apply", "k_loss_calls"] if fused_sa else
                   ["k_step_csr", "k_apply_buf"] if spath != _native.PT_PATH_SAMPLED else ["k_step_sampled", "k_apply"])
     names = list(_native.PATH_KERNELS.get(spath, ("sampling", "bucket scan"))) + step_names
@@ -855,7 +861,9 @@ def main():
         b = next((v for k, v in counted.items() if kname in k), None) if counted else None
         kernel_detail[kname] = {"ms": ms, "counted_bytes": b,
                                 "counted_TBps": None if b is None or ms <= 0 else b / (ms * 1e-3) / 1e12}
-    contrib_rt = 2 * bs * neg * dim * 4   # gradient rows of the corrupted entities: stored by the step, read by apply
+    # gradient rows of the corrupted entities: stored by the step, read by apply (slot-scale mode: an 8-byte record
+    # per slot and three base rows per positive instead)
+    contrib_rt = 2 * (bs * neg * 8 + bs * 3 * dim * 4) if slot_sc else 2 * bs * neg * dim * 4
 
     c3 = None if args.no_c3 else run_universes(args, ws, rank, dev, "c3", cpu=True)
     if c3 is not None and ws == 1 and not args.no_dropin:
@@ -911,6 +919,7 @@ def main():
                      "lib_sha256": library_sha256(), "counters_lib_sha256": pmc_sha,
                      "counters_match_build": pmc is not None,
                      "step_apply_fused": fused_sa,
+                     "slot_scale": slot_sc,
                      "contrib_roundtrip_bytes": contrib_rt if spath != _native.PT_PATH_SAMPLED else 0,
                      "contrib_share_of_counted": None if traffic is None or spath == _native.PT_PATH_SAMPLED
                      else contrib_rt / traffic,

@@ -143,6 +143,12 @@ int pt_trainer_last_path(const pt_trainer *t);
  * on = 0 keeps the step + apply pair. Default off (measured slower at C2: DESIGN.md section 4). Results
  * equal the pair's up to float-atomic order. */
 int pt_trainer_set_step_apply(pt_trainer *t, int32_t on);
+/* slot-scale mode (opt-in; TransE float4 rows on the counting-sort path): the step stores per (positive, negative)
+ * slot a record (positive, side, one scalar) and per positive its three normalized rows instead of the corrupted
+ * entity's gradient row, and the apply pass re-forms each slot's row from them and the entity's own row
+ * (CsrWork::slot_scale). pt_trainer_slot_scale: 1 when the current workspace is carved for it. */
+int pt_trainer_set_slot_scale(pt_trainer *t, int32_t on);
+int pt_trainer_slot_scale(const pt_trainer *t);
 /* whether the last enqueued in-kernel-sampled steps took the fused step + apply (ms4[2] of
  * pt_trainer_run_timed is then that kernel, ms4[3] the chunks' loss reduction) */
 int pt_trainer_step_apply(const pt_trainer *t);

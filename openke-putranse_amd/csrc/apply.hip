@@ -52,6 +52,11 @@ struct ApplyParams {
     float margin, inv_count;
     int dbg;   // timing experiments only (PT_STEP_DBG bit 3: contribution rows read from a 4096-row hot window)
     int loss_assign;
+    // slot-scale mode (CsrWork::slot_scale): the step's slot records and positive base rows, the model's p and
+    // norm_flag (k_apply_buf<..., true>)
+    const int2 *srec;
+    const float *bases;
+    int p_norm, norm_flag;
 };
 
 // block 0, first wave: advance the sampler streams and reduce the step's loss partials in a fixed
@@ -151,7 +156,7 @@ __global__ __launch_bounds__(256) void k_apply(ApplyParams A) {
 // loads return; a bucket's contribution rows stream NC at a time with out-of-range offsets past its
 // end (the hardware returns zeros, so the adds need no branches), summed in bucket order after the
 // row's own gradient row.
-template <int G, int VEC, int KCH, int NC, int RPW>
+template <int G, int VEC, int KCH, int NC, int RPW, bool SC = false>
 __global__ __launch_bounds__(256) void k_apply_buf(ApplyParams A) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = 256 / G;
@@ -200,6 +205,49 @@ __global__ __launch_bounds__(256) void k_apply_buf(ApplyParams A) {
         bload(g[u], make_rsrc(T.grad, (uint32_t)T.rows * rowb), flag[u] ? (uint32_t)row[u] * rowb : kOob, D, lane);
         len = c1[u] - c0[u] > len ? c1[u] - c0[u] : len;
     }
+    if constexpr (SC) {
+#pragma clang fp contract(off)   // (k v and the sum stay two roundings, as the stored row and its add were)
+        // slot-scale mode (CsrWork::slot_scale): each slot's row re-formed from its record and its positive's
+        // normalized rows with the step kernel's own operations - e-hat = normalize(x) (fast form), v = b-hat - e-hat
+        // (a corrupted tail) or (e-hat + r-hat) - t-hat (a corrupted head), then k v (p = 2) or k sign(v) (p = 1)
+        // - and summed in bucket order: the bits the stored contribution rows held
+        const auto b_rs = make_rsrc(A.bases, 0x7fffffffu);
+#pragma unroll
+        for (int u = 0; u < RPW; ++u) {
+            if (!live[u] || ti[u] != 0 || c0[u] == c1[u]) continue;
+            Vec eh;
+            if (A.norm_flag) vnormalize<true>(x[u], eh); else eh = x[u];
+            for (int j = c0[u]; j < c1[u]; j += NC) {
+                int2 rc[NC];
+#pragma unroll
+                for (int q = 0; q < NC; ++q) {
+                    const int2 r = j + q < c1[u] ? A.srec[j + q] : make_int2(0, 0);
+                    rc[q] = make_int2(uni<G>(r.x), uni<G>(r.y));
+                }
+                Vec ra[NC], rb[NC];
+#pragma unroll
+                for (int q = 0; q < NC; ++q) {
+                    const bool ok = j + q < c1[u];
+                    const uint32_t pb = (uint32_t)(rc[q].x >> 1) * 3u;
+                    const bool tail = rc[q].x & 1;
+                    bload(ra[q], b_rs, ok ? (tail ? pb : pb + 1u) * rowb : kOob, D, lane);
+                    bload(rb[q], b_rs, ok && !tail ? (pb + 2u) * rowb : kOob, D, lane);
+                }
+#pragma unroll
+                for (int q = 0; q < NC; ++q) {
+                    if (j + q >= c1[u]) break;
+                    const bool tail = rc[q].x & 1;
+                    const float kk = __int_as_float(rc[q].y);
+#pragma unroll
+                    for (int i = 0; i < Vec::N; ++i) {
+                        const float vk = tail ? ra[q].x[i] - eh.x[i] : (eh.x[i] + ra[q].x[i]) - rb[q].x[i];
+                        const float gs = A.p_norm == 1 ? (vk > 0.f ? kk : (vk < 0.f ? -kk : 0.f)) : vk * kk;
+                        g[u].x[i] += gs;
+                    }
+                }
+            }
+        }
+    } else {
     // contribution rows (entity table only): the rows' buckets streamed side by side, NC per row at a
     // time, out-of-range past each bucket's end (zeros), summed in bucket order
     const auto c_rs = make_rsrc(A.t[0].contrib, 0x7fffffffu);
@@ -219,6 +267,7 @@ __global__ __launch_bounds__(256) void k_apply_buf(ApplyParams A) {
             for (int q = 0; q < NC; ++q)
 #pragma unroll
                 for (int i = 0; i < Vec::N; ++i) g[u].x[i] += c[u][q].x[i];
+    }
     }
 #pragma unroll
     for (int u = 0; u < RPW; ++u) {
@@ -388,6 +437,11 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
     A.inv_count = P.inv_count;
     A.dbg = P.dbg;
     A.loss_assign = P.loss_assign;
+    const bool sc = csr && csr->slot_scale;
+    A.srec = sc ? csr->srec : nullptr;
+    A.bases = sc ? csr->bases : nullptr;
+    A.p_norm = P.p_norm;
+    A.norm_flag = P.norm_flag;
     int64_t rows = 0;
     for (int i = 0; i < A.ntab; ++i) rows += A.t[i].rows;
     // float4 rows through raw buffers (PT_APPLY_OLD=1 keeps the kernels below)
@@ -413,7 +467,10 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
         const dim3 grid((unsigned)((groups + gpb4 - 1) / gpb4)), block(256);
 #define PT_APPLYB(G_, K_, N_, R_)                                                              \
         if (G == G_ && KCH == K_ && nc == N_ && rpw == R_) {                                  \
-            hipLaunchKernelGGL((dev::k_apply_buf<G_, 4, K_, N_, R_>), grid, block, 0, st, A);   \
+            if (sc)                                                                             \
+                hipLaunchKernelGGL((dev::k_apply_buf<G_, 4, K_, N_, R_, true>), grid, block, 0, st, A); \
+            else                                                                                \
+                hipLaunchKernelGGL((dev::k_apply_buf<G_, 4, K_, N_, R_>), grid, block, 0, st, A); \
             return hipGetLastError();                                                         \
         }
         PT_APPLYB(2, 1, 4, 1) PT_APPLYB(4, 1, 4, 1) PT_APPLYB(8, 1, 4, 1) PT_APPLYB(16, 1, 4, 1)
@@ -422,6 +479,7 @@ hipError_t launch_apply(const StepParams &P, const StepWorkspace &W, uint64_t *s
         PT_APPLYB(64, 1, 2, 4) PT_APPLYB(64, 1, 1, 4)
 #undef PT_APPLYB
     }
+    if (sc) return hipErrorInvalidValue;   // slot records are read only by k_apply_buf
     const int64_t gpb = 256 / s.G;
     // PT_APPLY_RPW=2|4: several rows per lane group with one contribution stream (measured slower on
     // C2: 20.4 / 22.0 us vs 16.8 us for one row per group, which stays the default)

@@ -75,6 +75,7 @@ struct pt_trainer {
     // arrival words live in the counting-sort workspace (fr.gent == nullptr: not carved for it)
     pt::FusedRows fr{};
     bool step_apply_on = false;                         // pt_trainer_set_step_apply (opt-in: measured slower)
+    bool slot_scale_on = false;                         // pt_trainer_set_slot_scale (CsrWork::slot_scale)
     bool last_step_apply = false;                       // the last enqueued in-kernel-sampled steps took it
     bool csr_part = false;                              // k_sample_part prepared (its LDS limit raised)
     int last_path = -1;                                 // sampling path of the last enqueued chunk (PT_PATH_*)
@@ -353,6 +354,15 @@ static bool step_apply_wanted(const pt_trainer *t) {
     return t->step_apply_on && forced != 0;
 }
 
+// whether the slot-scale mode is wanted (pt_trainer_set_slot_scale; the tuning build's PT_SLOT_SCALE forces it)
+static bool slot_scale_wanted(const pt_trainer *t) {
+    static const int forced = [] {
+        const char *v = pt_tuning_env("PT_SLOT_SCALE");
+        return v ? atoi(v) : -1;
+    }();
+    return forced >= 0 ? forced != 0 : t->slot_scale_on;
+}
+
 // Workspace of the counting-sort path, carved once per (bs, neg): room for a chunk of pre-sampled
 // steps (<= kCsrChunk, fewer when a step's arrays are large) plus one step's gradient rows. A new
 // (bs, neg) re-carves it (and drops captured graphs, whose kernels hold the old pointers).
@@ -373,9 +383,13 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     chunk = std::min(chunk, kCsrChunk);
     const size_t a_use = sa ? al(4 * us * chunk) : 0, a_lp = sa ? al(4 * bs * chunk) : 0,
                  a_gent = sa ? al(4 * E * dp) : 0, a_grel = sa ? al(4 * R * dp) : 0, a_arr = sa ? al(8 * (E + R)) : 0;
+    // slot-scale mode: the step's slot records and positive base rows take the contribution region's place
+    // (TransE float4 rows: the k_step_csr / k_apply_buf pair; not with the fused step + apply)
+    const bool scm = slot_scale_wanted(t) && !sa && t->P.model == 0 && D % 4 == 0;
+    const size_t a_srec = al(8 * bs * neg), a_bases = al(4 * bs * 3 * D);
     const size_t a_pos = al(16 * bs * chunk), a_neg = al(4 * bs * neg * chunk), a_off = a_neg,
                  a_cnt = al(4 * cs * chunk), a_start = al(4 * ss * chunk), a_tick = al(4 * chunk + 4),
-                 a_con = al(4 * bs * neg * dp);
+                 a_con = std::max(al(4 * bs * neg * dp), scm ? a_srec + a_bases : (size_t)0);
     const size_t need = a_use + a_lp + a_gent + a_grel + a_arr + a_pos + a_neg + a_off + a_cnt + a_start + a_tick + a_con;
     PT_HIP(hipDeviceSynchronize());   // queued work may still use the old carving
     t->drop_graphs();
@@ -404,6 +418,9 @@ static int ensure_csr(pt_trainer *t, int64_t bs, int64_t neg) {
     t->csr.start = (int32_t *)b; b += a_start;
     t->csr.tick = (int32_t *)b; b += a_tick;
     t->csr.contrib = (float *)b;
+    t->csr.slot_scale = scm ? 1 : 0;
+    t->csr.srec = scm ? (int2 *)b : nullptr;
+    t->csr.bases = scm ? (float *)(b + a_srec) : nullptr;
     t->csr.cnt_stride = cs;
     t->csr.start_stride = ss;
     t->csr_bs = bs;
@@ -840,6 +857,15 @@ extern "C" int pt_trainer_set_step_apply(pt_trainer *t, int32_t on) {
     return PT_OK;
 }
 extern "C" int pt_trainer_step_apply(const pt_trainer *t) { return t && t->last_step_apply ? 1 : 0; }
+
+extern "C" int pt_trainer_set_slot_scale(pt_trainer *t, int32_t on) {
+    PT_CHECK(t, PT_EINVAL, "null trainer");
+    if (t->slot_scale_on != (on != 0)) t->csr_bs = 0;   // re-carve the workspace (slot records / base rows)
+    t->slot_scale_on = on != 0;
+    t->drop_graphs();
+    return PT_OK;
+}
+extern "C" int pt_trainer_slot_scale(const pt_trainer *t) { return t && t->csr.slot_scale ? 1 : 0; }
 
 extern "C" int pt_trainer_last_path(const pt_trainer *t) { return t ? t->last_path : -1; }
 

@@ -54,6 +54,15 @@ struct CsrWork {
     int32_t *uses = nullptr;
     int64_t use_stride = 0, rel_base = 0;
     float *lpart = nullptr;
+    // slot-scale mode (pt_trainer_set_slot_scale, k_step_csr + k_apply_buf): instead of a corrupted entity's
+    // gradient row, the step stores per slot (at its counting-sort destination) the positive (b << 1 | tail side)
+    // and the scalar k of d loss / d v = k v (p = 2) or k sign(v) (p = 1), plus per positive its normalized rows
+    // (h-hat + r-hat, r-hat, t-hat) in `bases` ([bs][3][dim]); the apply pass re-forms each slot's row from them
+    // and the entity's own row - the same operations, so the same bits - in bucket order. srec and bases live in
+    // the contrib region (one step).
+    int slot_scale = 0;
+    int2 *srec = nullptr;
+    float *bases = nullptr;
 };
 
 inline CsrWork csr_view(const CsrWork &w, int64_t call, int64_t bs, int64_t neg) {

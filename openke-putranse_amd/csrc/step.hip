@@ -423,6 +423,13 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
             vpos.x[i] = bt.x[i] - th.x[i];
         }
         ps = vpnorm<true>(vpos, p);
+        const bool scale_mode = cw.slot_scale != 0;
+        if (scale_mode && sub == 0) {   // the positive's normalized rows, for the apply pass to re-form slot rows
+            const auto base_rs = make_rsrc(cw.bases, (uint32_t)(P.batch_size * 3) * rowb);
+            bstore(bt, base_rs, (uint32_t)(b * 3) * rowb, D, lane);
+            bstore(rh, base_rs, (uint32_t)(b * 3 + 1) * rowb, D, lane);
+            bstore(th, base_rs, (uint32_t)(b * 3 + 2) * rowb, D, lane);
+        }
         auto process = [&](Vec(&E)[NCH], int k0) {
 #pragma unroll
             for (int u = 0; u < NCH; ++u) {
@@ -433,12 +440,15 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
                 const bool tail_side = r & 1;
                 Vec eh, vk, gs;
                 if (nf) vnormalize<true>(E[u], eh); else eh = E[u];
-                if (tail_side) {
+                {
+#pragma clang fp contract(off)   // e-hat's product stays rounded: k_apply_buf's slot-scale mode re-forms v the same way
+                    if (tail_side) {
 #pragma unroll
-                    for (int i = 0; i < Vec::N; ++i) vk.x[i] = bt.x[i] - eh.x[i];
-                } else {
+                        for (int i = 0; i < Vec::N; ++i) vk.x[i] = bt.x[i] - eh.x[i];
+                    } else {
 #pragma unroll
-                    for (int i = 0; i < Vec::N; ++i) vk.x[i] = (eh.x[i] + rh.x[i]) - th.x[i];
+                        for (int i = 0; i < Vec::N; ++i) vk.x[i] = (eh.x[i] + rh.x[i]) - th.x[i];
+                    }
                 }
                 const float ns = vpnorm<true>(vk, p);
                 const float a = uni<G>(ps - ns);
@@ -448,7 +458,15 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
                 // slot gradient d loss / d e-hat: -g for a corrupted tail, +g for a corrupted head
                 // (g = dL/dv); an inactive pair stores zeros (the reserved slot must be defined)
                 vpnorm_bwd<true>(vk, ns, p, tail_side ? c : -c, gs);
-                bstore(gs, con_rs, PT_ABLATE(P.dbg, 1) ? kOob : slot, D, lane);
+                if (scale_mode) {
+                    // the slot's record: its positive and side, and vpnorm_bwd's scalar (p = 2: ds / ns as the
+                    // fast form computes it, p = 1: ds) - the apply pass forms gs again from them
+                    const float ds = tail_side ? c : -c;
+                    const float kk = p == 1 ? ds : (ns == 0.f ? 0.f : ds * frcp<true>(ns));
+                    if (lane == 0) cw.srec[di] = make_int2((int32_t)(b << 1) | (tail_side ? 1 : 0), __float_as_int(kk));
+                } else {
+                    bstore(gs, con_rs, PT_ABLATE(P.dbg, 1) ? kOob : slot, D, lane);
+                }
                 if (tail_side) {
 #pragma unroll
                     for (int i = 0; i < Vec::N; ++i) At.x[i] -= gs.x[i];

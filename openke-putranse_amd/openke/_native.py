@@ -119,6 +119,8 @@ SIGNATURES = {
     "pt_universe_set_launch_times": (ctypes.c_int, [c_vp, ctypes.c_int64, c_vp, c_vp]),
     "pt_universes_train": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
                                           c_i64, c_vp, c_vp]),
+    "pt_trainer_set_slot_scale": (ctypes.c_int, [c_vp, c_i32]),
+    "pt_trainer_slot_scale": (ctypes.c_int, [c_vp]),
     "pt_torch_init_tables": (ctypes.c_int, [ctypes.POINTER(TorchInitJob), c_i64, c_vp]),
     "pt_universes_train_ex": (ctypes.c_int, [ctypes.POINTER(UniverseJob), c_i64, c_i32, c_i32, c_i32, c_i32, c_i64,
                                              c_i64, c_i32, c_vp, c_vp]),

@@ -640,6 +640,26 @@ TF_CASES = [
 @pytest.mark.parametrize("case", TF_CASES, ids=lambda c: "%s-d%d-p%d-nf%d-%s-bs%d-neg%d" % (c[0], c[1], c[2], c[3],
                                                                                          c[4], c[5], c[6]))
 def test_fast_trainer_steps_teacher_forced(case):
+    _teacher_forced_trainer(case)
+
+
+# the slot-scale mode (pt_trainer_set_slot_scale) teacher-forced the same way: TransE float4 rows on the
+# counting-sort path (neg >= 4), SGD and Adagrad, p 1 and 2, with and without normalization
+TF_SC_CASES = [
+    ("TransE", 200, 2, True, "sgd", 120, 25, 1, 1, 6),
+    ("TransE", 100, 2, False, "adagrad", 48, 12, 1, 1, 10),
+    ("TransE", 200, 1, True, "adagrad", 48, 9, 1, 1, 8),
+    ("TransE", 12, 1, True, "sgd", 40, 6, 0, 1, 10),
+]
+
+
+@pytest.mark.parametrize("case", TF_SC_CASES, ids=lambda c: "%s-d%d-p%d-nf%d-%s-bs%d-neg%d" % (c[0], c[1], c[2], c[3],
+                                                                                            c[4], c[5], c[6]))
+def test_slot_scale_steps_teacher_forced(case):
+    _teacher_forced_trainer(case, slot_scale=1)
+
+
+def _teacher_forced_trainer(case, slot_scale=0):
     from openke import _native
     from openke.module.model import TransE, TransH
     model, dim, p, nf, opt, bs, neg, bern, filt, steps = case
@@ -660,6 +680,8 @@ def test_fast_trainer_steps_teacher_forced(case):
     st = oracle.GlibcRand(seed).rand_reset(8)
     _native.check(L.pt_sampler_create(g, 8, st.ctypes.data, ctypes.byref(smp)))
     _native.check(L.pt_trainer_create(ctypes.byref(desc), ctypes.byref(tr)))
+    if slot_scale:
+        _native.check(L.pt_trainer_set_slot_scale(tr, 1))
     try:
         loss = torch.zeros(1, device="cuda")
         for k in range(steps):
@@ -689,6 +711,8 @@ def test_fast_trainer_steps_teacher_forced(case):
                 mask = step_noise(acc0[i], accs[i], got_acc[i]) if ada else None
                 assert_step_close(got[i], w, 2e-6, mask, what="step %d %s" % (k, name), before=tab0[i],
                                   gm=gm[name], lr=lr, acc_before=acc0[i])
+        if slot_scale:
+            assert L.pt_trainer_slot_scale(tr) == 1
         # the streams advanced exactly like one sampling() call per step
         nxt = np.zeros(8, dtype=np.uint64)
         _native.check(L.pt_sampler_get_seeds(smp, nxt.ctypes.data))
@@ -698,3 +722,39 @@ def test_fast_trainer_steps_teacher_forced(case):
         L.pt_trainer_free(tr)
         L.pt_sampler_free(smp)
         L.pt_graph_free(g)
+
+
+# The slot-scale mode (pt_trainer_set_slot_scale: per-slot records and per-positive base rows instead of the
+# corrupted entities' gradient rows; the apply pass re-forms every slot's row with the step kernel's own
+# operations) against the contribution-row pair, from the same tables over 12 SGD steps (p 1 and 2). The re-formed
+# rows are the stored rows' operations; the runs differ only by the order of the positive rows' float atomics,
+# which SGD passes on at rounding level (tolerance 1e-6). Adagrad turns such noise into +-lr steps: the mode is
+# teacher-forced against the oracle instead (test_slot_scale_steps_teacher_forced).
+@pytest.mark.parametrize("case", [(200, 2, True, "sgd", 64, 25), (200, 1, True, "sgd", 48, 9),
+                                  (12, 2, True, "sgd", 40, 6), (64, 1, False, "sgd", 32, 7)],
+                         ids=lambda c: "d%d_p%d_%s_neg%d" % (c[0], c[1], c[3], c[5]))
+def test_slot_scale_matches_contribution_rows(case):
+    from openke import _native
+    from openke.config import Trainer
+    from openke.module.loss import MarginLoss
+    from openke.module.model import TransE
+    from openke.module.strategy import NegativeSampling
+    dim, p, nf, opt, bs, neg = case
+    steps, lr, margin, seed = 12, (0.5 if opt == "sgd" else 0.1), 4.0, 11
+    runs = {}
+    for sc in (1, 0):
+        dl = _loader_path(KG_SMALL, 8, bs, neg, 1, 1, seed)
+        dl.nbatches = steps
+        torch.manual_seed(dim + neg)
+        kge = TransE(dl.get_ent_tot(), dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=nf)
+        ns = NegativeSampling(model=kge, loss=MarginLoss(margin=margin), batch_size=bs)
+        tr = Trainer(model=ns, data_loader=dl, train_times=1, alpha=lr, use_gpu=True, opt_method=opt)
+        tr._setup()
+        _native.check(_native.lib().pt_trainer_set_slot_scale(tr._native, sc))
+        tr.run()
+        assert _native.lib().pt_trainer_slot_scale(tr._native) == sc
+        runs[sc] = (tr.last_epoch_loss, _tables(kge))
+    (l1, t1), (l0, t0) = runs[1], runs[0]
+    np.testing.assert_allclose(l1, l0, rtol=1e-6)
+    for k in t1:
+        np.testing.assert_allclose(t1[k], t0[k], atol=1e-6, rtol=0)
