@@ -286,6 +286,15 @@ typedef struct {
 typedef struct {
     int32_t key, universe, anchor, rel, side;   /* anchor / rel are universe-LOCAL ids */
 } pt_lp_pair;
+/* The pairs above for every key and universe (host only; the universes eval_universes scores per key,
+ * Parallel_Universe_Config.py:470-476): universe u (< 2^31) holds the global entities ent_ids[ent_off[u] ..
+ * ent_off[u + 1]) and relations rel_ids[rel_off[u] .. rel_off[u + 1]) in local order; key k is (key_side[k],
+ * key_anchor[k], key_rel[k]) in global ids. Rows (k, u, local anchor, local relation, side) for every u holding
+ * both, ordered by key then universe. With out == NULL *n_out is an upper bound on the rows (the keys' anchor
+ * occurrences); with out, *n_out is the rows written (PT_EINVAL if more than cap). */
+int pt_lp_pairs(int64_t n, const int64_t *ent_off, const int64_t *ent_ids, const int64_t *rel_off,
+                const int64_t *rel_ids, int64_t n_keys, const int64_t *key_anchor, const int64_t *key_rel,
+                const int64_t *key_side, pt_lp_pair *out, int64_t cap, int64_t *n_out);
 int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, int32_t model, int32_t p_norm,
                      int32_t norm_flag, const pt_lp_pair *pairs, int64_t n_pairs, int64_t global_ent_total,
                      float *d_key_rows, float *d_key_tuple, void *stream);
@@ -324,6 +333,35 @@ int pt_known_partners(const pt_known *k, int32_t side, int64_t n, const int64_t 
                       int64_t *off, int64_t *list);
 int pt_rank_queries(const pt_known *k, int64_t ent_total, const int64_t *h, const int64_t *t, const int64_t *r,
                     int64_t n, int32_t side, const float *con, int64_t *raw, int64_t *filt, int64_t n_workers);
+
+/* Checkpoint encoding of the universe id maps (host only; save_parameters, Parallel_Universe_Config.py:890-899,
+ * writes the reference's dictionaries filled by process_universe_mappings, :179-207). Universes uids[u]
+ * (ascending, < 2^31) hold the global ids ids[off[u] .. off[u + 1]) in local order (< 2^31). Each call writes the
+ * item region of a protocol-4 pickle stream (the part between MARK and SETITEMS that
+ * openke/config/_map_pickle.py wraps with the container header); with out == NULL only *n_out (bytes) is set.
+ * pt_pickle_id_maps: per universe the pair uid: defaultdict(int){ids[off[u] + i]: i} (memo 0 / 1 must hold
+ * collections.defaultdict / builtins.int). pt_pickle_universe_sets: per global id, in order of first
+ * appearance, the pair id: {universes holding it} (EMPTY_SET + ADDITEMS, universe order). */
+int pt_pickle_id_maps(int64_t n, const int64_t *uids, const int64_t *off, const int64_t *ids, uint8_t *out,
+                      int64_t cap, int64_t *n_out);
+int pt_pickle_universe_sets(int64_t n, const int64_t *uids, const int64_t *off, const int64_t *ids, uint8_t *out,
+                            int64_t cap, int64_t *n_out);
+
+/* Checkpoint archive (host only; the file torch.save writes, read back by torch.load - save_parameters,
+ * Parallel_Universe_Config.py:890-899): records[i] (name with the archive folder, e.g. "ckpt/data.pkl", data,
+ * size) stored in order, each record's data on an `alignment` boundary (a power of two; torch uses 64), ZIP64 where
+ * a size, offset or the count needs it (force_zip64: everywhere). CRC-32s of records with crc_known == 0 are
+ * computed on up to `threads` threads and written back (crc_known = 1), so an immutable record's CRC can be
+ * reused by a later archive. Runs without the Python GIL when called through ctypes. PT_EIO on a file error. */
+typedef struct {
+    const char *name;
+    const void *data;
+    int64_t size;
+    uint32_t crc32;
+    int32_t crc_known;
+} pt_zip_record;
+int pt_zip_write(const char *path, pt_zip_record *records, int64_t n, int32_t alignment, int32_t threads,
+                 int32_t force_zip64);
 
 /* The sampler of the Base.so-compatible global context below (its LCG states follow setRandomSeed /
  * randReset and its graph follows importTrainFiles / swapHelpers), so pt_trainer_* can train on exactly

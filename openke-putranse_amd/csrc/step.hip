@@ -345,6 +345,9 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
 // formed with the sign of its slot and stored to its counting-sort slot, and two accumulators collect
 // the positive's rows: At = sum over tail-corrupted negatives of dL/dv, Ah over head-corrupted ones
 // (dL/dh-hat = At + g+, dL/dr-hat = At + Ah + g+, dL/dt-hat = -(Ah + g+)).
+#ifndef PT_VK_NOCONTRACT
+#define PT_VK_NOCONTRACT 1
+#endif
 template <int G>
 __device__ __forceinline__ int32_t gbcast(int32_t v, int j) {
     if constexpr (G == 64) return __builtin_amdgcn_readlane(v, j); else return __shfl(v, j, G);
@@ -441,7 +444,9 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
                 Vec eh, vk, gs;
                 if (nf) vnormalize<true>(E[u], eh); else eh = E[u];
                 {
+#if PT_VK_NOCONTRACT
 #pragma clang fp contract(off)   // e-hat's product stays rounded: k_apply_buf's slot-scale mode re-forms v the same way
+#endif
                     if (tail_side) {
 #pragma unroll
                         for (int i = 0; i < Vec::N; ++i) vk.x[i] = bt.x[i] - eh.x[i];

@@ -56,6 +56,12 @@ class LpUniverse(ctypes.Structure):
                 ("dim", c_i64), ("d_ent_remap", c_vp)]
 
 
+class ZipRecord(ctypes.Structure):
+    """pt_zip_record: one stored record of a checkpoint archive."""
+    _fields_ = [("name", ctypes.c_char_p), ("data", c_vp), ("size", c_i64), ("crc32", ctypes.c_uint32),
+                ("crc_known", c_i32)]
+
+
 class LpPair(ctypes.Structure):
     _fields_ = [("key", c_i32), ("universe", c_i32), ("anchor", c_i32), ("rel", c_i32), ("side", c_i32)]
 
@@ -130,6 +136,10 @@ SIGNATURES = {
     "pt_rank_types": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp,
                                      c_vp, c_vp]),
     "pt_known_partners": (ctypes.c_int, [c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "pt_pickle_id_maps": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "pt_zip_write": (ctypes.c_int, [ctypes.c_char_p, c_vp, c_i64, c_i32, c_i32, c_i32]),
+    "pt_lp_pairs": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "pt_pickle_universe_sets": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "pt_known_create": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(c_vp)]),
     "pt_known_free": (ctypes.c_int, [c_vp]),
     "pt_rank_queries": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64]),

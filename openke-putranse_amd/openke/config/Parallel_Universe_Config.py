@@ -24,6 +24,7 @@ re-organised for the GPU:
   pt_lp_metrics.
 """
 import ctypes
+import gc
 import os
 import pickle
 import random
@@ -38,6 +39,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from . import _checkpoint, _map_pickle
 from ..data import TestDataLoader
 from ..module.loss import MarginLoss
 from ..module.model.Model import Model
@@ -156,46 +158,28 @@ def lp_pairs(slot, ent_remap, rel_remap, key_anchor, key_rel, key_side):
 
 
 def lp_pairs_all(ent_remaps, rel_remaps, key_anchor, key_rel, key_side):
-    """lp_pairs of every universe slot at once (vectorized over universes): the anchor entity's
-    occurrences across all universes (an inverted index by global id) joined with the keys, then the
-    relation membership tested by a sorted (universe, global relation) code. Returns int32 [n][5]
-    rows (key, slot, local anchor, local relation, side), grouped by key."""
-    key_anchor = np.asarray(key_anchor, dtype=np.int64)
-    key_rel = np.asarray(key_rel, dtype=np.int64)
-    key_side = np.asarray(key_side, dtype=np.int64)
+    """lp_pairs of every universe slot at once (pt_lp_pairs: an inverted index of the universes' entities by
+    global id joined with the keys, the relation looked up in each universe's sorted relations). Returns int32
+    [n][5] rows (key, slot, local anchor, local relation, side), ordered by key then slot."""
+    key_anchor = np.ascontiguousarray(key_anchor, dtype=np.int64)
+    key_rel = np.ascontiguousarray(key_rel, dtype=np.int64)
+    key_side = np.ascontiguousarray(key_side, dtype=np.int64)
     if not ent_remaps or len(key_anchor) == 0:
         return np.zeros((0, 5), dtype=np.int32)
-    ne = np.array([len(m) for m in ent_remaps], dtype=np.int64)
-    nr = np.array([len(m) for m in rel_remaps], dtype=np.int64)
-    eg = np.concatenate([np.asarray(m, dtype=np.int64) for m in ent_remaps])          # global entity
-    eu = np.repeat(np.arange(len(ent_remaps), dtype=np.int64), ne)                     # its universe slot
-    el = np.concatenate([np.arange(n, dtype=np.int64) for n in ne])                    # its local id
-    rg = np.concatenate([np.asarray(m, dtype=np.int64) for m in rel_remaps])
-    ru = np.repeat(np.arange(len(rel_remaps), dtype=np.int64), nr)
-    rl = np.concatenate([np.arange(n, dtype=np.int64) for n in nr])
-    o = np.argsort(eg, kind="stable")
-    eg, eu, el = eg[o], eu[o], el[o]
-    lo = np.searchsorted(eg, key_anchor, side="left")
-    hi = np.searchsorted(eg, key_anchor, side="right")
-    cnt = hi - lo
-    k = np.repeat(np.arange(len(key_anchor), dtype=np.int64), cnt)
-    pos = np.repeat(lo - np.cumsum(cnt) + cnt, cnt) + np.arange(int(cnt.sum()), dtype=np.int64)
-    u, la = eu[pos], el[pos]
-    rmax = int(max(rg.max() if len(rg) else 0, key_rel.max() if len(key_rel) else 0)) + 1
-    code = ru * rmax + rg
-    ro = np.argsort(code, kind="stable")
-    code, rlo = code[ro], rl[ro]
-    want = u * rmax + key_rel[k]
-    at = np.searchsorted(code, want)
-    at_c = np.minimum(at, max(len(code) - 1, 0))
-    ok = (at < len(code)) & (code[at_c] == want) if len(code) else np.zeros(len(want), bool)
-    out = np.empty((int(ok.sum()), 5), dtype=np.int32)
-    out[:, 0] = k[ok]
-    out[:, 1] = u[ok]
-    out[:, 2] = la[ok]
-    out[:, 3] = rlo[at_c[ok]]
-    out[:, 4] = key_side[k[ok]]
-    return out
+    L = _native.lib()
+    n = len(ent_remaps)
+    eoff, roff = np.zeros(n + 1, dtype=np.int64), np.zeros(n + 1, dtype=np.int64)
+    np.cumsum([len(m) for m in ent_remaps], out=eoff[1:])
+    np.cumsum([len(m) for m in rel_remaps], out=roff[1:])
+    eids = np.ascontiguousarray(np.concatenate(ent_remaps), dtype=np.int64)
+    rids = np.ascontiguousarray(np.concatenate(rel_remaps), dtype=np.int64)
+    cnt = np.zeros(1, dtype=np.int64)
+    args = (n, eoff.ctypes.data, eids.ctypes.data, roff.ctypes.data, rids.ctypes.data, len(key_anchor),
+            key_anchor.ctypes.data, key_rel.ctypes.data, key_side.ctypes.data)
+    _native.check(L.pt_lp_pairs(*args, None, 0, cnt.ctypes.data))
+    out = np.empty((int(cnt[0]), 5), dtype=np.int32)
+    _native.check(L.pt_lp_pairs(*args, out.ctypes.data, len(out), cnt.ctypes.data))
+    return out[:int(cnt[0])]
 
 
 def lp_pair_array(parts):
@@ -239,18 +223,46 @@ class _KeyStore(object):
         return None if idx is None else idx
 
 
-class _Pickled(object):
-    """A checkpoint container serialized with the plain C pickler when wrapped (a snapshot: later changes
-    to the container are not in it) and restored as the container itself on load. torch.save's pickler
-    calls its persistent-id hook once per object, ~1 s for C3's id maps alone (768k entries); the C
-    pickler takes 0.02-0.09 s. The file's layout is unchanged: torch.load returns the plain dicts."""
-    __slots__ = ("data",)
+class _TensorArray(object):
+    """Pickles as torch.Tensor.numpy(t) (an ndarray over the tensor's storage)."""
+    __slots__ = ("t",)
 
-    def __init__(self, obj):
-        self.data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+    def __init__(self, t):
+        self.t = t
 
     def __reduce__(self):
-        return (pickle.loads, (self.data,))
+        return (torch.Tensor.numpy, (self.t,))
+
+
+class _TensorBytes(object):
+    """Pickles as bytes(torch.Tensor.numpy(t)): the bytes of a uint8 tensor."""
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+    def __reduce__(self):
+        return (bytes, (_TensorArray(self.t),))
+
+
+class _Pickled(object):
+    """A checkpoint container serialized with the plain C pickler when wrapped (a snapshot: later changes
+    to the container are not in it), or given as a ready pickle stream (_map_pickle), and restored as the
+    container itself on load: pickle.loads(bytes(<uint8 tensor>.numpy())). torch.save's pickler calls its
+    persistent-id hook once per object, ~1 s for C3's id maps alone (768k entries), and writes a bytes object
+    through protocol 2's latin-1 text form (~14 ms per MB, 1.5x the size); the stream travels as a tensor
+    storage instead (one raw record of the archive). The file's layout is unchanged: torch.load returns the
+    plain dicts."""
+    __slots__ = ("data",)
+
+    def __init__(self, obj=None, stream=None):
+        if stream is None:
+            stream = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+        self.data = torch.frombuffer(bytearray(stream), dtype=torch.uint8) if len(stream) else \
+            torch.zeros(0, dtype=torch.uint8)
+
+    def __reduce__(self):
+        return (pickle.loads, (_TensorBytes(self.data),))
 
 
 def universe_dim(dim_param, uid):
@@ -267,14 +279,20 @@ def _id_map_property(name):
     """A reference attribute holding per-universe id maps (entity_id_mappings, ...): universes committed since
     the last read are registered first (_materialize_maps), in one batch."""
     def get(self):
+        # the caller may change the dictionaries: from now on checkpoints pickle them as they are
+        self.__dict__["_maps_exposed"] = True
         self._materialize_maps()
         return self.__dict__[name]
 
     def put(self, value):
         if name == "_entity_id_mappings":
             self.__dict__["_pending_maps"] = []   # a replaced state (load / best state) drops pending ones
+        self.__dict__["_map_log"] = None   # dictionaries not built from registered universes alone
         self.__dict__[name] = value
     return property(get, put)
+
+
+_MAP_KEYS = ('entity_id_mappings', 'relation_id_mappings', 'entity_universes', 'relation_universes')
 
 
 class Parallel_Universe_Config(Tester):
@@ -320,6 +338,11 @@ class Parallel_Universe_Config(Tester):
 
         self.entity_universes = defaultdict(set)  # entity_id -> universe_id
         self.relation_universes = defaultdict(set)  # relation_id -> universe_id
+        # (uid, ent_remap, rel_remap) of every universe registered since the dictionaries were created: while
+        # nothing else wrote them (no load / best state) and no caller read them, the checkpoint pickles them from
+        # these arrays (_map_pickle) instead of materialising and pickling the dictionaries
+        self._map_log = []
+        self._maps_exposed = False
 
         self.initial_random_seed = self.train_dataloader.lib.getRandomSeed()
 
@@ -613,12 +636,15 @@ class Parallel_Universe_Config(Tester):
         em = np.ascontiguousarray(ent_remap, dtype=np.int64)
         rm = np.ascontiguousarray(rel_remap, dtype=np.int64)
         self._pending_maps.append((uid, em, rm))
+        if self.__dict__.get("_map_log") is not None:
+            self._map_log.append((uid, em, rm))
         self._remap_cache[uid] = (em, rm)   # the sorted lookup helpers on first use (_remaps)
 
     def _materialize_maps(self):
         """Register the pending universes' maps in the reference's dictionaries, all at once: the per-universe
         maps built by dict.update (C loops), the id -> universes sets grouped by id over every pending universe
-        (one set update per id instead of one add per (id, universe))."""
+        (one set update per id instead of one add per (id, universe)); new ids enter in order of first
+        appearance, as process_universe_mappings (:179-207) adds them one universe after another."""
         pend = self.__dict__.get("_pending_maps")
         if not pend:
             return
@@ -635,11 +661,11 @@ class Parallel_Universe_Config(Tester):
             us = np.repeat(np.array([p[0] for p in pend], dtype=np.int64), [len(p[col]) for p in pend])
             o = np.argsort(ids, kind="stable")
             ids, us = ids[o], us[o]
-            keys, starts = np.unique(ids, return_index=True)
-            ends = np.append(starts[1:], len(ids)).tolist()
+            keys, starts, counts = np.unique(ids, return_index=True, return_counts=True)
+            first = np.argsort(o[starts], kind="stable")
             ul = us.tolist()
-            for k, lo, hi in zip(keys.tolist(), starts.tolist(), ends):
-                target[k].update(ul[lo:hi])
+            for k, lo, c in zip(keys[first].tolist(), starts[first].tolist(), counts[first].tolist()):
+                target[k].update(ul[lo:lo + c])
 
     def add_universe(self, embedding_space, ent_remap, rel_remap):
         """Register a trained universe as id next_universe_id: add_embedding_space +
@@ -757,6 +783,17 @@ class Parallel_Universe_Config(Tester):
         return False
 
     def train_parallel_universes(self, num_of_embedding_spaces):
+        # the cyclic collector paused for the call: a wave creates tens of thousands of objects (modules, id maps),
+        # enough to trigger full collections over everything the process holds in the middle of the loop
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            self._train_parallel_universes(num_of_embedding_spaces)
+        finally:
+            if gc_was:
+                gc.enable()
+
+    def _train_parallel_universes(self, num_of_embedding_spaces):
         self._check_setup()
         training_duration = 0.0
         if not self._batched():
@@ -807,6 +844,8 @@ class Parallel_Universe_Config(Tester):
         t0 = time.time()
         self.flush_checkpoint()
         timing["checkpoint_flush_s"] = time.time() - t0
+        w = self.__dict__.pop("_ckpt_write_s", [])
+        timing["checkpoint_writes"], timing["checkpoint_write_s"] = len(w), sum(w)
         print('Time took for creation of embedding spaces: {:5.3f}s'.format(training_duration), end='\n')
 
     def wave_size(self):
@@ -1300,13 +1339,17 @@ class Parallel_Universe_Config(Tester):
         return self
 
     def extend_state_dict(self):
+        return self._state_fields({k: getattr(self, k) for k in _MAP_KEYS})
+
+    def _state_fields(self, maps):
+        """extend_state_dict's layout (:890-899) with the four id-map entries taken from `maps`."""
         return {'initial_num_universes': self.initial_num_universes,
                 'next_universe_id': self.next_universe_id,
                 'trained_embedding_spaces': self.trained_embedding_spaces,
-                'entity_id_mappings': self.entity_id_mappings,
-                'relation_id_mappings': self.relation_id_mappings,
-                'entity_universes': self.entity_universes,
-                'relation_universes': self.relation_universes,
+                'entity_id_mappings': maps['entity_id_mappings'],
+                'relation_id_mappings': maps['relation_id_mappings'],
+                'entity_universes': maps['entity_universes'],
+                'relation_universes': maps['relation_universes'],
                 'min_margin': self.min_margin,
                 'max_margin': self.max_margin,
                 'min_lr': self.min_lr,
@@ -1407,12 +1450,22 @@ class Parallel_Universe_Config(Tester):
         return spaces
 
     def _checkpoint_state(self):
-        """extend_state_dict() as written: the id maps and occurrence sets pre-pickled (_Pickled), the
-        universe dict shallow-copied - a snapshot of this moment (trained universes are not modified later)."""
-        state = dict(self.extend_state_dict())
+        """extend_state_dict() as written: the id maps and occurrence sets pre-pickled (_Pickled) - straight
+        from the registered remap arrays while the dictionaries hold nothing else (_map_log, _map_pickle), else
+        from the dictionaries - and the universe dict shallow-copied: a snapshot of this moment (trained
+        universes are not modified later)."""
+        log = self.__dict__.get("_map_log")
+        if log is not None and not self.__dict__.get("_maps_exposed"):
+            uids = [x[0] for x in log]
+            ems, rms = [x[1] for x in log], [x[2] for x in log]
+            maps = {'entity_id_mappings': _Pickled(stream=_map_pickle.id_maps_stream(uids, ems)),
+                    'relation_id_mappings': _Pickled(stream=_map_pickle.id_maps_stream(uids, rms)),
+                    'entity_universes': _Pickled(stream=_map_pickle.universes_stream(uids, ems)),
+                    'relation_universes': _Pickled(stream=_map_pickle.universes_stream(uids, rms))}
+        else:
+            maps = {k: _Pickled(getattr(self, k)) for k in _MAP_KEYS}
+        state = dict(self._state_fields(maps))
         state['trained_embedding_spaces'] = copy(self.trained_embedding_spaces)
-        for k in ('entity_id_mappings', 'relation_id_mappings', 'entity_universes', 'relation_universes'):
-            state[k] = _Pickled(state[k])
         return state
 
     def save_parameters(self, path, background=False):
@@ -1420,20 +1473,27 @@ class Parallel_Universe_Config(Tester):
         every universe is gathered to rank 0, which alone writes; all ranks leave after the file exists.
         background=True (the training loop's best-model saves, one rank, static setting): the state is
         snapshotted here and the file written by a writer thread while training continues; the next save,
-        load_parameters and the end of train_parallel_universes wait for it (flush_checkpoint)."""
+        load_parameters and the end of train_parallel_universes wait for it (flush_checkpoint). One rank writes
+        through _checkpoint.UniverseArchive (the same file; each universe copied to the host and pickled once per
+        run, the archive written by the library without the GIL)."""
         world, rank = _dist()
         if not (world == 1 and background and self.training_setting == "static"):
             self.flush_checkpoint()
         if world == 1:
             state = self._checkpoint_state()
+            # universes already serialized by an earlier save are reused (_checkpoint.UniverseArchive)
+            archive = self.__dict__.get("_ckpt_archive")
+            if archive is None:
+                archive = self._ckpt_archive = _checkpoint.UniverseArchive()
             if not (background and self.training_setting == "static"):
-                torch.save(state, path)
+                _checkpoint.save(archive, state, path)
                 return
             prev = getattr(self, "_ckpt_writer", None)
             err = prev[1] if prev is not None else []
             seq = self._ckpt_seq = getattr(self, "_ckpt_seq", 0) + 1
             latest = self.__dict__.setdefault("_ckpt_latest", {})
             latest[path] = seq
+            writes = self.__dict__.setdefault("_ckpt_write_s", [])   # wall seconds of each background write
 
             def write():
                 # writes land in save order: a writer first waits for the one before it (off the training thread)
@@ -1449,8 +1509,10 @@ class Parallel_Universe_Config(Tester):
                 # previous checkpoint intact
                 tmp = "%s.tmp%d" % (path, os.getpid())
                 try:
-                    torch.save(state, tmp)
+                    t0 = time.perf_counter()
+                    _checkpoint.save(archive, state, tmp, final_path=path)
                     os.replace(tmp, path)
+                    writes.append(time.perf_counter() - t0)
                 except BaseException as e:   # re-raised by flush_checkpoint on the caller's thread
                     err.append(e)
                     try:

@@ -106,7 +106,8 @@ def test_lp_pairs_all_matches_per_universe():
     want = sorted(tuple(int(x) for x in row) for s in range(n_u)
                   for row in lp_pairs(s, ems[s], rms[s], key_anchor, key_rel, key_side))
     got = lp_pairs_all(ems, rms, key_anchor, key_rel, key_side)
-    assert sorted(tuple(int(x) for x in row) for row in got) == want
+    assert got.dtype == np.int32 and got.flags.c_contiguous
+    assert [tuple(int(x) for x in row) for row in got] == want   # by key, then universe slot
     assert len(want) > 0
     assert len(lp_pairs_all([], [], key_anchor, key_rel, key_side)) == 0
 

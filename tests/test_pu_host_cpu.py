@@ -126,3 +126,82 @@ def test_checkpoint_layout_and_background_write(tmp_path):
         sa, sw = a["trained_embedding_spaces"][u].state_dict(), cfg.trained_embedding_spaces[u].state_dict()
         for k in sw:
             assert torch.equal(sa[k], sw[k])
+
+
+def _same_container(a, b):
+    """Same type, default factory, key order, values (inner dicts: items in order; sets: members - a set's
+    iteration order is not kept by a pickle round trip, the reference's checkpoints included)."""
+    assert type(a) is type(b) and getattr(a, "default_factory", None) is getattr(b, "default_factory", None)
+    assert list(a.keys()) == list(b.keys())
+    for k in a:
+        x, y = a[k], b[k]
+        assert type(x) is type(y) and getattr(x, "default_factory", None) is getattr(y, "default_factory", None)
+        assert (list(x.items()) if isinstance(x, dict) else x) == (list(y.items()) if isinstance(y, dict) else y), k
+
+
+def test_checkpoint_maps_from_arrays_equal_dictionaries(tmp_path, monkeypatch):
+    """While nobody read or replaced the id dictionaries, a checkpoint pickles them straight from the registered
+    remap arrays (_map_pickle, pt_pickle_id_maps / pt_pickle_universe_sets) without building them; torch.load
+    gives back exactly the reference's registration (:179-207): types, default factories, key order and values.
+    Once a caller reads them the checkpoint pickles the dictionaries themselves, with the same result."""
+    from openke.config import _map_pickle
+    calls = []
+    for fn in ("id_maps_stream", "universes_stream"):
+        orig = getattr(_map_pickle, fn)
+        monkeypatch.setattr(_map_pickle, fn, lambda *a, _o=orig, _n=fn: calls.append(_n) or _o(*a))
+    rng = np.random.default_rng(21)
+    cfg = _config(checkpoint_dir=str(tmp_path) + "/")
+    from openke.config.Parallel_Universe_Config import defaultdict_int
+    want = {"entity_id_mappings": defaultdict(defaultdict_int), "relation_id_mappings": defaultdict(defaultdict_int),
+            "entity_universes": defaultdict(set), "relation_universes": defaultdict(set)}
+    for uid in range(40):
+        em = rng.choice(400, int(rng.integers(1, 150)), replace=False)
+        rm = rng.choice(9, int(rng.integers(1, 9)), replace=False)
+        for local, g in enumerate(em.tolist()):   # the reference's loop (:196-201)
+            want["entity_universes"][g].add(uid)
+            want["entity_id_mappings"][uid][g] = local
+        for local, g in enumerate(rm.tolist()):
+            want["relation_universes"][g].add(uid)
+            want["relation_id_mappings"][uid][g] = local
+        cfg._register_maps(uid, em, rm)
+        cfg.trained_embedding_spaces[uid] = TransE.seeded(uid, len(em), len(rm), dim=4, p_norm=1, norm_flag=True)
+    cfg.next_universe_id = 40
+    cfg.save_model("fast.ckpt")
+    assert sorted(calls) == ["id_maps_stream"] * 2 + ["universes_stream"] * 2
+    assert len(cfg.__dict__["_pending_maps"]) == 40   # nothing materialised
+    fast = torch.load(str(tmp_path / "fast.ckpt"), weights_only=False)
+    for k in want:
+        _same_container(fast[k], want[k])
+    # a read exposes the dictionaries: the next checkpoint pickles them (same result)
+    calls.clear()
+    _same_container(cfg.entity_universes, want["entity_universes"])
+    cfg.save_model("slow.ckpt")
+    assert calls == []
+    slow = torch.load(str(tmp_path / "slow.ckpt"), weights_only=False)
+    for k in want:
+        _same_container(slow[k], want[k])
+    # replaced dictionaries (best state / load) are never re-derived from the arrays
+    cfg2 = _config(checkpoint_dir=str(tmp_path) + "/")
+    cfg2.entity_id_mappings = defaultdict(defaultdict_int)
+    cfg2._register_maps(0, np.array([5, 6]), np.array([1]))
+    assert cfg2.__dict__["_map_log"] is None
+
+
+def test_pickle_map_streams_edge_cases():
+    """No universes, universes without ids, and ids outside int32 (refused)."""
+    import pickle
+    from openke.config import _map_pickle
+    from openke.config.Parallel_Universe_Config import defaultdict_int
+    e = pickle.loads(_map_pickle.id_maps_stream([], []))
+    assert e == {} and e.default_factory is defaultdict_int
+    e = pickle.loads(_map_pickle.universes_stream([], []))
+    assert e == {} and e.default_factory is set
+    z = np.zeros(0, dtype=np.int64)
+    m = pickle.loads(_map_pickle.id_maps_stream([3, 7], [z, np.array([9, 2])]))
+    assert list(m.keys()) == [3, 7] and dict(m[3]) == {} and list(m[7].items()) == [(9, 0), (2, 1)]
+    s = pickle.loads(_map_pickle.universes_stream([3, 7, 8], [np.array([4, 1]), z, np.array([1, 0])]))
+    assert list(s.items()) == [(4, {3}), (1, {3, 8}), (0, {8})]
+    with pytest.raises(Exception):
+        _map_pickle.id_maps_stream([0], [np.array([1 << 31])])
+    with pytest.raises(Exception):
+        _map_pickle.universes_stream([1, 0], [np.array([1]), np.array([2])])   # universes not ascending
