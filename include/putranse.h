@@ -114,6 +114,10 @@ int pt_trainer_run(pt_trainer *t, pt_sampler *sampler, int64_t bs, int64_t neg, 
  * sampler); parts = workgroups per call of the split sampler (0 = automatic, ceil(512 / calls)). Every path
  * draws the same batches (bit-exact); this selects only how. */
 int pt_trainer_set_sampling(pt_trainer *t, int32_t path, int64_t parts);
+/* Split-sampler chunks sampled in two launches (same batches, bit-exact): the first `head` steps ahead of the
+ * first step, the rest on the trainer's side stream alongside the first steps' training. head = 0 or -1 (the
+ * default): one launch (measured faster); a chunk of <= head steps is sampled in one launch. */
+int pt_trainer_set_sample_split(pt_trainer *t, int64_t head);
 /* Reference-order (deterministic) mode of a trainer: every later pt_trainer_step / pt_trainer_run sums each
  * table row's gradient in slot order, lookup by lookup (batch_h, batch_t, batch_r; norm_vector(batch_r)),
  * as torch's embedding_dense_backward + AccumulateGrad do for Trainer.train_one_step (Trainer.py:44-56),

@@ -82,6 +82,10 @@ struct pt_trainer {
     int64_t lpart_cap = 0;                             // W.lpart capacity (positives)
     int device = -1;
     hipStream_t cap = nullptr;
+    // the split sampler's second launch of a chunk (sample_split_head): its stream and the fork / join events
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int64_t split_override = -1;                        // pt_trainer_set_sample_split: head steps, 0 off, -1 auto
     std::map<GraphKey, hipGraphExec_t> graphs;
     int path_override = -1;                             // pt_trainer_set_sampling: PT_PATH_* or -1 (automatic)
     int64_t parts_override = 0;                         // split-sampler workgroups per call (0: automatic)
@@ -100,6 +104,9 @@ struct pt_trainer {
     ~pt_trainer() {
         drop_graphs();
         if (cap) (void)hipStreamDestroy(cap);
+        if (side) (void)hipStreamDestroy(side);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
 
         if (ws_block) (void)hipFree(ws_block);
         if (csr_block) (void)hipFree(csr_block);
@@ -285,6 +292,9 @@ extern "C" int pt_trainer_create(const pt_model_desc *m, pt_trainer **out) {
     t->W.frel = (int *)b; b += fr;
     t->W.fnorm = fn ? (int *)b : nullptr;
     PT_HIP(hipStreamCreateWithFlags(&t->cap, hipStreamNonBlocking));
+    PT_HIP(hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking));
+    PT_HIP(hipEventCreateWithFlags(&t->ev_fork, hipEventDisableTiming));
+    PT_HIP(hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming));
     *out = t.release();
     return PT_OK;
 }
@@ -514,6 +524,51 @@ static int enqueue_sample_chunk(pt_trainer *t, pt_sampler *s, pt::CsrWork &w, in
     return PT_OK;
 }
 
+// Steps of a split-sampler chunk sampled ahead of the first step (0: the chunk is sampled by one launch). The
+// batch stream does not depend on the tables, so the chunk's other steps can be sampled by a second launch on
+// the trainer's side stream while the first steps train: the chunk's first step then waits for `head` steps'
+// sampling instead of the whole chunk's (the driver's 20-step chunk: 52 us). Opt-in (pt_trainer_set_sample_split;
+// the tuning build's PT_SAMPLE_SPLIT): measured slower on the driver's command, 38.4 -> 39.6 us per step at
+// head 1, 2 or 4 - the side launch's workgroups take the CUs of the steps it runs beside (step 0: 22 -> 43 us)
+// and the join across hardware queues leaves the main queue idle for ~11 us (profiles/r05_c2_split_sampling.json).
+// Not under the measurement hook (its events time each launch alone) nor for the fused step + apply.
+static int64_t sample_split_head(const pt_trainer *t, int path, int64_t calls, const Timing *tm) {
+    if (path != PT_PATH_PART || tm) return 0;
+    int64_t h = t->split_override;
+    if (h < 0) {
+        h = 0;
+        if (const char *v = pt_tuning_env("PT_SAMPLE_SPLIT")) h = atoll(v);
+    }
+    return h > 0 && h < calls ? h : 0;
+}
+
+// A split-sampler chunk in two launches: the first `head` calls on `st`, the rest on the trainer's side stream
+// forked from `st` after it (neither launch advances the streams: join_sample_split does, after both).
+static int enqueue_sample_split(pt_trainer *t, pt_sampler *s, pt::CsrWork &w, int64_t bs, int64_t neg, int64_t bern,
+                                int64_t filter, int64_t calls, int64_t head, hipStream_t st) {
+    const pt::DeviceGraph dg = s->g->dev;
+    t->last_path = PT_PATH_PART;
+    w.rank_only = 1;
+    const int64_t parts = part_count(t, calls, bs);
+    pt::CsrWork w0 = w, w1 = pt::csr_view(w, head, bs, neg);
+    w0.prof = w1.prof = nullptr;
+    w1.tick = w.tick + head;
+    PT_HIP(pt::launch_sample_part(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, head, parts,
+                                  t->P.ent_total, w0, st, 0, 0));
+    PT_HIP(hipEventRecord(t->ev_fork, st));
+    PT_HIP(hipStreamWaitEvent(t->side, t->ev_fork, 0));
+    PT_HIP(pt::launch_sample_part(dg, s->d_states, s->threads, bs, neg, (int)bern, (int)filter, calls - head, parts,
+                                  t->P.ent_total, w1, t->side, head, 0));
+    PT_HIP(hipEventRecord(t->ev_join, t->side));
+    return PT_OK;
+}
+// `st` waits for the side launch of enqueue_sample_split, then the streams advance past the chunk's draws
+static int join_sample_split(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, int64_t calls, hipStream_t st) {
+    PT_HIP(hipStreamWaitEvent(st, t->ev_join, 0));
+    PT_HIP(pt::launch_advance(s->d_states, s->threads, bs, (1 + 2 * neg) * calls, st));
+    return PT_OK;
+}
+
 // whether in-kernel-sampled steps of P take the fused step + apply (carved for in ensure_csr)
 static bool step_apply_on(const pt_trainer *t, const pt::StepParams &P) {
     return step_apply_wanted(t) && t->fr.gent && t->csr.uses && pt::step_apply_supported(P, P.batch_size, P.neg);
@@ -540,8 +595,15 @@ static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, in
         if (!sa) w.uses = nullptr;   // (the sampler counts row uses only for the fused kernel)
         for (int64_t c0 = 0; c0 < steps; c0 += chunk) {
             const int64_t calls = std::min(chunk, steps - c0);
-            int rc = enqueue_sample_chunk(t, s, w, bs, neg, bern, filter, calls, sample_mode(t), st, tm);
-            if (rc) return rc;
+            const int path = choose_path(t, calls, bs, neg, sample_mode(t));
+            const int64_t head = sa ? 0 : sample_split_head(t, path, calls, tm);
+            if (head) {
+                int rc = enqueue_sample_split(t, s, w, bs, neg, bern, filter, calls, head, st);
+                if (rc) return rc;
+            } else {
+                int rc = enqueue_sample_chunk(t, s, w, bs, neg, bern, filter, calls, sample_mode(t), st, tm);
+                if (rc) return rc;
+            }
             t->csr.rank_only = w.rank_only;   // (read by pt_trainer_run_timed's re-timing of the last batch)
             if (sa) {   // one launch per step, then the chunk's losses
                 // arrival words back to zero every chunk (the last arriver of a row also clears its word): a step
@@ -555,6 +617,10 @@ static int enqueue_run(pt_trainer *t, pt_sampler *s, int64_t bs, int64_t neg, in
                 continue;
             }
             for (int64_t j = 0; j < calls; ++j) {
+                if (head && j == head) {   // the rest of the chunk sampled: join, then advance the streams
+                    int rc = join_sample_split(t, s, bs, neg, calls, st);
+                    if (rc) return rc;
+                }
                 const pt::CsrWork v = pt::csr_view(t->csr, j, bs, neg);
                 float *loss = d_losses ? d_losses + c0 + j : nullptr;
                 PT_TIMED(2, pt::launch_step(P, dg, s->d_states, s->threads, (int)bern, (int)filter, nullptr, nullptr,
@@ -680,6 +746,14 @@ extern "C" int pt_trainer_set_sampling(pt_trainer *t, int32_t path, int64_t part
     PT_CHECK(parts >= 0, PT_EINVAL, "parts must be >= 0");
     t->path_override = path;
     t->parts_override = parts;
+    t->drop_graphs();   // captured epochs hold the previous choice
+    return PT_OK;
+}
+
+extern "C" int pt_trainer_set_sample_split(pt_trainer *t, int64_t head) {
+    PT_CHECK(t, PT_EINVAL, "null trainer");
+    PT_CHECK(head >= -1, PT_EINVAL, "head must be >= -1");
+    t->split_override = head;
     t->drop_graphs();   // captured epochs hold the previous choice
     return PT_OK;
 }
@@ -887,7 +961,14 @@ extern "C" int pt_trainer_sample_csr(pt_trainer *t, pt_sampler *s, int64_t bs, i
         PT_CHECK(t->csr_part && pt::sample_part_fits(bs, neg, t->P.ent_total, part_count(t, calls, bs)), PT_ENOTSUP,
                  "split sampling plan does not fit LDS");
     hipStream_t st = (hipStream_t)stream;
-    rc = enqueue_sample_chunk(t, s, t->csr, bs, neg, bern, filter, calls, path, st, nullptr);
+    const int64_t head = path == PT_PATH_PART && t->split_override > 0 && t->split_override < calls ? t->split_override
+                                                                                                    : 0;
+    if (head) {   // the split pair (pt_trainer_set_sample_split), joined before the copies
+        rc = enqueue_sample_split(t, s, t->csr, bs, neg, bern, filter, calls, head, st);
+        if (!rc) rc = join_sample_split(t, s, bs, neg, calls, st);
+    } else {
+        rc = enqueue_sample_chunk(t, s, t->csr, bs, neg, bern, filter, calls, path, st, nullptr);
+    }
     if (rc) return rc;
     const pt::CsrWork &w = t->csr;
     const int64_t E = t->P.ent_total, slots = bs * neg;

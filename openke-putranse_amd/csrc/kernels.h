@@ -136,7 +136,7 @@ bool sample_part_fits(int64_t bs, int64_t neg, int64_t n, int64_t parts);
 bool sample_part_prepare(int64_t bs, int64_t neg, int64_t n, int64_t parts);
 hipError_t launch_sample_part(const DeviceGraph &g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                               int bern, int filter, int64_t calls, int64_t parts, int64_t n, const CsrWork &w,
-                              hipStream_t st);
+                              hipStream_t st, int64_t call0 = 0, int advance = 1);
 hipError_t launch_scan_counts(const CsrWork &w, int64_t n, int64_t calls, uint64_t *states, int64_t threads,
                               int64_t bs, int64_t dpp, hipStream_t st);
 bool step_fits(const StepParams &P, int64_t neg, bool csr);

@@ -340,10 +340,13 @@ __device__ __forceinline__ int32_t lds_bucket(const int32_t *cnt, int64_t e) {
 // both sides: every part's adds are seen, and the counts are clear for the next chunk) and scans them
 // into start[]; the last call's last part then advances the sampler streams. off[] keeps the ranks
 // (CsrWork::rank_only): the step kernel adds start[entity] when it loads a slot's record.
+// A launch may sample calls [call0, call0 + gridDim.x / parts) of a chunk (`w` viewed at call0: its per-call
+// arrays and tickets start there; the draws take their stream positions from call0 + call); advance = 0 leaves
+// the stream advance to a later launch (k_advance), so two launches can sample one chunk side by side.
 template <int NT, bool PACK, int SL>
 __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *states,
                                                     int64_t threads, int64_t bs, int64_t neg, int bern, int filter,
-                                                    int64_t parts, CsrWork w) {
+                                                    int64_t parts, CsrWork w, int64_t call0, int advance) {
     extern __shared__ __attribute__((aligned(16))) int32_t lds[];
     __shared__ int32_t wtot[NT / 64];
     __shared__ int32_t is_last;
@@ -362,7 +365,7 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
     jump_tab_fill<NT>(jt, neg, tid);
     const int64_t dpp = 1 + 2 * neg;
     for (int64_t b = b0 + tid; b < b1; b += NT) {
-        const PosDraw pd = draw_positive(g, states, threads, bs, b, dpp, call);
+        const PosDraw pd = draw_positive(g, states, threads, bs, b, dpp, call0 + call);
         int32_t *q = pi + 12 * (b - b0);
         q[0] = __float_as_int(bern ? g.bern_prob[pd.r] : 500.f);
         q[1] = pd.hr_lo; q[2] = pd.hr_hi; q[3] = pd.tr_lo; q[4] = pd.tr_hi;
@@ -514,6 +517,7 @@ __global__ __launch_bounds__(NT) void k_sample_part(DeviceGraph g, uint64_t *sta
 #undef PT_PHASE
     // the last call's last part advances the sampler streams past every call's draws: every part of every
     // call read them (positive draws) before its count atomics and tickets
+    if (!advance) return;
     __syncthreads();
     if (tid == 0) is_last = agent_add(&w.tick[gridDim.x / parts], 1) == (int32_t)(gridDim.x / parts - 1);
     __syncthreads();
@@ -1100,7 +1104,7 @@ bool sample_part_prepare(int64_t bs, int64_t neg, int64_t n, int64_t parts) {
 
 hipError_t launch_sample_part(const DeviceGraph &g, uint64_t *states, int64_t threads, int64_t bs, int64_t neg,
                               int bern, int filter, int64_t calls, int64_t parts, int64_t n, const CsrWork &w,
-                              hipStream_t st) {
+                              hipStream_t st, int64_t call0, int advance) {
     if (!sample_part_fits(bs, neg, n, parts) || n + 1 > w.start_stride || n > w.cnt_stride || !w.tick)
         return hipErrorInvalidValue;
     const size_t lds = sample_part_lds(bs, neg, n, parts);
@@ -1110,7 +1114,7 @@ hipError_t launch_sample_part(const DeviceGraph &g, uint64_t *states, int64_t th
 #define PT_PART(NT_, PK_, SL_)                                                                                 \
     if (part_nt() == NT_ && pk == PK_ && sl == SL_) {                                                        \
         hipLaunchKernelGGL((dev::k_sample_part<NT_, PK_, SL_>), grid, dim3(NT_), lds, st, g, states, threads, \
-                           bs, neg, bern, filter, parts, w);                                                  \
+                           bs, neg, bern, filter, parts, w, call0, advance);                                  \
         return hipGetLastError();                                                                            \
     }
     PT_PART(256, true, 2) PT_PART(256, true, 4) PT_PART(256, false, 2) PT_PART(256, false, 4)

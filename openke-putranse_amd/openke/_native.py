@@ -94,6 +94,7 @@ SIGNATURES = {
     "pt_trainer_last_path": (ctypes.c_int, [c_vp]),
     "pt_trainer_set_deterministic": (ctypes.c_int, [c_vp, c_i32]),
     "pt_trainer_set_sampling": (ctypes.c_int, [c_vp, c_i32, c_i64]),
+    "pt_trainer_set_sample_split": (ctypes.c_int, [c_vp, c_i64]),
     "pt_trainer_set_step_apply": (ctypes.c_int, [c_vp, c_i32]),
     "pt_universe_dim_supported": (ctypes.c_int, [c_i64, c_i32]),
     "pt_trainer_step_apply": (ctypes.c_int, [c_vp]),

@@ -149,3 +149,52 @@ def test_split_sampler_any_part_count(parts):
         _check_batches(ctx.sample(bs, neg, bern, filt, calls, PATHS["part"]), want, E, bs, neg)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("head", [1, 2, 7])
+@pytest.mark.parametrize("case", [(200, 13, 1, 1, 20, 17), (3000, 25, 1, 1, 6, 19), (200, 13, 0, 0, 9, 23)],
+                         ids=lambda c: "bs%d-neg%d-bern%d-filter%d-calls%d" % c[:5])
+def test_split_sampler_two_launches(case, head):
+    """A chunk sampled by two k_sample_part launches side by side (pt_trainer_set_sample_split: the first `head`
+    calls on the caller's stream, the rest on the trainer's side stream, the streams advanced after both):
+    the same batches as the oracle, and the streams end past exactly `calls` calls."""
+    bs, neg, bern, filt, calls, seed = case
+    want, E = _oracle_batches(seed, bs, neg, bern, filt, calls)
+    ctx = _Ctx(seed)
+    ctx.n.check(ctx.L.pt_trainer_set_sample_split(ctx.t, head))
+    try:
+        _check_batches(ctx.sample(bs, neg, bern, filt, calls, PATHS["part"]), want, E, bs, neg)
+        kg = oracle.KG.load(KG_SMALL)
+        st = oracle.GlibcRand(seed).rand_reset(THREADS)
+        for _ in range(calls):
+            kg.sample(st, THREADS, bs, neg, bern, filt)
+        nxt = ctx.sample(bs, neg, bern, filt, 1, PATHS["part"])
+        h, t, r, _ = kg.sample(st, THREADS, bs, neg, bern, filt)
+        np.testing.assert_array_equal(nxt[0][0][:, 0], h[:bs].astype(np.int32))
+        np.testing.assert_array_equal(nxt[0][0][:, 2], t[:bs].astype(np.int32))
+    finally:
+        ctx.close()
+
+
+def test_split_sampling_run_equals_single_launch():
+    """pt_trainer_run over a 20-step chunk (the driver's shape) with the chunk's sampling split in two launches
+    (opt-in) and in one: the same per-step losses and tables, up to the float-atomic order of the step."""
+    from openke import _native
+    L = _native.lib()
+    res = []
+    for head in (0, 2):
+        ctx = _Ctx(29, dim=24)
+        try:
+            g = torch.Generator().manual_seed(3)
+            ctx.ent.copy_(((torch.rand(ctx.ent.shape, generator=g) - 0.5) * 0.2).cuda())
+            ctx.rel.copy_(((torch.rand(ctx.rel.shape, generator=g) - 0.5) * 0.2).cuda())
+            _native.check(L.pt_trainer_set_sample_split(ctx.t, head))
+            losses = torch.zeros(20, device="cuda")
+            _native.check(L.pt_trainer_run(ctx.t, ctx.s, 100, 25, 1, 1, 20, _native.ptr(losses), _native.stream()))
+            torch.cuda.synchronize()
+            assert L.pt_trainer_last_path(ctx.t) == PATHS["part"]
+            res.append((losses.cpu(), ctx.ent.cpu(), ctx.rel.cpu()))
+        finally:
+            ctx.close()
+    for a, b in zip(res[0], res[1]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
