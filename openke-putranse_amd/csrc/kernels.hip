@@ -845,9 +845,19 @@ __device__ __forceinline__ float sum8(int D, F f) {
     return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
+// acc + |v| as one VOP3 add with the abs source modifier. (Left to itself the compiler packs the adds of two
+// partial sums into v_pk_add_f32, which has no abs modifier, and spends a v_and_b32 per term on |v|: 2 VALU
+// instructions per term instead of 1.5 with v_pk_fma_f32 + this.)
+__device__ __forceinline__ float add_abs(float acc, float v) {
+    float r;
+    asm("v_add_f32_e64 %0, %1, |%2|" : "=v"(r) : "v"(acc), "v"(v));
+    return r;
+}
+
 // NP sums of the sum8 form (the same partial sums and combination order for each) over one pass of d: the
-// caller's function f(q, d) for sum q reads shared operands (the LDS row) once for all of them
-template <int NP, typename F>
+// caller's function f(q, d) for sum q reads shared operands (the LDS row) once for all of them; ABS: the terms
+// are |f(q, d)|
+template <int NP, bool ABS = false, typename F>
 __device__ __forceinline__ void sum8xn(int D, F f, float (&r)[NP]) {
     float a[NP][8];
 #pragma unroll
@@ -855,28 +865,38 @@ __device__ __forceinline__ void sum8xn(int D, F f, float (&r)[NP]) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) a[q][k] = 0.f;
     int d = 0;
-    // (two 8-dim groups per iteration: the next group's operand loads issue before the current group's waits)
-#pragma unroll 2
-    for (; d + 8 <= D; d += 8) {
+    auto group = [&](int d0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k)
 #pragma unroll
-            for (int q = 0; q < NP; ++q) a[q][k] += f(q, d + k);
+            for (int q = 0; q < NP; ++q) a[q][k] = ABS ? add_abs(a[q][k], f(q, d0 + k)) : a[q][k] + f(q, d0 + k);
+    };
+    // (two 8-dim groups per iteration: the next group's operand loads issue before the current group's waits;
+    // unrolled by hand - the compiler does not unroll a loop holding the asm add of add_abs)
+    for (; d + 16 <= D; d += 16) {
+        group(d);
+        group(d + 8);
+    }
+    if (d + 8 <= D) {
+        group(d);
+        d += 8;
     }
     for (int k = 0; d + k < D; ++k)
 #pragma unroll
-        for (int q = 0; q < NP; ++q) a[q][k] += f(q, d + k);
+        for (int q = 0; q < NP; ++q) a[q][k] = ABS ? add_abs(a[q][k], f(q, d + k)) : a[q][k] + f(q, d + k);
 #pragma unroll
     for (int q = 0; q < NP; ++q)
         r[q] = ((a[q][0] + a[q][1]) + (a[q][2] + a[q][3])) + ((a[q][4] + a[q][5]) + (a[q][6] + a[q][7]));
 }
 
 #ifndef PT_LP_PAIRS
+#ifndef PT_LP_PAIRS
 #define PT_LP_PAIRS 2   // (measured r05, C4 k_lp_scan_t total: 1 pair 137.9 ms, 2 pairs 99.4, 4 pairs 105.3, 8 pairs 128.5)
 #endif
+#endif
 
-template <int MODEL>
-__global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
+template <int MODEL, int NW>
+__global__ __launch_bounds__(64 * NW) void k_lp_scan_t(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
                                                    const int64_t *__restrict__ uoff, const int32_t *__restrict__ uids,
                                                    int p_norm, int norm_flag, int64_t global_E, int64_t ds,
                                                    const float *__restrict__ base, const float *__restrict__ normal,
@@ -893,7 +913,7 @@ __global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restri
         const int ne = U.ent_total - e0 < 64 ? (int)(U.ent_total - e0) : 64;
         __syncthreads();   // (the previous tile's readers are done)
         const float *src = U.ent + e0 * D;
-        for (int i = (int)threadIdx.x; i < ne * D; i += 256) {
+        for (int i = (int)threadIdx.x; i < ne * D; i += 64 * NW) {
             const int r = i / D;
             s_x[r * S + (i - r * D)] = src[i];
         }
@@ -909,17 +929,17 @@ __global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restri
         int64_t pi = p0 + wave;
         if constexpr (MODEL == 0) {
             // TransE: the tile's rows normalized in place once (x * inv: the same rounded products the per-pair form
-            // computed), then the wave's pairs PT_LP_PAIRS at a time - pi, pi + 4, ... share every LDS read of the row. Each
-            // score keeps its expression and its sum8 order, so the scores are bit-identical to one pair at a time.
-            // (the four waves share the tile: every wave has read it for its norm, then wave 0 normalizes it while
-            // the others wait)
+            // computed), then the wave's pairs PT_LP_PAIRS at a time - pi, pi + NW, ... share every LDS read of the row.
+            // Each score keeps its expression and its sum8 order, so the scores are bit-identical to one pair at a time.
+            // (the NW waves share the tile: every wave has read it for its norm, then wave 0 normalizes it while the
+            // others wait)
             __syncthreads();
             if (wave == 0 && live && norm_flag) {
                 for (int d = 0; d < D; ++d) xr[d] = xr[d] * inv;
             }
             __syncthreads();
-            constexpr int NPP = PT_LP_PAIRS;   // pairs per pass: pi, pi + 4, ..., pi + 4 (NPP - 1)
-            for (; pi + 4 * (NPP - 1) < p1; pi += 4 * NPP) {
+            constexpr int NPP = PT_LP_PAIRS;   // pairs per pass: pi, pi + NW, ..., pi + NW (NPP - 1)
+            for (; pi + NW * (NPP - 1) < p1; pi += NW * NPP) {
                 LpPair pr[NPP];
                 const float *bq[NPP];
                 float sg[NPP], acc[NPP];
@@ -927,15 +947,15 @@ __global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restri
                 int old[NPP];
 #pragma unroll
                 for (int q = 0; q < NPP; ++q) {
-                    pr[q] = pairs[pi + 4 * q];
-                    bq[q] = base + (pi + 4 * q) * ds;
+                    pr[q] = pairs[pi + NW * q];
+                    bq[q] = base + (pi + NW * q) * ds;
                     sg[q] = pr[q].side == 0 ? 1.f : -1.f;
                     // the key-row cells this pass may lower, read before the sums (their latency hidden behind them)
                     cell[q] = reinterpret_cast<int *>(rows + (int64_t)pr[q].key * global_E + col);
                     old[q] = live ? __builtin_nontemporal_load(cell[q]) : 0;
                 }
                 if (p_norm == 1)
-                    sum8xn<NPP>(D, [&](int q, int d) { return fabsf(sg[q] * xr[d] + bq[q][d]); }, acc);
+                    sum8xn<NPP, true>(D, [&](int q, int d) { return sg[q] * xr[d] + bq[q][d]; }, acc);
                 else
                     sum8xn<NPP>(D,
                                 [&](int q, int d) {
@@ -954,7 +974,7 @@ __global__ __launch_bounds__(256) void k_lp_scan_t(const LpUniverseDev *__restri
             }
             inv = 1.f;   // (the row is normalized in LDS now)
         }
-        for (; pi < p1; pi += 4) {
+        for (; pi < p1; pi += NW) {
             const LpPair pr = pairs[pi];
             const float *b = base + pi * ds;
             const float sg = pr.side == 0 ? 1.f : -1.f;   // side 0: x-hat + b; side 1: b - x-hat
@@ -1177,6 +1197,16 @@ hipError_t launch_score_queries(const StepParams &P, int side, const int64_t *qh
 #ifndef PT_LP_SCAN_T
 #define PT_LP_SCAN_T 1
 #endif
+// k_lp_scan_t's waves per workgroup sharing one tile (PT_LP_WAVES = 4 | 8 | 16 in the tuning build; measured r05,
+// C4's nine launches: 4 waves 85.3 ms, 8 waves 77.1 ms, 16 waves 91.3 ms, profiles/r05_c4_lp_waves.json)
+static int lp_waves() {
+    static const int nw = [] {
+        const char *v = pt_tuning_env("PT_LP_WAVES");
+        const int x = v ? atoi(v) : 8;
+        return x == 4 || x == 16 ? x : 8;
+    }();
+    return nw;
+}
 hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, const int64_t *uoff,
                          const int32_t *uids, int64_t n_active, int64_t dim, int64_t max_ent, int model, int p_norm,
                          int norm_flag, int64_t global_E, int64_t ds, float *base, float *normal, float *rows,
@@ -1185,19 +1215,34 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
     const Shape s = pick_shape(dim);
     // the transposed scan's tile of 64 rows in LDS (row stride dim + 1)
     const size_t lds_t = sizeof(float) * 64 * (size_t)(dim + 1);
+    const int nw = lp_waves();
     if (PT_LP_SCAN_T && lds_t > (64 << 10) && lds_t <= (160 << 10)) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_lp_scan_t<0>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_t);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_lp_scan_t<1>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_t);
-        if (e != hipSuccess) return e;
+        const void *fn[6] = {reinterpret_cast<const void *>(dev::k_lp_scan_t<0, 4>),
+                             reinterpret_cast<const void *>(dev::k_lp_scan_t<1, 4>),
+                             reinterpret_cast<const void *>(dev::k_lp_scan_t<0, 8>),
+                             reinterpret_cast<const void *>(dev::k_lp_scan_t<1, 8>),
+                             reinterpret_cast<const void *>(dev::k_lp_scan_t<0, 16>),
+                             reinterpret_cast<const void *>(dev::k_lp_scan_t<1, 16>)};
+        const int k = nw == 4 ? 0 : nw == 8 ? 2 : 4;
+        for (int m = 0; m < 2; ++m) {
+            const hipError_t e = hipFuncSetAttribute(fn[k + m], hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_t);
+            if (e != hipSuccess) return e;
+        }
     }
     const int64_t gpb = 256 / s.G;
     const dim3 gb((unsigned)((n_pairs + gpb - 1) / gpb)), block(256);
     int64_t bx = (max_ent + gpb * 4 - 1) / (gpb * 4);
     if (bx > 32) bx = 32;
     if (bx < 1) bx = 1;
+#define PT_LPT(NW_)                                                                                                \
+    if (nw == NW_) {                                                                                               \
+        if (model == 0)                                                                                            \
+            hipLaunchKernelGGL((dev::k_lp_scan_t<0, NW_>), gt, bt, lds_t, st, us, pairs, uoff, uids + y0, p_norm,    \
+                               norm_flag, global_E, ds, base, normal, rows);                                       \
+        else                                                                                                       \
+            hipLaunchKernelGGL((dev::k_lp_scan_t<1, NW_>), gt, bt, lds_t, st, us, pairs, uoff, uids + y0, p_norm,    \
+                               norm_flag, global_E, ds, base, normal, rows);                                       \
+    }
 #define PT_LP(G_, V_, K_)                                                                                          \
     if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                                               \
         for (int64_t y0 = 0; y0 < n_active; y0 += 65535) {                                                         \
@@ -1211,13 +1256,8 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
                                        p_norm, norm_flag, ds, base, normal, tuple_min);                            \
             }                                                                                                      \
             if (PT_LP_SCAN_T && lds_t <= (160 << 10)) {                                                         \
-                const dim3 gt((unsigned)((max_ent + 63) / 64), gs.y);                                               \
-                if (model == 0)                                                                                    \
-                    hipLaunchKernelGGL((dev::k_lp_scan_t<0>), gt, block, lds_t, st, us, pairs, uoff, uids + y0,      \
-                                       p_norm, norm_flag, global_E, ds, base, normal, rows);                        \
-                else                                                                                               \
-                    hipLaunchKernelGGL((dev::k_lp_scan_t<1>), gt, block, lds_t, st, us, pairs, uoff, uids + y0,      \
-                                       p_norm, norm_flag, global_E, ds, base, normal, rows);                        \
+                const dim3 gt((unsigned)((max_ent + 63) / 64), gs.y), bt((unsigned)(64 * nw));                   \
+                PT_LPT(4) PT_LPT(8) PT_LPT(16)                                                                     \
             } else if (model == 0)                                                                                 \
                 hipLaunchKernelGGL((dev::k_lp_scan<0, G_, V_, K_>), gs, block, 0, st, us, pairs, uoff, uids + y0,   \
                                    p_norm, norm_flag, global_E, ds, base, normal, rows);                            \
@@ -1229,6 +1269,7 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
     }
     PT_SHAPES(PT_LP)
 #undef PT_LP
+#undef PT_LPT
     return hipErrorInvalidValue;
 }
 
