@@ -345,15 +345,14 @@ __global__ __launch_bounds__(256) void k_step_sampled(StepParams P, DeviceGraph 
 // formed with the sign of its slot and stored to its counting-sort slot, and two accumulators collect
 // the positive's rows: At = sum over tail-corrupted negatives of dL/dv, Ah over head-corrupted ones
 // (dL/dh-hat = At + g+, dL/dr-hat = At + Ah + g+, dL/dt-hat = -(Ah + g+)).
-#ifndef PT_VK_NOCONTRACT
-#define PT_VK_NOCONTRACT 1
-#endif
 template <int G>
 __device__ __forceinline__ int32_t gbcast(int32_t v, int j) {
     if constexpr (G == 64) return __builtin_amdgcn_readlane(v, j); else return __shfl(v, j, G);
 }
 
-template <int G, int VEC, int KCH, int NCH, int S, int PN, int NT = 256>
+// SC: the slot-scale mode (CsrWork::slot_scale) as its own instantiation - its branches inside the default
+// kernel had cost 1.5-2 us per C2 step (same-box A/B, tools_gpu/r05_ac.sh)
+template <int G, int VEC, int KCH, int NCH, int S, int PN, int NT = 256, bool SC = false>
 __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, CsrWork cw) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = NT / G;      // lane groups per block
@@ -426,7 +425,7 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
             vpos.x[i] = bt.x[i] - th.x[i];
         }
         ps = vpnorm<true>(vpos, p);
-        const bool scale_mode = cw.slot_scale != 0;
+        constexpr bool scale_mode = SC;
         if (scale_mode && sub == 0) {   // the positive's normalized rows, for the apply pass to re-form slot rows
             const auto base_rs = make_rsrc(cw.bases, (uint32_t)(P.batch_size * 3) * rowb);
             bstore(bt, base_rs, (uint32_t)(b * 3) * rowb, D, lane);
@@ -443,10 +442,16 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
                 const bool tail_side = r & 1;
                 Vec eh, vk, gs;
                 if (nf) vnormalize<true>(E[u], eh); else eh = E[u];
-                {
-#if PT_VK_NOCONTRACT
+                if constexpr (SC) {
 #pragma clang fp contract(off)   // e-hat's product stays rounded: k_apply_buf's slot-scale mode re-forms v the same way
-#endif
+                    if (tail_side) {
+#pragma unroll
+                        for (int i = 0; i < Vec::N; ++i) vk.x[i] = bt.x[i] - eh.x[i];
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < Vec::N; ++i) vk.x[i] = (eh.x[i] + rh.x[i]) - th.x[i];
+                    }
+                } else {
                     if (tail_side) {
 #pragma unroll
                         for (int i = 0; i < Vec::N; ++i) vk.x[i] = bt.x[i] - eh.x[i];
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(NT) void k_step_csr(StepParams P, GlobalSink sink, 
                 // slot gradient d loss / d e-hat: -g for a corrupted tail, +g for a corrupted head
                 // (g = dL/dv); an inactive pair stores zeros (the reserved slot must be defined)
                 vpnorm_bwd<true>(vk, ns, p, tail_side ? c : -c, gs);
-                if (scale_mode) {
+                if constexpr (scale_mode) {
                     // the slot's record: its positive and side, and vpnorm_bwd's scalar (p = 2: ds / ns as the
                     // fast form computes it, p = 1: ds) - the apply pass forms gs again from them
                     const float ds = tail_side ? c : -c;
@@ -681,7 +686,11 @@ hipError_t launch_step(const StepParams &P, const DeviceGraph &g, const uint64_t
         if (G == G_ && KCH == K_ && nch == N_ && S == S_) {                                          \
             constexpr int NT_ = S_ * G_ >= 256 || 256 % (S_ * G_) != 0 ? S_ * G_ : 256;             \
             const dim3 grid((unsigned)((P.batch_size * S_ * G_ + NT_ - 1) / NT_)), block(NT_);        \
-            if (P.p_norm == 1)                                                                       \
+            if (csr->slot_scale && P.p_norm == 1)                                                    \
+                hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 1, NT_, true>), grid, block, 0, st, P, sink, *csr); \
+            else if (csr->slot_scale)                                                                \
+                hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 2, NT_, true>), grid, block, 0, st, P, sink, *csr); \
+            else if (P.p_norm == 1)                                                                  \
                 hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 1, NT_>), grid, block, 0, st, P, sink, *csr); \
             else                                                                                     \
                 hipLaunchKernelGGL((dev::k_step_csr<G_, 4, K_, N_, S_, 2, NT_>), grid, block, 0, st, P, sink, *csr); \
