@@ -337,3 +337,39 @@ def test_bench_rejects_world_size_mismatch():
     p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--launch-check"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode != 0 and not p.stdout.strip().startswith("{")
+
+
+def test_lp_pairs_all_edges():
+    """The native pair join (pt_lp_pairs): universes without entities or relations, keys whose anchor or relation
+    no universe holds (ids beyond every universe's), and a key set of one; the rows are the per-universe
+    selection's, ordered by key then universe."""
+    em = [np.array([5, 2, 9]), np.zeros(0, np.int64), np.array([2, 40])]
+    rm = [np.array([1]), np.array([0, 1]), np.zeros(0, np.int64)]
+    ka, kr, ks = np.array([2, 9, 100, 2]), np.array([1, 1, 1, 0]), np.array([0, 1, 1, 0])
+    got = [tuple(int(x) for x in row) for row in lp_pairs_all(em, rm, ka, kr, ks)]
+    assert got == [(0, 0, 1, 0, 0), (1, 0, 2, 0, 1)]
+    assert [tuple(int(x) for x in r) for r in lp_pairs_all(em, rm, np.array([9]), np.array([1]), np.array([1]))] == \
+        [(0, 0, 2, 0, 1)]
+    assert lp_pairs_all(em, rm, np.zeros(0), np.zeros(0), np.zeros(0)).shape == (0, 5)
+
+
+def test_lp_pairs_native_rejects_bad_layouts():
+    import ctypes
+    from openke import _native
+    L = _native.lib()
+    off = np.array([0, 2], np.int64)
+    bad_off = np.array([1, 2], np.int64)       # offsets must start at 0
+    ids = np.array([3, -1], np.int64)          # ids must be >= 0
+    good = np.array([3, 4], np.int64)
+    k = np.array([3], np.int64)
+    n = np.zeros(1, np.int64)
+    call = lambda eo, ei: L.pt_lp_pairs(1, eo.ctypes.data, ei.ctypes.data, off.ctypes.data, good.ctypes.data, 1,
+                                        k.ctypes.data, k.ctypes.data, k.ctypes.data, None, 0, n.ctypes.data)
+    assert call(off, good) == 0 and n[0] == 1
+    assert call(bad_off, good) == 1
+    assert call(off, ids) == 1
+    out = np.zeros((1, 5), np.int32)
+    rel = np.array([3, 4], np.int64)
+    rc = L.pt_lp_pairs(1, off.ctypes.data, good.ctypes.data, off.ctypes.data, rel.ctypes.data, 1, k.ctypes.data,
+                       k.ctypes.data, k.ctypes.data, out.ctypes.data, 0, n.ctypes.data)   # no room for the row
+    assert rc == 1
