@@ -15,7 +15,9 @@ best-model save holds every universe trained so far) and a trained universe neve
   on several threads) with the GIL released, so a background write leaves the training thread running.
 
 A state this cannot express (a table that is not float32, tables on several devices, one module object under two
-universe ids) falls back to torch.save."""
+universe ids) falls back to torch.save, and so does a run whose host copies would pass the archive's budget
+(`max_host_bytes`: a quarter of the machine's memory, at most 16 GiB) - torch.save holds a checkpoint's copies only
+while it writes."""
 import ctypes
 import io
 import os
@@ -76,7 +78,14 @@ def _shadow(mod, fills):
 class UniverseArchive(object):
     """Per-config cache of the universes' fragments and host segments (see the module docstring)."""
 
-    def __init__(self):
+    def __init__(self, max_host_bytes=None):
+        if max_host_bytes is None:
+            try:
+                phys = os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES")
+            except (ValueError, OSError, AttributeError):
+                phys = 16 << 30
+            max_host_bytes = min(16 << 30, phys // 4)
+        self.max_host_bytes = int(max_host_bytes)
         self._frags = {}      # uid -> (module object, fragment bytes, segment key)
         self._segments = {}   # key -> [host uint8 tensor, crc32 or None]
         self._next_key = 0
@@ -128,6 +137,9 @@ class UniverseArchive(object):
             raise _Unsupported("tables on several devices")
         numel = [t.numel() for t in srcs]
         total = sum(numel)
+        held = sum(seg.numel() for seg, _ in self._segments.values())
+        if held + 4 * total > self.max_host_bytes:
+            raise _Unsupported("host copies over the archive's budget")
         dev = next(iter(devs)) if devs else torch.device("cpu")
         if dev.type == "cuda":
             if self._stream is None:

@@ -122,3 +122,16 @@ def test_zip_writer_rejects_bad_arguments(tmp_path):
     r[0].size = 0
     assert L.pt_zip_write(str(tmp_path / "z").encode(), r, 1, 48, 1, 0) == 1   # alignment not a power of two
     assert L.pt_zip_write(str(tmp_path / "no_dir" / "z").encode(), r, 1, 64, 1, 0) == 2   # PT_EIO
+
+
+def test_host_budget_falls_back_to_torch_save(tmp_path):
+    """A run whose host copies would pass the archive's budget is written by torch.save (same file contents)."""
+    rng = np.random.default_rng(6)
+    sp = _spaces(0, 6, rng)
+    ar = _checkpoint.UniverseArchive(max_host_bytes=64)
+    _checkpoint.save(ar, _state(sp), str(tmp_path / "a.ckpt"))
+    assert not ar._segments
+    torch.save(_state(sp), str(tmp_path / "a_ref.ckpt"))
+    _same(torch.load(str(tmp_path / "a.ckpt"), weights_only=False),
+          torch.load(str(tmp_path / "a_ref.ckpt"), weights_only=False))
+    assert _checkpoint.UniverseArchive().max_host_bytes <= 16 << 30
