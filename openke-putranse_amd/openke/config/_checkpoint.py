@@ -58,6 +58,15 @@ class _Unsupported(Exception):
     pass
 
 
+def _signature(mod):
+    """Where a universe's tables live (storage pointer, offset, shape, dtype, device of every parameter and buffer):
+    a table replaced since the universe was serialized (`weight.data = ...`, `.to(...)`) changes it. The archive
+    relies on the universes' tables not being rewritten in place after training (they are not, in the reference's
+    protocol: a universe is trained once and then only read)."""
+    return tuple((t.untyped_storage().data_ptr(), t.storage_offset(), tuple(t.shape), t.dtype, str(t.device))
+                 for t in list(mod.parameters()) + list(mod.buffers()))
+
+
 def _shadow(mod, fills):
     """A module object like `mod` (same class, attributes, submodules) whose parameters / buffers are filled in
     later with host copies; `fills` collects (owner dict, name, source tensor, is_parameter)."""
@@ -86,7 +95,7 @@ class UniverseArchive(object):
                 phys = 16 << 30
             max_host_bytes = min(16 << 30, phys // 4)
         self.max_host_bytes = int(max_host_bytes)
-        self._frags = {}      # uid -> (module object, fragment bytes, segment key)
+        self._frags = {}      # uid -> (module object, fragment bytes, segment key, table signature)
         self._segments = {}   # key -> [host uint8 tensor, crc32 or None]
         self._next_key = 0
         self._keys = {}       # storage _cdata -> key (segments and this write's other storages)
@@ -171,7 +180,7 @@ class UniverseArchive(object):
             else:
                 owner[name] = v
         for uid, m, sh, _ in shadows:
-            self._frags[uid] = (m, self._pickle(sh), key)
+            self._frags[uid] = (m, self._pickle(sh), key, _signature(m))
 
     # ------------------------------------------------------------------------------------- write --
     def _data_pkl(self, state):
@@ -197,7 +206,8 @@ class UniverseArchive(object):
         spaces = state.get("trained_embedding_spaces")
         if not isinstance(spaces, dict):
             raise _Unsupported("no universe dict")
-        new = [(u, m) for u, m in spaces.items() if u not in self._frags or self._frags[u][0] is not m]
+        new = [(u, m) for u, m in spaces.items()
+               if u not in self._frags or self._frags[u][0] is not m or self._frags[u][3] != _signature(m)]
         if len({id(m) for _, m in new}) != len(new) or any(not isinstance(m, nn.Module) for _, m in new):
             raise _Unsupported("universe objects")
         if new:
@@ -255,7 +265,7 @@ class UniverseArchive(object):
     def _prune(self, spaces):
         """Drop fragments of universes no longer held (a restored best state) and segments nothing uses."""
         for u in [u for u in self._frags if spaces.get(u) is not self._frags[u][0]]:
-            del self._frags[u]
+            del self._frags[u]   # (a re-serialized universe's entry was replaced by _add)
         live = {f[2] for f in self._frags.values()}
         for key in [k for k in self._segments if k not in live]:
             seg = self._segments.pop(key)[0]

@@ -135,3 +135,18 @@ def test_host_budget_falls_back_to_torch_save(tmp_path):
     _same(torch.load(str(tmp_path / "a.ckpt"), weights_only=False),
           torch.load(str(tmp_path / "a_ref.ckpt"), weights_only=False))
     assert _checkpoint.UniverseArchive().max_host_bytes <= 16 << 30
+
+
+def test_replaced_table_is_serialized_again(tmp_path):
+    """A universe whose table was replaced after an earlier checkpoint (`weight.data = ...`) is written with its
+    new table, not the cached one."""
+    rng = np.random.default_rng(8)
+    sp = _spaces(0, 4, rng)
+    ar = _checkpoint.UniverseArchive()
+    ar.write(str(tmp_path / "a.ckpt"), _state(sp))
+    w = sp[2].ent_embeddings.weight
+    w.data = w.data * 2.0 + 1.0
+    ar.write(str(tmp_path / "b.ckpt"), _state(sp))
+    got = torch.load(str(tmp_path / "b.ckpt"), weights_only=False)["trained_embedding_spaces"]
+    assert torch.equal(got[2].ent_embeddings.weight, sp[2].ent_embeddings.weight)
+    assert torch.equal(got[1].ent_embeddings.weight, sp[1].ent_embeddings.weight)
