@@ -8,7 +8,7 @@ best-model save holds every universe trained so far) and a trained universe neve
   the archive (one copy per segment, a storage of the archive shared by their tables), its module pickled once
   into a fragment of protocol-2 opcodes referring to that segment; a later checkpoint reuses the fragments and
   the segments (and the segments' CRC-32s) - only universes new since the last one are copied and pickled;
-- data.pkl is assembled from fragments: the state dict's items pickled one by one (each fragment with its own
+- data.pkl (pickle protocol 3) is assembled from fragments: the state dict's items pickled one by one (each fragment with its own
   memo, BINPUT before BINGET inside it) around the universes' fragments, with the tensors of the other entries
   (the pre-pickled id maps, _Pickled) as archive storages too;
 - the archive is written by the library (pt_zip_write: torch's record layout and 64-byte data alignment, CRC-32s
@@ -32,20 +32,24 @@ import torch.nn as nn
 from .. import _native
 
 _ALIGN = 64
-_PROTO2 = b"\x80\x02"
+# data.pkl's protocol: 3, not torch.save's default 2 - protocol 3 has BINBYTES (a bytes object, such as the
+# pre-pickled id maps, is copied as it is instead of through protocol 2's latin-1 text form) and, unlike 4, no
+# frames (the fragments are concatenated). torch.load reads any protocol.
+PICKLE_PROTOCOL = 3
+_PROTO = bytes([0x80, PICKLE_PROTOCOL])
 
 
 def _fragment_bytes(data):
-    """A protocol-2 pickle without its PROTO header and STOP: an opcode fragment that pushes one object."""
-    assert data[:2] == _PROTO2 and data[-1:] == b"."
+    """A protocol-3 pickle without its PROTO header and STOP: an opcode fragment that pushes one object."""
+    assert data[:2] == _PROTO and data[-1:] == b"."
     return data[2:-1]
 
 
 class _Pickler(pickle.Pickler):
-    """protocol 2 with torch.save's persistent ids for storages, the keys handed out by the archive."""
+    """torch.save's persistent ids for storages, the keys handed out by the archive."""
 
     def __init__(self, f, archive):
-        super().__init__(f, protocol=2)
+        super().__init__(f, protocol=PICKLE_PROTOCOL)
         self._archive = archive
 
     def persistent_id(self, obj):
@@ -184,7 +188,7 @@ class UniverseArchive(object):
 
     # ------------------------------------------------------------------------------------- write --
     def _data_pkl(self, state):
-        out = [_PROTO2, b"}("]
+        out = [_PROTO, b"}("]
         for k, v in state.items():
             out.append(self._pickle(k))
             if k == "trained_embedding_spaces":
@@ -277,4 +281,4 @@ def save(archive, state, path, threads=8, final_path=None):
     try:
         archive.write(path, state, threads, final_path)
     except _Unsupported:
-        torch.save(state, path)
+        torch.save(state, path, pickle_protocol=PICKLE_PROTOCOL)
