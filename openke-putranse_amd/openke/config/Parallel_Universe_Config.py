@@ -223,21 +223,46 @@ class _KeyStore(object):
         return None if idx is None else idx
 
 
+class _ArrayOf(object):
+    """Pickles as numpy.asarray(t): the ndarray over a CPU tensor's memory."""
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+    def __reduce__(self):
+        return (np.asarray, (self.t,))
+
+
+class _BytesOf(object):
+    """Pickles as bytes(numpy.asarray(t)): the bytes of a uint8 tensor."""
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+    def __reduce__(self):
+        return (bytes, (_ArrayOf(self.t),))
+
+
 class _Pickled(object):
     """A checkpoint container serialized with the plain C pickler when wrapped (a snapshot: later changes
     to the container are not in it), or given as a ready pickle stream (_map_pickle), and restored as the
-    container itself on load: pickle.loads(<bytes>). torch.save's pickler calls its persistent-id hook once per
-    object, ~1 s for C3's id maps alone (768k entries); the stream is one bytes object instead. Checkpoints holding
-    these are written with pickle protocol 3 (_checkpoint.PICKLE_PROTOCOL), whose BINBYTES opcode copies a bytes
-    object as it is - protocol 2, torch.save's default, writes it through a latin-1 text form (~14 ms per MB, 1.5x
-    the size). The file's layout is unchanged: torch.load returns the plain dicts."""
+    container itself on load: pickle.loads(bytes(numpy.asarray(<uint8 tensor>))). torch.save's pickler calls its
+    persistent-id hook once per object, ~1 s for C3's id maps alone (768k entries), and writes a bytes object
+    through protocol 2's latin-1 text form (~14 ms per MB, 1.5x the size); the stream travels as a tensor storage
+    instead (one raw record of the archive), rebuilt with torch's own tensor reconstruction and numpy / builtin
+    callables only. The file's layout is unchanged: torch.load returns the plain dicts."""
     __slots__ = ("data",)
 
     def __init__(self, obj=None, stream=None):
-        self.data = bytes(stream) if stream is not None else pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+        if stream is None:
+            stream = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+        self.data = torch.frombuffer(bytearray(stream), dtype=torch.uint8) if len(stream) else \
+            torch.zeros(0, dtype=torch.uint8)
 
     def __reduce__(self):
-        return (pickle.loads, (self.data,))
+        return (pickle.loads, (_BytesOf(self.data),))
 
 
 def universe_dim(dim_param, uid):
