@@ -32,9 +32,9 @@ import torch.nn as nn
 from .. import _native
 
 _ALIGN = 64
-# data.pkl's protocol: 3, not torch.save's default 2 - protocol 3 has BINBYTES (a bytes object, such as the
-# pre-pickled id maps, is copied as it is instead of through protocol 2's latin-1 text form) and, unlike 4, no
-# frames (the fragments are concatenated). torch.load reads any protocol.
+# data.pkl's protocol: 3, not torch.save's default 2 - protocol 3 has BINBYTES (a bytes object in the state is
+# copied as it is instead of through protocol 2's latin-1 text form) and, unlike 4, no frames (the fragments are
+# concatenated). torch.load reads any protocol.
 PICKLE_PROTOCOL = 3
 _PROTO = bytes([0x80, PICKLE_PROTOCOL])
 
