@@ -205,3 +205,22 @@ def test_pickle_map_streams_edge_cases():
         _map_pickle.id_maps_stream([0], [np.array([1 << 31])])
     with pytest.raises(Exception):
         _map_pickle.universes_stream([1, 0], [np.array([1]), np.array([2])])   # universes not ascending
+
+
+def test_pickle_map_entry_points_reject_bad_layouts():
+    """pt_pickle_id_maps / pt_pickle_universe_sets: offsets not starting at 0, decreasing offsets, universes not
+    ascending, negative ids and a too-small buffer are refused (PT_EINVAL); the size query matches the stream."""
+    L = _native.lib()
+    uids = np.array([0, 3], np.int64)
+    off = np.array([0, 2, 3], np.int64)
+    ids = np.array([5, 1, 7], np.int64)
+    n = np.zeros(1, np.int64)
+    for fn in (L.pt_pickle_id_maps, L.pt_pickle_universe_sets):
+        assert fn(2, uids.ctypes.data, off.ctypes.data, ids.ctypes.data, None, 0, n.ctypes.data) == 0 and n[0] > 0
+        out = np.zeros(int(n[0]), np.uint8)
+        assert fn(2, uids.ctypes.data, off.ctypes.data, ids.ctypes.data, out.ctypes.data, len(out), n.ctypes.data) == 0
+        assert fn(2, uids.ctypes.data, off.ctypes.data, ids.ctypes.data, out.ctypes.data, len(out) - 1,
+                  n.ctypes.data) == 1
+        for bad_u, bad_o, bad_i in ((uids, np.array([1, 2, 3], np.int64), ids), (uids, np.array([0, 2, 1], np.int64), ids),
+                                    (np.array([3, 0], np.int64), off, ids), (uids, off, np.array([5, -1, 7], np.int64))):
+            assert fn(2, bad_u.ctypes.data, bad_o.ctypes.data, bad_i.ctypes.data, None, 0, n.ctypes.data) == 1
