@@ -24,7 +24,7 @@ import os
 import pickle
 import random
 import sys
-from collections import OrderedDict, defaultdict
+from collections import defaultdict
 
 import torch
 import torch.nn as nn
