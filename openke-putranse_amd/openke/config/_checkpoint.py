@@ -63,12 +63,16 @@ class _Unsupported(Exception):
 
 
 def _signature(mod):
-    """Where a universe's tables live (storage pointer, offset, shape, dtype, device of every parameter and buffer):
-    a table replaced since the universe was serialized (`weight.data = ...`, `.to(...)`) changes it. The archive
-    relies on the universes' tables not being rewritten in place after training (they are not, in the reference's
-    protocol: a universe is trained once and then only read)."""
-    return tuple((t.untyped_storage().data_ptr(), t.storage_offset(), tuple(t.shape), t.dtype, str(t.device))
-                 for t in list(mod.parameters()) + list(mod.buffers()))
+    """What a universe's cached fragment depends on: every parameter's and buffer's storage pointer, offset, shape,
+    dtype, device and version counter, each parameter's requires_grad, and every submodule's training flag. A table
+    replaced since the universe was serialized (`weight.data = ...`, `.to(...)`) or rewritten in place through
+    autograd-visible ops (`add_` / `copy_` under no_grad, an optimizer step, load_state_dict) changes it. Writes
+    through `.data` are invisible here as they are to autograd (torch gives `.data` its own version counter);
+    `UniverseArchive.forget` drops a universe's fragment for callers that write that way."""
+    mods = list(mod.modules())
+    return (tuple((t.untyped_storage().data_ptr(), t.storage_offset(), tuple(t.shape), t.dtype, str(t.device),
+                   t._version, bool(t.requires_grad)) for t in list(mod.parameters()) + list(mod.buffers())),
+            tuple(m.training for m in mods))
 
 
 def _shadow(mod, fills):
@@ -183,8 +187,26 @@ class UniverseArchive(object):
                 owner[name] = p
             else:
                 owner[name] = v
-        for uid, m, sh, _ in shadows:
-            self._frags[uid] = (m, self._pickle(sh), key, _signature(m))
+        before = set(self._storages)
+        try:
+            for uid, m, sh, _ in shadows:
+                self._frags[uid] = (m, self._pickle(sh), key, _signature(m))
+        finally:
+            extra = [k for k in self._storages if k not in before]
+            for k in extra:   # a storage outside the segment: write() would not hold it for the fragment
+                self._keys.pop(self._storages.pop(k)._cdata, None)
+        if extra:
+            for uid, _, _, _ in shadows:
+                self._frags.pop(uid, None)
+            self._keys.pop(self._segments.pop(key)[0].untyped_storage()._cdata, None)
+            raise _Unsupported("a universe module holds a tensor that is not a parameter or buffer")
+
+    def forget(self, uid=None):
+        """Drop the cached fragment of universe `uid` (all universes: None); its next save serializes it again."""
+        if uid is None:
+            self._frags.clear()
+        else:
+            self._frags.pop(uid, None)
 
     # ------------------------------------------------------------------------------------- write --
     def _data_pkl(self, state):

@@ -402,12 +402,183 @@ def case_tc(out, name, model, dim, p, tseed):
                         **tables)
 
 
+# ------------------------------------------------------------------------------------------------------------------
+# Real scale (round 6): the reference's own benchmark data and trained tables (SURVEY §8c fixture recipe).
+# The folders are packed into tests/golden/real_<name>.npz (realdata.pack_dataset) and the reference is run on the
+# folder realdata.write_dataset rebuilds from them, i.e. on exactly what the tests read.
+#   wn18:  benchmarks/WN18 as it is (train / valid / test, type_constrain.txt), E = 40,943, R = 18.
+#   fb15k: benchmarks/FB15K has no train2id.txt (.MISSING_LARGE_BLOBS:1), so the folder takes its valid split
+#          (50,000 triples) as train2id.txt, test2id.txt lines 300-599 as valid2id.txt and lines 0-299 as
+#          test2id.txt; E = 14,951, R = 1,345.
+# Checkpoints are read with torch.load(weights_only=True) only.
+REAL_DATA = {"wn18": os.path.join(HERE, "real_wn18.npz"), "fb15k": os.path.join(HERE, "real_fb15k.npz")}
+
+REAL_LP_CASES = [
+    # name, dataset, checkpoint (best_models/), model, p_norm, type_constrain, queries whose score vectors are kept
+    ("wn18h", "wn18", "transH_WN18_optimal_model.ckpt", "TransH", 1, True, [0]),
+    ("fb15ke", "fb15k", "transe_FB15K_optimal_model.ckpt", "TransE", 2, False, [0, 150]),
+]
+
+REAL_SAMPLER_CASES = [
+    # name, batch_size, neg_ent, bern, filter, seed, calls (WN18, 8 threads); C1's bs 1414 and 100, and C2's
+    # bs 2000 x 25 negatives on WN18's graph
+    ("w1", 1414, 1, 0, 0, 4, 6),
+    ("w2", 1414, 1, 1, 1, 4, 6),
+    ("w3", 100, 1, 0, 1, 7, 6),
+    ("w4", 100, 1, 1, 0, 7, 6),
+    ("w5", 2000, 25, 1, 1, 4, 4),
+]
+
+
+def _sha1(*arrays):
+    import hashlib
+    m = hashlib.sha1()
+    for a in arrays:
+        m.update(np.ascontiguousarray(a, dtype=np.int64).tobytes())
+    return m.hexdigest()
+
+
+def _real_dir(tmp, name):
+    sys.path.insert(0, os.path.dirname(HERE))
+    import realdata
+    return realdata.write_dataset(REAL_DATA[name], os.path.join(tmp, "real_" + name))
+
+
+def case_real_lp(out, name, ds, ckpt, model, p, tc, vec_queries):
+    """Tester.run_link_prediction (Tester.py:70-93) on a reference-trained table over the full entity set, plus
+    every query's raw / filtered (and type-constrained) counts as testHead / testTail compute them
+    (Test.h:118-359): the loop of run_link_prediction, with the accumulators zeroed before each query and read
+    after it (they are exact integers there)."""
+    import torch
+    from openke.config import Tester
+    from openke.data import TestDataLoader
+    from openke.module.model import TransE, TransH
+    path = _real_dir(TMP, ds)
+    test_dl = TestDataLoader(path, "link")
+    if tc:
+        test_dl.lib.importTypeFiles()   # the reference's Python never calls it (DESIGN.md §7)
+    sd = torch.load(os.path.join(REF, "best_models", ckpt), weights_only=True, map_location="cpu")
+    dim = sd["ent_embeddings.weight"].shape[1]
+    cls = TransE if model == "TransE" else TransH
+    kge = cls(ent_tot=test_dl.get_ent_tot(), rel_tot=test_dl.get_rel_tot(), dim=dim, p_norm=p, norm_flag=True)
+    kge.load_state_dict(sd)
+    tables = {k.split(".")[0]: v.detach().numpy().copy() for k, v in kge.state_dict().items()
+              if "embeddings" in k or "norm_vector" in k}
+    tester = Tester(model=kge, data_loader=test_dl, use_gpu=False)
+    res = tester.run_link_prediction(type_constrain=bool(tc))
+    lib = tester.lib
+    plain = [lib.getTestLinkMRR(0), lib.getTestLinkMR(0), lib.getTestLinkHit10(0), lib.getTestLinkHit3(0),
+             lib.getTestLinkHit1(0)]
+    names = ["l_rank", "l_filter_rank", "r_rank", "r_filter_rank"]
+    if tc:
+        names += [n + "_constrain" for n in names]
+    acc = [ctypes.c_float.in_dll(lib, n) for n in names]
+    test_dl.set_sampling_mode("link")
+    n = lib.getTestTotal()
+    ranks = np.zeros((len(names), n), dtype=np.int32)
+    queries = np.zeros((n, 3), dtype=np.int32)
+    vecs_h, vecs_t = [], []
+    for index, (dh, dt) in enumerate(test_dl):
+        for a in acc:
+            a.value = 0.0
+        sh = tester.test_one_step(dh)
+        lib.testHead(sh.__array_interface__["data"][0], index, int(tc))
+        st = tester.test_one_step(dt)
+        lib.testTail(st.__array_interface__["data"][0], index, int(tc))
+        ranks[:, index] = [int(a.value) - 1 for a in acc]   # accumulated 1 + count
+        queries[index] = (dh["batch_h"][0], dh["batch_t"][0], dh["batch_r"][0])
+        if index in vec_queries:
+            vecs_h.append(np.asarray(sh, dtype=np.float32).copy())
+            vecs_t.append(np.asarray(st, dtype=np.float32).copy())
+    np.savez_compressed(out, dataset=ds, checkpoint=ckpt, model=model, dim=dim, p_norm=p, type_constrain=int(tc),
+                        metrics=np.array(plain, dtype=np.float64),
+                        metrics_tc=np.array(res if tc else plain, dtype=np.float64),
+                        rank_names=np.array(names), ranks=ranks, queries=queries,
+                        vec_queries=np.array(vec_queries, dtype=np.int64), vec_head=np.stack(vecs_h),
+                        vec_tail=np.stack(vecs_t), **tables)
+
+
+def case_real_sampler(out, bs, neg, bern, filt, seed, calls):
+    """sampling() (Base.cpp:266-310) on WN18: SHA-1 of each call's (h, t, r) int64 arrays, the first call kept."""
+    from openke.data import TrainDataLoader
+    path = _real_dir(TMP, "wn18")
+    dl = TrainDataLoader(in_path=path, batch_size=bs, threads=8, sampling_mode="normal", bern_flag=bern,
+                         filter_flag=filt, neg_ent=neg, neg_rel=0, random_seed=seed)
+    digests, first = [], None
+    for c in range(calls):
+        d = dl.sampling()
+        digests.append(_sha1(d["batch_h"], d["batch_t"], d["batch_r"]))
+        if c == 0:
+            first = np.stack([d["batch_h"], d["batch_t"], d["batch_r"]]).astype(np.int32)
+    np.savez_compressed(out, batch_size=bs, neg_ent=neg, bern=bern, filter=filt, seed=seed, calls=calls,
+                        digests=np.array(digests), first=first)
+
+
+def case_real_universes(out, seeds, tc_range, bal_range):
+    """The per-universe protocol on WN18 (Parallel_Universe_Config.py:157-161, 209-226; UniverseConstructor.h:
+    327-397): set_random_seed(s), randrange(tc), uniform(balance), getParallelUniverse; remaps, universe sizes,
+    then swapHelpers and two sampling() calls of the universe (nbatches 20) as SHA-1 digests."""
+    import random
+    from openke.data import TrainDataLoader
+    path = _real_dir(TMP, "wn18")
+    dl = TrainDataLoader(in_path=path, nbatches=20, threads=8, sampling_mode="normal", bern_flag=0, filter_flag=0,
+                         neg_ent=1, neg_rel=0, random_seed=4)
+    rec = {"seeds": np.array(seeds, dtype=np.int64)}
+    for s in seeds:
+        dl.lib.setRandomSeed(s)
+        dl.lib.randReset()
+        random.seed(s)
+        tc = random.randrange(*tc_range)
+        bal = round(random.uniform(*bal_range), 2)
+        dl.compile_universe_dataset(tc, bal)
+        em, rm = dl.get_universe_mappings()
+        rec["s%d_tc" % s], rec["s%d_balance" % s] = tc, bal
+        rec["s%d_train_total" % s] = dl.lib.getTrainTotalUniverse()
+        rec["s%d_batch_size" % s] = dl.batch_size
+        rec["s%d_ent_remap" % s] = em.astype(np.int32)
+        rec["s%d_rel_remap" % s] = rm.astype(np.int32)
+        dl.swap_helpers()
+        digests = []
+        for _ in range(2):   # (sampling() returns the same buffers each call: hash each batch before the next)
+            d = dl.sampling()
+            digests.append(_sha1(d["batch_h"], d["batch_t"], d["batch_r"]))
+        rec["s%d_digests" % s] = np.array(digests)
+        dl.reset_universe()
+    np.savez_compressed(out, tc_range=np.array(tc_range), bal_range=np.array(bal_range), **rec)
+
+
+def pack_real_data():
+    sys.path.insert(0, os.path.dirname(HERE))
+    import realdata
+    bench = os.path.join(REF, "benchmarks")
+    if not os.path.exists(REAL_DATA["wn18"]):
+        src = os.path.join(bench, "WN18")
+        realdata.pack_dataset(REAL_DATA["wn18"], 40943, 18,
+                              {f: realdata.read_triples(os.path.join(src, f)) for f in realdata.SPLITS},
+                              type_file=os.path.join(src, "type_constrain.txt"),
+                              source="benchmarks/WN18/{train,valid,test}2id.txt, type_constrain.txt")
+    if not os.path.exists(REAL_DATA["fb15k"]):
+        src = os.path.join(bench, "FB15K")
+        test = realdata.read_triples(os.path.join(src, "test2id.txt"))
+        realdata.pack_dataset(REAL_DATA["fb15k"], 14951, 1345,
+                              {"train2id.txt": realdata.read_triples(os.path.join(src, "valid2id.txt")),
+                               "valid2id.txt": test[300:600], "test2id.txt": test[:300]},
+                              source="benchmarks/FB15K: train2id := valid2id.txt (train2id.txt is not in the "
+                                     "reference), valid2id := test2id.txt[300:600], test2id := test2id.txt[:300]")
+
+
+TMP = None
+
+
 def run_case(kind, args_json, out, tmp):
+    global TMP
+    TMP = tmp
     args = json.loads(args_json)
     _import_reference(tmp)
     _silence()
     {"glibc": case_glibc, "sampler": case_sampler, "sampler_mode": case_sampler_mode, "train": case_train, "universes": case_universes,
-     "lp": case_lp, "lpt": case_lpt, "val": case_val, "nbr": case_nbr, "tc": case_tc}[kind](out, *args)
+     "lp": case_lp, "lpt": case_lpt, "val": case_val, "nbr": case_nbr, "tc": case_tc, "real_lp": case_real_lp,
+     "real_sampler": case_real_sampler, "real_universes": case_real_universes}[kind](out, *args)
 
 
 def main():
@@ -428,6 +599,10 @@ def main():
     jobs += [("val", list(c), "val_%s.npz" % c[0]) for c in VAL_CASES]
     jobs += [("nbr", list(c), "nbr_%s.npz" % c[0]) for c in NBR_CASES]
     jobs += [("tc", list(c), "tc_%s.npz" % c[0]) for c in TC_CASES]
+    pack_real_data()
+    jobs += [("real_lp", list(c), "reallp_%s.npz" % c[0]) for c in REAL_LP_CASES]
+    jobs += [("real_sampler", list(c[1:]), "realsampler_%s.npz" % c[0]) for c in REAL_SAMPLER_CASES]
+    jobs += [("real_universes", [list(range(4, 12)), [500, 2000], [0.25, 0.5]], "realuniverses_wn18.npz")]
     only = sys.argv[1:]
     for kind, args, fname in jobs:
         if only and not any(fname.startswith(o) for o in only):

@@ -150,3 +150,40 @@ def test_replaced_table_is_serialized_again(tmp_path):
     got = torch.load(str(tmp_path / "b.ckpt"), weights_only=False)["trained_embedding_spaces"]
     assert torch.equal(got[2].ent_embeddings.weight, sp[2].ent_embeddings.weight)
     assert torch.equal(got[1].ent_embeddings.weight, sp[1].ent_embeddings.weight)
+
+
+def test_in_place_write_is_serialized_again(tmp_path):
+    """In-place writes to a trained universe after a checkpoint (add_ / copy_ under no_grad, load_state_dict) bump the
+    table's version counter, so the next checkpoint carries the new values; so do eval() and requires_grad changes.
+    A write through `.data` (invisible to version counters) is picked up after UniverseArchive.forget."""
+    rng = np.random.default_rng(9)
+    sp = _spaces(0, 5, rng)
+    ar = _checkpoint.UniverseArchive()
+    ar.write(str(tmp_path / "a.ckpt"), _state(sp))
+    with torch.no_grad():
+        sp[1].ent_embeddings.weight.add_(0.5)
+        sp[3].rel_embeddings.weight.copy_(torch.ones_like(sp[3].rel_embeddings.weight))
+    sp[4].load_state_dict({k: v + 1.0 for k, v in sp[4].state_dict().items()})
+    sp[0].eval()
+    sp[2].ent_embeddings.weight.requires_grad_(False)
+    for name in ("b", "c"):
+        if name == "c":
+            sp[2].rel_embeddings.weight.data.mul_(3.0)
+            ar.forget(2)
+        ar.write(str(tmp_path / (name + ".ckpt")), _state(sp))
+        torch.save(_state(sp), str(tmp_path / (name + "_ref.ckpt")))
+        _same(torch.load(str(tmp_path / (name + ".ckpt")), weights_only=False),
+              torch.load(str(tmp_path / (name + "_ref.ckpt")), weights_only=False))
+
+
+def test_module_with_foreign_tensor_falls_back(tmp_path):
+    """A universe module holding a tensor that is neither a parameter nor a buffer (its storage would not be in the
+    archive's segment) is written by torch.save, not as a fragment pointing at a missing record."""
+    rng = np.random.default_rng(10)
+    sp = _spaces(0, 3, rng)
+    sp[1].extra = torch.arange(4.0)
+    ar = _checkpoint.UniverseArchive()
+    _checkpoint.save(ar, _state(sp), str(tmp_path / "a.ckpt"))
+    assert not ar._frags and not ar._segments
+    got = torch.load(str(tmp_path / "a.ckpt"), weights_only=False)
+    assert torch.equal(got["trained_embedding_spaces"][1].extra, sp[1].extra)

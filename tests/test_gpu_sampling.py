@@ -35,13 +35,13 @@ THREADS = 8
 
 
 class _Ctx:
-    def __init__(self, seed, dim=4):
+    def __init__(self, seed, dim=4, path=KG_SMALL):
         from openke import _native
         _native.require_gpu()
         self.n = _native
         self.L = _native.lib()
         self.g = ctypes.c_void_p()
-        _native.check(self.L.pt_graph_load(KG_SMALL.encode(), ctypes.byref(self.g)))
+        _native.check(self.L.pt_graph_load(path.encode(), ctypes.byref(self.g)))
         self.E = int(self.L.pt_graph_ent_total(self.g))
         R = int(self.L.pt_graph_rel_total(self.g))
         self.st0 = oracle.GlibcRand(seed).rand_reset(THREADS)

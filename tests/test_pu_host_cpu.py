@@ -224,3 +224,30 @@ def test_pickle_map_entry_points_reject_bad_layouts():
         for bad_u, bad_o, bad_i in ((uids, np.array([1, 2, 3], np.int64), ids), (uids, np.array([0, 2, 1], np.int64), ids),
                                     (np.array([3, 0], np.int64), off, ids), (uids, off, np.array([5, -1, 7], np.int64))):
             assert fn(2, bad_u.ctypes.data, bad_o.ctypes.data, bad_i.ctypes.data, None, 0, n.ctypes.data) == 1
+
+
+def test_checkpoint_after_a_universe_registered_twice(tmp_path):
+    """process_universe_mappings called twice for one next_universe_id: the reference merges the second call into the
+    same dictionaries (:179-207). The checkpoint then pickles the materialised dictionaries instead of the streams
+    (which require ascending universe ids) and holds the merged maps."""
+    from openke.config.Parallel_Universe_Config import defaultdict_int
+    cfg = _config(checkpoint_dir=str(tmp_path) + "/")
+    want = {"entity_id_mappings": defaultdict(defaultdict_int), "relation_id_mappings": defaultdict(defaultdict_int),
+            "entity_universes": defaultdict(set), "relation_universes": defaultdict(set)}
+    regs = [(0, np.array([5, 9, 2]), np.array([1])), (1, np.array([3, 5]), np.array([0, 2])),
+            (1, np.array([7, 3, 8]), np.array([2]))]
+    for uid, em, rm in regs:
+        for local, g in enumerate(em.tolist()):
+            want["entity_universes"][g].add(uid)
+            want["entity_id_mappings"][uid][g] = local
+        for local, g in enumerate(rm.tolist()):
+            want["relation_universes"][g].add(uid)
+            want["relation_id_mappings"][uid][g] = local
+        cfg._register_maps(uid, em, rm)
+        cfg.trained_embedding_spaces[uid] = TransE.seeded(uid, len(em), len(rm), dim=4, p_norm=1, norm_flag=True)
+    cfg.next_universe_id = 2
+    cfg.save_model("twice.ckpt")
+    assert cfg.__dict__["_map_log"] is None
+    got = torch.load(str(tmp_path / "twice.ckpt"), weights_only=False)
+    for k in want:
+        _same_container(got[k], want[k])
