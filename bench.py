@@ -122,6 +122,70 @@ def all_reduce(t, op):
         t.copy_(h)
 
 
+def all_gather_padded(t, ws):
+    """Every rank's 1-D tensor `t` (lengths may differ) on every rank, as a list in rank order: one all_gather of
+    the lengths, one of the payloads padded to the longest (through host memory when the backend is gloo)."""
+    import torch.distributed as dist
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+    ns = [torch.zeros_like(n) for _ in range(ws)]
+    gloo = dist.get_backend() != "nccl"
+    if gloo:
+        ns = [x.cpu() for x in ns]
+        dist.all_gather(ns, n.cpu())
+    else:
+        dist.all_gather(ns, n)
+    lens = [int(x.item()) for x in ns]
+    m = max(max(lens), 1)
+    pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+    pad[:t.numel()] = t
+    outs = [torch.zeros_like(pad) for _ in range(ws)]
+    if gloo:
+        outs = [x.cpu() for x in outs]
+        dist.all_gather(outs, pad.cpu())
+        outs = [x.to(t.device) for x in outs]
+    else:
+        dist.all_gather(outs, pad)
+    return [o[:k] for o, k in zip(outs, lens)]
+
+
+def gather_universes(unis, ws):
+    """Every rank's trained universes (tables, remaps, dims) on every rank - the input of an N = 1 recomputation of
+    the link prediction: one all_gather each of the universes' sizes, their tables (float32) and their remaps
+    (int64). Returns the union as a list of universe dicts (rank order, then each rank's order)."""
+    dev = unis[0]["ent"].device if unis else (torch.device("cuda", torch.cuda.current_device())
+                                              if torch.cuda.is_available() else torch.device("cpu"))
+    meta = torch.tensor([[u["ent"].shape[0], u["rel"].shape[0], u["dim"], int(u["nv"] is not None)] for u in unis],
+                        dtype=torch.int64, device=dev).reshape(-1)
+    flat = [u[k].reshape(-1) for u in unis for k in ("ent", "rel", "nv") if u[k] is not None]
+    tabs = torch.cat(flat) if flat else torch.zeros(0, device=dev)
+    maps = torch.from_numpy(np.concatenate([np.concatenate([u["em"], u["rm"]]) for u in unis])
+                            if unis else np.zeros(0, np.int64)).to(dev)
+    metas, tabss, mapss = (all_gather_padded(x, ws) for x in (meta, tabs, maps))
+    out = []
+    for mt, tb, mp in zip(metas, tabss, mapss):
+        mt = mt.reshape(-1, 4).cpu().numpy()
+        mp = mp.cpu().numpy()
+        ot = om = 0
+        for E, R, D, has_nv in mt:
+            u = {"dim": int(D)}
+            for k, rows in (("ent", E), ("rel", R), ("nv", R if has_nv else 0)):
+                u[k] = tb[ot:ot + rows * D].reshape(int(rows), int(D)) if rows else None
+                ot += rows * D
+            u["em"], u["rm"] = mp[om:om + E].copy(), mp[om + E:om + E + R].copy()
+            om += E + R
+            out.append(u)
+    return out
+
+
+def rank_digest(ranks):
+    """SHA-1 of the raw / filtered head and tail rank vectors (int64, query order)."""
+    import hashlib
+    m = hashlib.sha1()
+    for r in ranks:
+        m.update(np.ascontiguousarray(r, dtype=np.int64).tobytes())
+    return m.hexdigest()
+
+
 def cpu_workers():
     """Host threads for the CPU baseline: the cores this process may run on, at most 16 (a one-GPU box's
     CPU share; the reference's sampler uses 8 pthreads, Base.cpp:266-310)."""
@@ -173,6 +237,69 @@ PU_WORKLOADS = {
 }
 
 
+# Chain roofline of a universe (the universe lines' bound: one universe is one workgroup's dependent step chain,
+# its working set cache-resident, so HBM bandwidth does not describe it). Latency constants from
+# /opt/skills/guides/MI355X_MICROARCH.md "Per-instruction cycle constants": global_load L2-hit latency ~180-225 cyc,
+# ds_read latency ~50 cyc, v_fma dependent latency ~4 cyc; a DPP / permlane step of a lane-group reduction is
+# taken as 8 cyc (an op plus its data hazard), a workgroup barrier as 50 cyc.
+CHAIN_L2, CHAIN_LDS, CHAIN_DPP, CHAIN_BAR = 200, 50, 8, 50
+
+
+def universe_shape(mid, D):
+    """(G, VEC, KCH, NT, RB) of a universe row of dim D - pick_universe_shape / universe_class_threads /
+    universe_run's RB (csrc/universes.hip, universes.h, universes_kern.h)."""
+    vec = 4 if D % 4 == 0 else 1
+    chunks = -(-D // vec)
+    per_lane = 2 if vec == 4 else (8 if mid == 0 else 4)
+    G = 2
+    while G < 64 and G * per_lane < chunks:
+        G *= 2
+    kch = 1
+    while G * kch < chunks:
+        kch *= 2
+    if (2 if vec == 4 else 4) <= G <= (8 if vec == 4 else 16):
+        kch = -(-chunks // G)
+    floats = vec * kch
+    nt = 1024 if mid == 0 and floats <= 8 else 512
+    rb = 1 if floats >= 16 else ((1 if (mid == 1 or nt > 512) else 2) if floats > 4 else (2 if nt > 512 else 4))
+    return G, vec, kch, nt, rb
+
+
+def chain_floor(mid, D, bs, rows_per_step, valu_per_step=None):
+    """Cycles per step a universe's step chain cannot go below (universes_kern.h universe_run), by phase:
+    phase A, ceil(bs / lane groups) rounds of one positive per lane group, each round the dependent chain
+      LDS (batch) -> L2 (positive rows; wide rows also the first negative's) -> reduction (normalizations)
+      -> reduction (positive score) -> [narrow rows: LDS + L2 (negative row) + reduction] -> reduction (negative
+      score) -> 4 LDS round trips (the contribution links: negative, relation flag, head, tail);
+    phase B, ceil(rows / (lane groups x rows per group)) rounds, each
+      LDS (work list) -> LDS (list head) -> L2 (row, Adagrad state, first contribution) -> reduction (the
+      normalize Jacobian's dot product);
+    two workgroup barriers per step; a reduction over G lanes = log2(G) DPP steps + one op. With
+    `valu_per_step` (VALU wave-instructions per step of the universe, rocprofv3 SQ_INSTS_VALU of it alone) the
+    issue time of those instructions on the CU's 4 SIMDs at 2 cycles each (SIMD-32 throughput) is added: the
+    floor then is latency chain + VALU issue."""
+    G, vec, kch, nt, rb = universe_shape(mid, D)
+    gpb = nt // G
+    red = CHAIN_DPP * (G.bit_length() - 1) + CHAIN_DPP
+    wide = G >= 32 and mid == 0
+    rounds_a = -(-max(bs, 1) // gpb)
+    a_round = CHAIN_LDS + CHAIN_L2 + 3 * red + (0 if wide else CHAIN_LDS + CHAIN_L2 + red) + 4 * CHAIN_LDS
+    rounds_b = -(-max(int(round(rows_per_step)), 1) // (gpb * rb))
+    b_round = 2 * CHAIN_LDS + CHAIN_L2 + red
+    lat = rounds_a * a_round + rounds_b * b_round + 2 * CHAIN_BAR
+    out = {"shape": {"lanes": G, "vec": vec, "chunks_per_lane": kch, "threads": nt, "lane_groups": gpb,
+                     "rows_per_group": rb},
+           "rounds_a": rounds_a, "a_round_cycles": a_round, "rounds_b": rounds_b, "b_round_cycles": b_round,
+           "barriers_cycles": 2 * CHAIN_BAR, "latency_cycles": lat,
+           "constants": {"l2_hit": CHAIN_L2, "lds": CHAIN_LDS, "dpp_step": CHAIN_DPP, "barrier": CHAIN_BAR}}
+    if valu_per_step is not None:
+        out["valu_issue_cycles"] = 2.0 * valu_per_step / 4.0
+        out["floor_cycles"] = lat + out["valu_issue_cycles"]
+    else:
+        out["floor_cycles"] = float(lat)
+    return out
+
+
 def universe_draws(k, tc_range=(500, 2000), margin_range=(1, 4), seed0=4):
     """Python-RNG hyperparameters of universe k exactly as Parallel_Universe_Config draws them
     (:157-161, :210-236): randrange(tc), uniform(balance), randrange(margin), randrange(epochs),
@@ -192,7 +319,41 @@ def _xavier(rng, rows, dim):
     return rng.uniform(-b, b, (rows, dim)).astype(np.float32)
 
 
-def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
+def chain_profile(L, us, reset, idx, time_set, mid, name, prof_on):
+    """One extra (untimed) training of the set with the per-universe cycle counters on: the longest universe's
+    measured cycles per step, its phases and phase-B rows, against chain_floor. VALU issue joins the floor when
+    profiles/pmc_<name>_chain.json holds rocprofv3 counters of that universe alone on this library build."""
+    from openke import _native
+    if not prof_on:
+        _native.check(L.pt_universe_set_profiling(us, 1))
+    time_set(us, reset, idx, 1, 0)
+    pr = np.zeros(64 * len(idx), dtype=np.uint64)
+    _native.check(L.pt_universe_set_profile(us, pr.ctypes.data))
+    if not prof_on:
+        _native.check(L.pt_universe_set_profiling(us, 0))
+    pr = pr.reshape(-1, 64).astype(np.float64)
+    span = pr[:, :3].sum(axis=1)
+    i = int(np.argmax(span))
+    steps = max(pr[i, 3], 1.0)
+    bs, D, E = int(pr[i, 4]), int(pr[i, 5]), int(pr[i, 6])
+    rows = pr[i, 62] / steps
+    pmc, _ = load_pmc("%s_chain" % name)
+    valu = None
+    if pmc and pmc.get("longest") == {"bs": bs, "dim": D, "ent": E, "steps": int(steps)}:
+        valu = pmc["valu_per_step"]
+    fl = chain_floor(mid, D, bs, rows, valu)
+    achieved = span[i] / steps
+    return {"achieved": achieved, "floor": fl["floor_cycles"], "frac": fl["floor_cycles"] / achieved,
+            "unit": "cycles/step", "longest_universe": {"bs": bs, "dim": D, "ent": E, "steps": int(steps),
+                                                        "rows_per_step": rows, "cycles": span[i],
+                                                        "ms_at_2.4GHz": span[i] / 2.4e6,
+                                                        "cycles_per_step": {"presample": pr[i, 0] / steps,
+                                                                            "phase_a": pr[i, 1] / steps,
+                                                                            "phase_b": pr[i, 2] / steps}},
+            "floor_model": fl, "valu_counted": valu is not None}
+
+
+def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check_lp=False):
     """PuTransE / PuTransH universes placed over ranks by LPT (place_universes; no collective in training), Adagrad,
     neg 1, bern 0, filter 0, nbatches 20, 8 sampler threads. One step = every universe's full training
     run (all its epochs) in one persistent launch. C4 adds link prediction over the test split: each
@@ -334,9 +495,17 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
                         "each launch's stream); overlap = summed launch time / span"}
 
     every = list(range(len(jobs)))
+    if getattr(args, "longest_only", False) and jobs:
+        # the set's longest universe alone (by the placement cost model): its chain, e.g. under rocprofv3 --pmc
+        i_long = max(every, key=lambda i: universe_cost(int(jobs[i].epochs), int(jobs[i].batch_size) * 20,
+                                                        int(jobs[i].dim)))
+        every = [i_long]
+        slots_step = int(jobs[i_long].epochs) * 20 * int(jobs[i_long].batch_size) * 2
+        bytes_step = slots_step * algorithmic_bytes_per_slot(model, "adagrad", int(jobs[i_long].dim))
     uset, reset = make_set(every)
     el = time_set(uset, reset, every, args.c3_steps, args.c3_warmup)
     class_launches = launch_times(uset)
+    chain = chain_profile(L, uset, reset, every, time_set, mid, name, prof_on) if every else None
     tot = torch.tensor([el, float(slots_step), float(bytes_step)], dtype=torch.float64, device=dev)
     if ws > 1:
         import torch.distributed as dist
@@ -417,12 +586,14 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
            "universes_per_gpu": len(own), "host_universe_build_s": build_s,
            "note_runs": "every timed run trains every universe from its initial tables, Adagrad state and sampler "
                         "streams (restored before the run, outside the timed region)",
-           "roofline": {"bound": "latency (per-universe dependent step chain)", "achieved_per_gpu": achieved,
-                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                        "note": "algorithmic bytes (SURVEY 8(d) per slot) per wall second vs the HBM peak, not an HBM "
-                                "measurement: a universe's working set (tables, Adagrad state, contribution rows, "
-                                "a few hundred KB) is cache-resident and its work lists, relation gradient rows and "
-                                "presampled batches live in LDS, so frac > 1 (C4) means on-chip service"}}
+           "roofline": dict(chain or {}, bound="chain", algorithmic_GBps_per_gpu=achieved,
+                            note="the set ends with its longest universe, one workgroup's dependent step chain: achieved "
+                                 "= that universe's measured shader cycles per step (pt_universe_set_profiling, one "
+                                 "extra untimed training), floor = chain_floor's model of it (bench.py: L2 / LDS round "
+                                 "trips, lane-group reductions, barriers, + VALU issue when its rocprofv3 counters are "
+                                 "committed for this build), frac = floor / achieved. algorithmic_GBps_per_gpu (SURVEY "
+                                 "8(d) bytes per wall second) is not an HBM measurement: the universes' working sets "
+                                 "are cache- and LDS-resident")}
     if class_launches is not None:
         out["class_launches"] = class_launches
     if det_s is not None:
@@ -433,7 +604,20 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False):
     if longest is not None:
         out["longest_universe_cycles"] = longest
     if do_lp:
-        out["link_prediction"] = universe_link_prediction(L, path, unis, mid, p_norm, ws, dev)
+        out["link_prediction"] = lp = universe_link_prediction(L, path, unis, mid, p_norm, ws, dev)
+        if check_lp and ws > 1:
+            # the N = 1 recomputation: every rank's trained universes gathered, rank 0 scores and ranks all of them
+            # alone (no collective) - the distributed ranks must be bit-identical (MIN is exact)
+            t0 = time.perf_counter()
+            allu = gather_universes(unis, ws)
+            lp["gather_universes_s"] = time.perf_counter() - t0
+            if rank == 0:
+                ref = universe_link_prediction(L, path, allu, mid, p_norm, 1, dev)
+                lp["n1_universes"] = len(allu)
+                lp["n1_rank_digest"] = ref["rank_digest"]
+                lp["n1_mrr_mr_hit10_hit3_hit1"] = ref["mrr_mr_hit10_hit3_hit1"]
+                lp["digest_match"] = ref["rank_digest"] == lp["rank_digest"]
+            del allu
     L.pt_graph_free(g)
     if cpu and ws == 1 and rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = universe_cpu_baseline(path, name, args.cpu_seconds, getattr(args, "dim", 0),
@@ -637,6 +821,7 @@ def universe_link_prediction(L, path, unis, mid, p_norm, ws, dev):
     dim_of = np.array([u["dim"] for u in unis], dtype=np.int64)
     cell_dims = int((ent_of[pair_arr[:, 1]] * dim_of[pair_arr[:, 1]]).sum()) if len(pair_arr) else 0
     return {"queries": int(n), "keys": len(keys), "pairs_this_rank": len(pair_arr), "seconds": el,
+            "rank_digest": rank_digest(ranks),
             "scored_cells": cells, "scored_cell_dims": cell_dims,
             "score_s": t_score, "min_combine_s": t_comb, "rank_s": el - t_score - t_comb,
             "mrr_mr_hit10_hit3_hit1": [float(x) for x in met[:5]],
@@ -701,6 +886,8 @@ def main():
     ap.add_argument("--slot-scale", type=int, default=-1,
                     help="C2 / C1: 1 = slot-scale mode (per-slot records + positive base rows instead of contribution "
                          "rows; pt_trainer_set_slot_scale), 0 = contribution rows, -1 = the library's default")
+    ap.add_argument("--longest-only", action="store_true",
+                    help="universe workloads: train only the set's longest universe (its chain alone)")
     ap.add_argument("--no-dropin", action="store_true",
                     help="universe workloads: skip the drop-in Parallel_Universe_Config timing")
     ap.add_argument("--launch-check", action="store_true",
@@ -882,6 +1069,15 @@ def main():
         a2 = _copy.copy(args)
         a2.universes, a2.dim, a2.place_world, a2.deterministic_timing = 6000, 20, 0, 0
         c3r = run_universes(a2, ws, rank, dev, "c3", cpu=False)
+    # N > 1: the one collective of the path (north_star: RCCL over xGMI for the score combine at link prediction) in
+    # the default line - C4's 1,024 universes placed over the ranks by LPT, each rank's universes MIN-combined into
+    # the key rows, one all_reduce(MIN), GPU ranking; rank 0 checks the ranks against an N = 1 recomputation
+    c4lp = None
+    if ws > 1 and not args.no_c3:
+        import copy as _copy
+        a4 = _copy.copy(args)
+        a4.universes, a4.dim, a4.place_world, a4.deterministic_timing = 0, 0, 0, 0
+        c4lp = run_universes(a4, ws, rank, dev, "c4", cpu=False, check_lp=True)
     if rank != 0:
         if ws > 1:
             import torch.distributed as dist
@@ -944,12 +1140,17 @@ def main():
         rec["pu_c3_weak"] = c3w
     if c3r is not None:
         rec["pu_c3_ref6000"] = c3r
+    if c4lp is not None:
+        rec["pu_c4_lp"] = c4lp
     if ws == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(path, wl, args.cpu_seconds)
     print(json.dumps(rec), flush=True)
     if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    if c4lp is not None and not c4lp["link_prediction"].get("digest_match", False):
+        print("bench.py: pu_c4_lp ranks differ from the N = 1 recomputation", file=sys.stderr)
+        sys.exit(4)
 
 
 if __name__ == "__main__":

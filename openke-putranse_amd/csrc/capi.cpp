@@ -1210,6 +1210,18 @@ hipError_t class_streams(int device, int mode, size_t n, std::vector<hipStream_t
 }
 }  // namespace
 
+// Team universes (universes_team.h): the widest team a set may give one universe (1: none), process-wide like the
+// reference's global state; read when a set is created
+namespace {
+std::atomic<int> g_team_width{4};
+}
+extern "C" int pt_set_universe_team_width(int32_t w) {
+    PT_CHECK(w == 1 || w == 2 || w == 4, PT_EINVAL, "pt_set_universe_team_width: 1, 2 or 4");
+    g_team_width.store(w);
+    return PT_OK;
+}
+extern "C" int32_t pt_get_universe_team_width(void) { return g_team_width.load(); }
+
 // Train many universes with the persistent multi-universe kernel (universes.hip).
 struct pt_universe_set {
     int32_t model = 0, p_norm = 1, norm_flag = 1, opt = PT_ADAGRAD;
@@ -1223,7 +1235,13 @@ struct pt_universe_set {
         int64_t off, n;
         double work;
         int64_t share = 1;   // workgroups (= CUs) of its launch
+        // team launch (shape class >= kUniTeamBase): [grid][2] universe (index from off) and member (-1: idle)
+        int32_t *d_map = nullptr;
+        int64_t grid = 0;
     };
+    uint32_t *d_team_sync = nullptr;      // team universes' arrival counters (inside the arena, zeroed per call)
+    int64_t n_team_sync = 0;
+    pt::UniverseLaunch team_cfg;          // the team launches' LDS plan
     std::vector<Group> groups;            // runs of d_us with one shape class (one kernel launch each)
     std::vector<hipStream_t> streams;     // PT_UNI_STREAMS=0 only: per-set side streams (else the process pool's)
     std::vector<hipEvent_t> events;
@@ -1240,7 +1258,9 @@ struct pt_universe_set {
     bool ordered = false;
     void *ord_arena = nullptr;            // per universe [4][seq][dim] gradient rows
     int64_t ord_max_seq = 0;
+    void *team_arena = nullptr;           // team universes: partials, arrival counters, launch maps
     ~pt_universe_set() {
+        if (team_arena) (void)hipFree(team_arena);
         for (auto e : events) (void)hipEventDestroy(e);
         for (auto e : t_start) (void)hipEventDestroy(e);
         for (auto e : t_stop) (void)hipEventDestroy(e);
@@ -1324,6 +1344,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     // kernel is register-allocated for all its shapes at once: the longest C3 universe's shape alone runs its
     // chain in 78 instead of 94 Mcycles. At most four launches in all (the hardware queues a process gets).
     std::vector<int> cls_v((size_t)n);
+    std::vector<int> team_w;
     {
         std::vector<int> shape_v((size_t)n);
         std::map<int, double> hot_cost;   // class-1 shape -> its longest universe (steps x (4 + rounds))
@@ -1354,6 +1375,62 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
             if (atoi(v) == 0) hot.clear();
         for (int64_t i = 0; i < n; ++i)
             if (hot.count(shape_v[i])) cls_v[i] = pt::kUniHotBase + shape_v[i];
+        // Teams (universes_team.h): with fewer universes than CUs the set's makespan is its longest chain and CUs
+        // idle. The spare CUs go, two at a time, to the universe whose modelled time is longest: its team doubles
+        // (1 -> 2 -> 4 workgroups, modelled speed-ups kTeamSpeed), as long as a team universe's LDS plan fits and
+        // at most two row shapes take teams (one launch per shape).
+        int cus_t = 0;
+        PT_HIP(hipDeviceGetAttribute(&cus_t, hipDeviceAttributeMultiprocessorCount, set->device));
+        const int wmax = g_team_width.load();
+        team_w.assign((size_t)n, 1);
+        if (model == PT_TRANSE && wmax > 1 && n < cus_t) {
+            static const double kTeamSpeed[5] = {0.0, 1.0, 1.6, 0.0, 2.4};
+            std::vector<bool> ok((size_t)n, false);
+            int64_t cap = 1;   // the set's work-list capacity (its largest batch)
+            for (int64_t i = 0; i < n; ++i) cap = std::max<int64_t>(cap, jobs[i].batch_size * (4 + jobs[i].neg));
+            for (int64_t i = 0; i < n; ++i)
+                ok[i] = pt::universe_team_shape(shape_v[i], model) && jobs[i].batch_size > 0 &&
+                        jobs[i].epochs * jobs[i].nbatches > 0;
+            // the team launch's LDS with one presampled batch, over its universes' largest sizes (the launch gets as
+            // many batches as then fit)
+            int64_t m_rel = 0, m_ent = 0, m_slots = 0, m_seq = 0, m_dim = 0;
+            auto fits_with = [&](int64_t i) {
+                const pt::Graph &g = reinterpret_cast<const pt_graph *>(jobs[i].graph)->g;
+                const int64_t b = jobs[i].batch_size;
+                return pt::universe_team_lds_bytes(cap, std::max(m_rel, g.rel_total), std::max(m_ent, g.ent_total),
+                                                   std::max(m_slots, b * (2 + jobs[i].neg)),
+                                                   1, std::max(m_seq, b * (1 + jobs[i].neg)),
+                                                   std::max(m_dim, jobs[i].dim)) <= lds_budget;
+            };
+            int64_t spare = (int64_t)cus_t - n;
+            auto t_of = [&](int64_t i) { return work(i) / kTeamSpeed[team_w[(size_t)i]]; };
+            while (spare > 0) {
+                int64_t best = -1;
+                for (int64_t i = 0; i < n; ++i)
+                    if (best < 0 || t_of(i) > t_of(best)) best = i;
+                if (best < 0 || !ok[best] || team_w[best] >= wmax) break;   // the longest cannot get faster
+                const int64_t cost = team_w[best];
+                if (cost > spare) break;
+                std::set<int> shapes;
+                for (int64_t i = 0; i < n; ++i)
+                    if (team_w[i] > 1 || i == best) shapes.insert(shape_v[i]);
+                if (shapes.size() > 2 || (team_w[best] == 1 && !fits_with(best))) break;
+                if (team_w[best] == 1) {
+                    const pt::Graph &g = reinterpret_cast<const pt_graph *>(jobs[best].graph)->g;
+                    m_rel = std::max(m_rel, g.rel_total);
+                    m_ent = std::max(m_ent, g.ent_total);
+                    m_slots = std::max(m_slots, jobs[best].batch_size * (2 + jobs[best].neg));
+                    m_seq = std::max(m_seq, jobs[best].batch_size * (1 + jobs[best].neg));
+                    m_dim = std::max(m_dim, jobs[best].dim);
+                }
+                team_w[best] *= 2;
+                spare -= cost;
+            }
+            if (const char *v = pt_tuning_env("PT_UNI_TEAMS"))   // tuning: 0 = no teams
+                if (atoi(v) == 0) team_w.assign((size_t)n, 1);
+            for (int64_t i = 0; i < n; ++i)
+                if (team_w[i] > 1) cls_v[i] = pt::kUniTeamBase + shape_v[i];
+        }
     }
     auto cls_of = [&](int64_t i) { return cls_v[(size_t)i]; };
     std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
@@ -1368,6 +1445,14 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         set->groups.back().work += work(order[k]);
     }
     PT_CHECK(set->groups.size() <= 64, PT_EINVAL, "too many universe shape classes");
+    // a team launch takes one CU per member of its universes
+    auto is_team = [&](size_t k) { return set->groups[k].shape >= pt::kUniTeamBase; };
+    for (size_t k = 0; k < set->groups.size(); ++k) {
+        if (!is_team(k)) continue;
+        int64_t w = 0;
+        for (int64_t q = set->groups[k].off; q < set->groups[k].off + set->groups[k].n; ++q) w += team_w[order[q]];
+        set->groups[k].share = w;
+    }
     // CU shares: a universe's time by the step-cost model (`work`); give every group one CU,
     // then each further CU to the group whose LPT makespan over its current share is longest (the launches run
     // concurrently, so the slowest group ends the set)
@@ -1395,11 +1480,16 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
             return end;
         };
         std::vector<double> ms(set->groups.size());
-        for (size_t k = 0; k < set->groups.size(); ++k) ms[k] = makespan(k, 1);
-        for (int64_t left = (int64_t)cus - (int64_t)set->groups.size(); left > 0; --left) {
+        int64_t left = (int64_t)cus;
+        for (size_t k = 0; k < set->groups.size(); ++k) {
+            ms[k] = makespan(k, 1);
+            left -= set->groups[k].share;
+        }
+        for (; left > 0; --left) {
             size_t best = set->groups.size();
             for (size_t k = 0; k < set->groups.size(); ++k)
-                if (set->groups[k].share < set->groups[k].n && (best == set->groups.size() || ms[k] > ms[best]))
+                if (!is_team(k) && set->groups[k].share < set->groups[k].n &&
+                    (best == set->groups.size() || ms[k] > ms[best]))
                     best = k;
             if (best == set->groups.size()) break;
             set->groups[best].share += 1;
@@ -1478,6 +1568,10 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         U.threads = J.threads; U.bs = J.batch_size; U.nbatches = J.nbatches; U.epochs = J.epochs; U.dim = J.dim;
         U.lr = J.lr; U.margin = J.margin;
         U.shape = pt::universe_shape_id(J.dim, model);
+        U.team_w = team_w.empty() ? 1 : team_w[(size_t)i];
+        U.team_part = nullptr;
+        U.team_sync = nullptr;
+        U.team_err = nullptr;
         if (set->host_of_job.empty()) set->host_of_job.assign((size_t)n, -1);
         set->host_of_job[(size_t)i] = (int64_t)set->host.size();
         set->host.push_back(U);
@@ -1530,6 +1624,81 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     C.threads = 512;
     // tuning overrides (benchmarks): PT_UNI_RELGRAD / CONTRIB / LDSFLAGS / PRESAMPLE = 0 disable the
     // LDS placements above, PT_UNI_FENCE=1 forces agent-scope fences
+    // Team launches (universes_team.h): their LDS plan (every universe's presampled batches, as many as fit), one
+    // arena for the relation / loss partials and arrival counters of their universes and the launch maps, each team's
+    // members on blocks of one residue mod 8 (the dispatcher's round-robin over the XCDs: one L2 for the team -
+    // performance only, the protocol does not depend on it)
+    {
+        int64_t t_rel = 0, t_ent = 0, t_slots = 0, t_seq = 0, t_dim = 0, t_nb = 0, part_b = 0, n_team = 0, map_b = 0;
+        std::vector<int64_t> grid_of(set->groups.size(), 0);
+        std::vector<std::vector<int32_t>> maps(set->groups.size());
+        for (size_t k = 0; k < set->groups.size(); ++k) {
+            const auto &gr = set->groups[k];
+            if (gr.shape < pt::kUniTeamBase) continue;
+            std::vector<std::pair<int, int64_t>> teams;   // (members, index from off)
+            for (int64_t q = gr.off; q < gr.off + gr.n; ++q) {
+                const pt::UniverseDev &U = set->host[(size_t)q];
+                teams.push_back({U.team_w, q - gr.off});
+                t_rel = std::max(t_rel, U.g.rel_total);
+                t_ent = std::max(t_ent, U.g.ent_total);
+                t_slots = std::max(t_slots, U.bs * (2 + set->neg));
+                t_seq = std::max(t_seq, U.bs * (1 + set->neg));
+                t_dim = std::max(t_dim, U.dim);
+                t_nb = std::max(t_nb, U.nbatches);
+                part_b += al(4 * (U.team_w * U.g.rel_total * U.dim + U.team_w * U.epochs));
+                ++n_team;
+            }
+            std::stable_sort(teams.begin(), teams.end(), [](const std::pair<int, int64_t> &a,
+                                                            const std::pair<int, int64_t> &b) { return a.first > b.first; });
+            int64_t used[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            std::vector<std::pair<int64_t, std::pair<int32_t, int32_t>>> blocks;
+            for (const auto &t : teams) {
+                int x = 0;
+                for (int c = 1; c < 8; ++c)
+                    if (used[c] < used[x]) x = c;
+                for (int m = 0; m < t.first; ++m) blocks.push_back({x + 8 * (used[x] + m), {(int32_t)t.second, m}});
+                used[x] += t.first;
+            }
+            int64_t rows = 0;
+            for (int c = 0; c < 8; ++c) rows = std::max(rows, used[c]);
+            grid_of[k] = 8 * rows;
+            maps[k].assign((size_t)(2 * grid_of[k]), -1);
+            for (const auto &b : blocks) {
+                maps[k][(size_t)(2 * b.first)] = b.second.first;
+                maps[k][(size_t)(2 * b.first + 1)] = b.second.second;
+            }
+            map_b += al(4 * (int64_t)maps[k].size());
+        }
+        if (n_team > 0) {
+            auto &T = set->team_cfg;
+            T = C;
+            const int64_t fixed = pt::universe_team_lds_bytes(C.list_cap, t_rel, t_ent, t_slots, 0, t_seq, t_dim);
+            T.pchunk = std::min<int64_t>(t_nb, (lds_budget - fixed) / std::max<int64_t>(12 * t_seq, 1));
+            PT_CHECK(T.pchunk >= 1, PT_EINVAL, "team universes: LDS plan does not fit");
+            T.lds_bytes = pt::universe_team_lds_bytes(C.list_cap, t_rel, t_ent, t_slots, T.pchunk, t_seq, t_dim);
+            const int64_t sync_b = al(4 * (n_team + 1));   // + the error word
+            PT_HIP(hipMalloc(&set->team_arena, (size_t)(part_b + sync_b + map_b)));
+            char *tb = (char *)set->team_arena;
+            set->d_team_sync = (uint32_t *)(tb + part_b);
+            set->n_team_sync = n_team;
+            int64_t po = 0, si = 0, mo = part_b + sync_b;
+            for (size_t k = 0; k < set->groups.size(); ++k) {
+                auto &gr = set->groups[k];
+                if (gr.shape < pt::kUniTeamBase) continue;
+                for (int64_t q = gr.off; q < gr.off + gr.n; ++q) {
+                    pt::UniverseDev &U = set->host[(size_t)q];
+                    U.team_part = (float *)(tb + po);
+                    po += al(4 * (U.team_w * U.g.rel_total * U.dim + U.team_w * U.epochs));
+                    U.team_sync = set->d_team_sync + si++;
+                    U.team_err = set->d_team_sync + n_team;
+                }
+                gr.d_map = (int32_t *)(tb + mo);
+                gr.grid = grid_of[k];
+                PT_HIP(hipMemcpy(gr.d_map, maps[k].data(), 4 * maps[k].size(), hipMemcpyHostToDevice));
+                mo += al(4 * (int64_t)maps[k].size());
+            }
+        }
+    }
     *out = set.release();
     return PT_OK;
 }
@@ -1614,6 +1783,7 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
         set->t_start.push_back(a);
         set->t_stop.push_back(b);
     }
+    if (set->n_team_sync > 0) PT_HIP(hipMemsetAsync(set->d_team_sync, 0, 4 * (set->n_team_sync + 1), st));
     PT_HIP(hipEventRecord(set->events[0], st));
     for (size_t k = 0; k < ng; ++k)
         if (qs[k] != st) PT_HIP(hipStreamWaitEvent(qs[k], set->events[0], 0));
@@ -1628,6 +1798,15 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
             const char *v = pt_tuning_env("PT_UNI_GRID");
             return v && atoi(v) != 0;
         }();
+        if (gr.shape >= pt::kUniTeamBase) {
+            const hipError_t e = pt::launch_universes_team(set->d_us + gr.off, gr.d_map, gr.grid,
+                                                           gr.shape - pt::kUniTeamBase, set->p_norm, set->norm_flag,
+                                                           set->opt, set->neg, (int)set->bern, (int)set->filter,
+                                                           set->team_cfg, q);
+            if (e != hipSuccess) return pt::fail(PT_EHIP, std::string("launch_universes_team: ") + hipGetErrorString(e));
+            PT_HIP(hipEventRecord(set->t_stop[k], q));
+            continue;
+        }
         const hipError_t e = pt::launch_universes(set->d_us + gr.off, gr.n, set->d_counter + k, gr.shape,
                                                   per_universe ? gr.n : share,
                                                   set->model, set->p_norm, set->norm_flag, set->opt, set->neg,
@@ -1643,6 +1822,11 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
     // the host array must outlive the async copy: this call returns only after it has been consumed
     PT_HIP(hipStreamSynchronize(st));
     set->timed = true;
+    if (set->n_team_sync > 0) {
+        uint32_t err = 0;
+        PT_HIP(hipMemcpy(&err, set->d_team_sync + set->n_team_sync, 4, hipMemcpyDeviceToHost));
+        PT_CHECK(err == 0, PT_EHIP, "team universes: a team member never arrived (workgroups not co-resident)");
+    }
     return PT_OK;
 }
 
@@ -1668,6 +1852,19 @@ extern "C" int pt_universe_set_launch_times(pt_universe_set *set, int64_t cap, f
         out[3 * k] -= lo;
         out[3 * k + 1] -= lo;
     }
+    return PT_OK;
+}
+
+// how the set trains: universes in team launches and the workgroups (CUs) those take
+extern "C" int pt_universe_set_teams(const pt_universe_set *set, int64_t *team_universes, int64_t *team_workgroups) {
+    PT_CHECK(set && team_universes && team_workgroups, PT_EINVAL, "pt_universe_set_teams: null argument");
+    *team_universes = 0;
+    *team_workgroups = 0;
+    for (const auto &gr : set->groups)
+        if (gr.shape >= pt::kUniTeamBase) {
+            *team_universes += gr.n;
+            *team_workgroups += gr.share;
+        }
     return PT_OK;
 }
 
@@ -1706,7 +1903,8 @@ extern "C" int pt_universe_set_profiling(pt_universe_set *set, int32_t on) {
 }
 
 // diagnostics: per universe (set order) 64 words: cycles in presampling / phase A / phase B, steps, batch size,
-// dim and entities of the last train call with profiling on; words 8-63 phase stamps of one step (tuning build)
+// dim, entities, start / duration (100 MHz wall clock) of the last train call with profiling on; word 62 the rows
+// updated in phase B summed over the steps; the other words 8-63 phase stamps of one step (tuning build)
 extern "C" int pt_universe_set_profile(pt_universe_set *set, uint64_t *out) {
     PT_CHECK(set && out, PT_EINVAL, "null argument");
     PT_CHECK(set->prof, PT_ESTATE, "profiling not enabled (pt_universe_set_profiling)");
@@ -2254,6 +2452,9 @@ extern "C" void importTestFiles(void) {
         all.insert(all.end(), l.valid.begin(), l.valid.end());
     }
     l.triple_total = (int64_t)all.size();
+    // type lists read for an earlier import belong to that dataset: a type-constrained ranking of this one
+    // reads its own type_constrain.txt (importTypeFiles again, or the drop-in Tester's load on first use)
+    l.types_loaded = false;
     std::vector<int64_t> h(all.size()), t(all.size()), r(all.size());
     for (size_t i = 0; i < all.size(); ++i) { h[i] = all[i].h; t[i] = all[i].t; r[i] = all[i].r; }
     pt_known *k = nullptr;

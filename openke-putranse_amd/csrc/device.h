@@ -236,7 +236,9 @@ constexpr uint32_t kOob = 0x80000000u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
 }
-template <int G, int VEC, int KCH>
+// AUX: the buffer instruction's cache-policy bits (16 = sc1: agent-coherent, past the CU's L1 - the hand-off form of
+// MI355X_MICROARCH.md for data another workgroup wrote or reads)
+template <int G, int VEC, int KCH, int AUX = 0>
 __device__ __forceinline__ void bload(V<G, VEC, KCH> &o, __amdgpu_buffer_rsrc_t rs, uint32_t row_bytes, int D,
                                       int lane) {
 #pragma unroll
@@ -244,16 +246,16 @@ __device__ __forceinline__ void bload(V<G, VEC, KCH> &o, __amdgpu_buffer_rsrc_t 
         const int c = k * G + lane;
         const uint32_t off = c * VEC < D ? row_bytes + (uint32_t)(c * VEC * 4) : kOob;
         if constexpr (VEC == 4) {
-            const pt_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+            const pt_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUX);
             o.x[k * 4 + 0] = __uint_as_float(v.x); o.x[k * 4 + 1] = __uint_as_float(v.y);
             o.x[k * 4 + 2] = __uint_as_float(v.z); o.x[k * 4 + 3] = __uint_as_float(v.w);
         } else {
             static_assert(VEC == 1, "bload: VEC 1 or 4");
-            o.x[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+            o.x[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, AUX));
         }
     }
 }
-template <int G, int VEC, int KCH>
+template <int G, int VEC, int KCH, int AUX = 0>
 __device__ __forceinline__ void bstore(const V<G, VEC, KCH> &o, __amdgpu_buffer_rsrc_t rs, uint32_t row_bytes, int D,
                                        int lane) {
 #pragma unroll
@@ -263,9 +265,9 @@ __device__ __forceinline__ void bstore(const V<G, VEC, KCH> &o, __amdgpu_buffer_
         if constexpr (VEC == 4) {
             const pt_u32x4 v = {__float_as_uint(o.x[k * 4 + 0]), __float_as_uint(o.x[k * 4 + 1]),
                                 __float_as_uint(o.x[k * 4 + 2]), __float_as_uint(o.x[k * 4 + 3])};
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, AUX);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.x[k]), rs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o.x[k]), rs, off, 0, AUX);
         }
     }
 }

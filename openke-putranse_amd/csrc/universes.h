@@ -24,6 +24,10 @@ struct UniverseDev {
     int64_t threads, bs, nbatches, epochs, dim;
     float lr, margin;
     int32_t shape;                                  // universe_shape_id(dim)
+    int32_t team_w;                                 // workgroups training it (universes_team.h), 1: one
+    float *team_part;                               // team: [team_w][rel][dim] relation partials, [team_w][epochs] losses
+    uint32_t *team_sync;                            // team: arrival counter (zeroed before each launch)
+    uint32_t *team_err;                             // team: the set's error word (a bounded poll ran out)
 };
 
 // workgroup size of each (model, shape class) kernel. TransE's narrow classes (<= 8 floats per lane) run 1,024
@@ -44,6 +48,9 @@ constexpr int universe_hot_threads(int G) { return G >= 32 ? PT_UNI_HOT_WIDE_NT 
 // class ids from kUniHotBase on: a "hot" class-1 shape (id - kUniHotBase) run by a kernel compiled for that shape
 // alone (its own register allocation; see pt_universe_set_create)
 constexpr int kUniHotBase = 64;
+// class ids from kUniTeamBase on: universes of shape (id - kUniTeamBase) trained by teams of workgroups
+// (universes_team.h), one launch per shape
+constexpr int kUniTeamBase = 128;
 
 // launch configuration of one group of universes (host-chosen for the largest universe of the group)
 struct UniverseLaunch {
@@ -77,6 +84,14 @@ hipError_t launch_universes(const UniverseDev *d_us, int64_t n, int *counter, in
                             int p_norm, int norm_flag, int opt, int64_t neg, int bern, int filter,
                             const UniverseLaunch &cfg, hipStream_t st);
 int universe_shape_class(int shape);
+// team universes (universes_team.h): whether a shape has a team kernel (TransE, 8-float class), the dynamic LDS of
+// its launch, and the launch over `grid` workgroups (map: [grid][2] universe index into d_us, member or -1)
+bool universe_team_shape(int shape, int model);
+int64_t universe_team_lds_bytes(int64_t list_cap, int64_t rel, int64_t ent, int64_t slots, int64_t pchunk,
+                                int64_t seq, int64_t dim);
+hipError_t launch_universes_team(const UniverseDev *d_us, const int32_t *d_map, int64_t grid, int shape, int p_norm,
+                                 int norm_flag, int opt, int64_t neg, int bern, int filter, const UniverseLaunch &cfg,
+                                 hipStream_t st);
 int universe_shape_groups(int shape, int model);
 int universe_shape_row_slots(int shape);
 

@@ -70,6 +70,12 @@ __device__ __forceinline__ void phase_barrier(bool agent) {
 // on one C4 component in r03, is within the forward-error bound the parity tests use since r04.) The
 // reference-order kernel (ordered.hip) keeps IEEE forms throughout.
 constexpr bool kUF = true;
+// PT_UNI_FAST_WIDE=0 (measurement builds): the wide rows (lane groups of 32 / 64 lanes: C4's D = 200) take the IEEE
+// forms too
+#ifndef PT_UNI_FAST_WIDE
+#define PT_UNI_FAST_WIDE 1
+#endif
+constexpr bool uni_fast(int G, int floats) { return kUF && floats <= 8 && (PT_UNI_FAST_WIDE || G < 32); }
 
 // backward of F.normalize (vnormalize_bwd) without a branch on the norm: the rows of a wave's lane groups
 // take the (g - x (x.g)/n^2) / n form or the clamp's g / eps form by selects, not by divergent paths
@@ -227,12 +233,25 @@ struct UniverseSink {
 // per-negative row-role bookkeeping). get_neg(q, k, &e, &tail_side). Gradients in normalized space, like
 // group_step for TransE; a corrupted row equal to a positive row is simply a separate contribution.
 // Positive q's gradient rows go to sink sk[q] (its own contribution slots). Returns the summed losses.
-template <int NP, int G, int VEC, int KCH, bool PF = false, typename Sink, typename NegFn>
+// Row of a universe table for transe_step: SC1 (a team universe, universes_team.h) loads it past the CU's L1 with
+// sc1 buffer loads (rows another team member updated), else uload.
+template <bool SC1, int G, int VEC, int KCH>
+__device__ __forceinline__ void trow(V<G, VEC, KCH> &o, const float *table, int64_t rows, int row, int D, int lane) {
+    if constexpr (SC1)
+        bload<G, VEC, KCH, 16>(o, make_rsrc(table, (uint32_t)(rows * D * 4)), (uint32_t)(row * D * 4), D, lane);
+    else
+        uload(o, table + row * D, D, lane);
+}
+
+// ALWAYS (team universes): every entity row of the positive goes to its sink, a zero row for an inactive pair, so
+// each positive fills its static contribution slots (neg negatives, head, tail) whatever its margin decisions.
+template <int NP, int G, int VEC, int KCH, bool PF = false, bool ALWAYS = false, bool SC1 = false, typename Sink,
+          typename NegFn>
 __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp)[NP], const int (&rp)[NP],
                                              const int (&tp)[NP], int neg, NegFn get_neg, const Sink (&sk)[NP],
                                              int lane) {
     using Vec = V<G, VEC, KCH>;
-    constexpr bool kFm = kUF && VEC * KCH <= 8;   // hardware sqrt / rcp (see kUF)
+    constexpr bool kFm = uni_fast(G, VEC * KCH);   // hardware sqrt / rcp (see kUF)
     const int D = (int)P.dim;
     const int p = P.p_norm;
     const bool nf = P.norm_flag != 0;
@@ -240,9 +259,9 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
     Vec hh[NP], th[NP], rh[NP];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
-        uload(hh[q], P.ent + hp[q] * D, D, lane);
-        uload(th[q], P.ent + tp[q] * D, D, lane);
-        uload(rh[q], P.rel + rp[q] * D, D, lane);
+        trow<SC1>(hh[q], P.ent, P.ent_total, hp[q], D, lane);
+        trow<SC1>(th[q], P.ent, P.ent_total, tp[q], D, lane);
+        trow<SC1>(rh[q], P.rel, P.rel_total, rp[q], D, lane);
     }
     // long wide rows (16 floats per lane over >= 16 lanes: TransE rows over 512 floats since r04): the first
     // negative's row loads with the positive's, the rest one at a time in the loop (measured r02 on C4's then
@@ -261,7 +280,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
         tail_side[q] = false;
         if (kPrefetch && neg > 0) {
             get_neg(q, 0, e[q], tail_side[q]);
-            uload(x[q], P.ent + e[q] * D, D, lane);
+            trow<SC1>(x[q], P.ent, P.ent_total, e[q], D, lane);
         }
     }
     float ps[NP], csum[NP], lsum[NP];
@@ -293,7 +312,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
 #pragma unroll
             for (int q = 0; q < NP; ++q) {
                 get_neg(q, k, e[q], tail_side[q]);
-                uload(x[q], P.ent + e[q] * D, D, lane);
+                trow<SC1>(x[q], P.ent, P.ent_total, e[q], D, lane);
             }
         }
 #pragma unroll
@@ -320,6 +339,9 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
                 }
                 sk[q].ent(e[q], x[q], D, lane);   // corrupted tail gets -g, corrupted head +g
                 PT_USTAMP(sk[0].trace, 3);
+            } else if constexpr (ALWAYS) {
+                vzero(x[q]);
+                sk[q].ent(e[q], x[q], D, lane);
             }
         }
     }
@@ -351,6 +373,9 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
             sk[q].ent(hp[q], aH[q], D, lane);
             PT_USTAMP(sk[0].trace, 6);
             sk[q].ent(tp[q], aT[q], D, lane);
+        } else if constexpr (ALWAYS) {   // (no active pair: the accumulators are zero)
+            sk[q].ent(hp[q], aH[q], D, lane);
+            sk[q].ent(tp[q], aT[q], D, lane);
         }
         loss += lsum[q];
     }
@@ -367,7 +392,7 @@ template <int G, int VEC, int KCH, typename Sink, typename NegFn>
 __device__ __forceinline__ float transh_step(const StepParams &P, int hp, int rp, int tp, int neg,
                                              NegFn get_neg, const Sink &sink, int lane) {
     using Vec = V<G, VEC, KCH>;
-    constexpr bool kFm = kUF && VEC * KCH <= 8;   // hardware sqrt / rcp (see kUF)
+    constexpr bool kFm = uni_fast(G, VEC * KCH);   // hardware sqrt / rcp (see kUF)
     const int D = (int)P.dim;
     const int p = P.p_norm;
     const bool nf = P.norm_flag != 0;
@@ -501,6 +526,70 @@ struct PreTables {
     Affine c[kPreC][2];     // LCG^(c * per * dpp), LCG^(c * rem * dpp) (rem: the last non-empty slice's size)
 };
 
+// The presampler of a universe workgroup (every `pchunk` steps): the next nb batches (TrainDataLoader.sampling()
+// calls) drawn at once into LDS, lane-parallel - batch j of the chunk is sampler call j after the chunk-start stream
+// states - then the streams advanced past them
+template <int NT>
+struct Presampler {
+    const DeviceGraph &g;
+    uint64_t *s_states;
+    const PreTables *pre;
+    FastMod fm_n, fm_e;
+    int threads, bs, neg, bern, filter, dpp, per, seq;
+    bool fastpre;
+    int32_t *s_bh, *s_br, *s_bt;
+    __device__ __forceinline__ void draw(int nb) const {
+        const int tid = threadIdx.x;
+        for (int q = tid; q < nb * bs; q += NT) {
+            const int s = q / bs, b = q - s * bs;
+            if (fastpre && !filter) {
+                // the same draws as draw_positive / draw_negative (bit-identical streams and values):
+                // table jumps, 32-bit slice arithmetic, rand_max by fastmod
+                const int id = b / per, j = b - id * per;
+                const PreTables &T = *pre;
+                const Affine m1 = T.j[j], m2 = T.c[s][bs - id * per >= per ? 0 : 1];
+                uint64_t st = m1.a * s_states[id] + m1.c;
+                st = m2.a * st + m2.c;
+                const int i = (int)fastmod(lcg_next(st), fm_n);
+                i32x4 ra, rc;
+                graph_rec(g, i, ra, rc);
+                int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
+                bh[b] = ra.x; br[b] = ra.y; bt[b] = ra.z;
+                const float prob = bern ? g.bern_prob[ra.y] : 500.f;
+                for (int k = 0; k < neg; ++k) {
+                    // coin, then the corruption (Corrupt.h:18-25, 68-74: skips the passed entity)
+                    const bool tail = (float)(lcg_next(st) % 1000ULL) < prob;
+                    const int tmp = (int)fastmod(lcg_next(st), fm_e);
+                    const int skip = tail ? ra.x : ra.z;
+                    const int e = tmp < skip ? tmp : tmp + 1;
+                    const int o = (k + 1) * bs + b;
+                    bh[o] = tail ? ra.x : e;
+                    bt[o] = tail ? e : ra.z;
+                    br[o] = ra.y;
+                }
+                continue;
+            }
+            const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp, s);
+            int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
+            bh[b] = (int32_t)pd.h; br[b] = (int32_t)pd.r; bt[b] = (int32_t)pd.t;
+            for (int k = 0; k < neg; ++k) {
+                int side;
+                const int e = (int)draw_negative(g, pd, k, bern, filter, &side);
+                const int o = (k + 1) * bs + b;
+                bh[o] = (int32_t)(side ? pd.h : e);
+                bt[o] = (int32_t)(side ? e : pd.t);
+                br[o] = (int32_t)pd.r;
+            }
+        }
+        __syncthreads();
+        if (tid < threads) {   // the chunk consumed nb calls of the streams
+            int len = bs - tid * per;
+            len = len < 0 ? 0 : (len > per ? per : len);
+            s_states[tid] = lcg_jump(s_states[tid], (uint64_t)len * (uint64_t)dpp * (uint64_t)nb);
+        }
+    }
+};
+
 // Dynamic LDS layout (int32 units; the host sizes it for the largest universe of the launch):
 //   list[list_cap] | flags[E + 2R] or [2R] | head[E] + next[ccap] (contrib) |
 //   batch h, r, t [3][pchunk * bs * (1 + neg)] (pchunk > 0) | rel (+ norm) gradient rows [R][D] floats
@@ -611,8 +700,10 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
         sink.gnorm = s_grel + R * D;
     }
     const DeviceGraph &g = U.g;
+    const Presampler<NT> presample{g, s_states, S.pre, fm_n, fm_e, threads, bs, neg, bern, filter, dpp, per, seq,
+                                   fastpre, s_bh, s_br, s_bt};
     float epoch_loss = 0.f;
-    uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0;
+    uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0, rows_b = 0;
     const uint64_t w_start = U.prof ? wall_clock64() : 0;   // (100 MHz wall clock: the set's schedule)
     __syncthreads();
     for (int epoch = 0; epoch < epochs; ++epoch) {
@@ -621,58 +712,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // tuning build: stamps of step 5 of epoch 1 (phase A rounds [8 + 8r, +8), phase B rounds [48 + r])
             uint64_t *const tr = U.prof && epoch == 1 && step == 5 && grp == 0 ? U.prof : nullptr;
             const int cs = pchunk > 0 ? step % pchunk : 0;
-            if (presampled && cs == 0) {
-                // the next min(pchunk, left) batches drawn at once into LDS: batch j of the chunk is
-                // sampler call j after the chunk-start stream states
-                const int nb = nbatches - step < pchunk ? nbatches - step : pchunk;
-                for (int q = tid; q < nb * bs; q += NT) {
-                    const int s = q / bs, b = q - s * bs;
-                    if (fastpre && !filter) {
-                        // the same draws as draw_positive / draw_negative (bit-identical streams and values):
-                        // table jumps, 32-bit slice arithmetic, rand_max by fastmod
-                        const int id = b / per, j = b - id * per;
-                        const PreTables &T = *S.pre;
-                        const Affine m1 = T.j[j], m2 = T.c[s][bs - id * per >= per ? 0 : 1];
-                        uint64_t st = m1.a * s_states[id] + m1.c;
-                        st = m2.a * st + m2.c;
-                        const int i = (int)fastmod(lcg_next(st), fm_n);
-                        i32x4 ra, rc;
-                        graph_rec(g, i, ra, rc);
-                        int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
-                        bh[b] = ra.x; br[b] = ra.y; bt[b] = ra.z;
-                        const float prob = bern ? g.bern_prob[ra.y] : 500.f;
-                        for (int k = 0; k < neg; ++k) {
-                            // coin, then the corruption (Corrupt.h:18-25, 68-74: skips the passed entity)
-                            const bool tail = (float)(lcg_next(st) % 1000ULL) < prob;
-                            const int tmp = (int)fastmod(lcg_next(st), fm_e);
-                            const int skip = tail ? ra.x : ra.z;
-                            const int e = tmp < skip ? tmp : tmp + 1;
-                            const int o = (k + 1) * bs + b;
-                            bh[o] = tail ? ra.x : e;
-                            bt[o] = tail ? e : ra.z;
-                            br[o] = ra.y;
-                        }
-                        continue;
-                    }
-                    const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp, s);
-                    int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
-                    bh[b] = (int32_t)pd.h; br[b] = (int32_t)pd.r; bt[b] = (int32_t)pd.t;
-                    for (int k = 0; k < neg; ++k) {
-                        int side;
-                        const int e = (int)draw_negative(g, pd, k, bern, filter, &side);
-                        const int o = (k + 1) * bs + b;
-                        bh[o] = (int32_t)(side ? pd.h : e);
-                        bt[o] = (int32_t)(side ? e : pd.t);
-                        br[o] = (int32_t)pd.r;
-                    }
-                }
-                __syncthreads();
-                if (tid < threads) {   // the chunk consumed nb calls of the streams
-                    int len = bs - tid * per;
-                    len = len < 0 ? 0 : (len > per ? per : len);
-                    s_states[tid] = lcg_jump(s_states[tid], (uint64_t)len * (uint64_t)dpp * (uint64_t)nb);
-                }
-            }
+            if (presampled && cs == 0) presample.draw(nbatches - step < pchunk ? nbatches - step : pchunk);
             if (tid == 0) {
                 s_count = 0;
                 s_ccount = 0;
@@ -754,6 +794,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // ---- phase B: row updates of the touched rows, RB rows per lane group at a time (all their
             // loads in flight together: the pass is a chain of dependent memory round trips otherwise)
             const int n = s_count;
+            if (U.prof) rows_b += (uint64_t)n;
             // (TransH: 2 rows of 8 floats per lane in flight spill its step's registers; TransE keeps 2)
             // (1024-thread workgroups: half the rows per lane group, twice the lane groups; 128 VGPRs per lane)
             // (r04: two rows per lane group in the hot kernels' 5-6-float shapes spill 28-68 B per lane, phase B
@@ -761,7 +802,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // (r04: the hot kernels' phase B on lane groups of half the width - twice the floats per lane, twice the
             // rows per round: phase B of C3's D = 68 universe 4.3k -> 14.2k, of C4's longest 23k -> 89k cycles per step)
             constexpr int RB = VEC * KCH >= 16 ? 1 : (VEC * KCH > 4 ? (MODEL == 1 || NT > 512 ? 1 : 2) : (NT > 512 ? 2 : 4));
-            constexpr bool kFastUpd = kUF && VEC * KCH <= 8;
+            constexpr bool kFastUpd = uni_fast(G, VEC * KCH);
             // (guards, not breaks, inside the unrolled loops: the row arrays must stay in registers)
             PT_USTAMP(tr, 47);
             for (int i0 = grp * RB; i0 < n; i0 += GPB * RB) {
@@ -872,6 +913,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
         U.prof[6] = (uint64_t)E;
         // the universe's start on the 100 MHz wall clock (low 32 bits) and its duration in those ticks
         U.prof[7] = (w_start << 32) | ((wall_clock64() - w_start) & 0xffffffffull);
+        U.prof[62] = rows_b;   // rows updated in phase B, summed over the steps (a slot the tuning stamps leave free)
     }
     if (tid < threads) U.states[tid] = s_states[tid];
 }

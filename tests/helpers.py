@@ -260,6 +260,16 @@ def assert_step_close(ours, want, atol, mask=None, max_frac=1e-2, what="", befor
                "max_err": float(err[keep].max()) if keep.any() else 0.0,
                "max_allowed": float(tol[keep].max()) if keep.any() else 0.0,
                "compared": int(keep.sum())}
+        if keep.any():   # the largest error: where, and what its (uncapped) bound is made of
+            m = int(np.argmax(np.where(keep, err, -np.inf)))
+            r_, c_ = np.unravel_index(m, err.shape)
+            kb = np.broadcast_to(k, err.shape)
+            rec.update(max_at=[int(r_), int(c_)], max_k=float(kb[r_, c_]), max_unit=float(unit[r_, c_]),
+                       max_uncapped=float(atol + KAPPA_C * np.sqrt(kb[r_, c_]) * unit[r_, c_] + 4.0 * EPS32 *
+                                          delta[r_, c_]),
+                       max_g=float(np.asarray(gm["g"])[r_, c_]), max_abs=float(np.asarray(gm["abs"])[r_, c_]),
+                       max_delta=float(delta[r_, c_]), max_ours=float(ours[r_, c_]), max_want=float(want[r_, c_]),
+                       max_acc=None if acc_before is None else float(np.asarray(acc_before)[r_, c_]))
         if sel.any():   # the worst element: its error, its allowed bound and what the bound is made of
             w = np.argmax(np.where(sel, over, -np.inf))
             rec.update(worst_err=float(err.flat[w]), worst_allowed=float(tol.flat[w]), worst_k=float(k.flat[w] if

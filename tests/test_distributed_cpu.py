@@ -373,3 +373,84 @@ def test_lp_pairs_native_rejects_bad_layouts():
     rc = L.pt_lp_pairs(1, off.ctypes.data, good.ctypes.data, off.ctypes.data, rel.ctypes.data, 1, k.ctypes.data,
                        k.ctypes.data, k.ctypes.data, out.ctypes.data, 0, n.ctypes.data)   # no room for the row
     assert rc == 1
+
+
+def _synthetic_universe(uid, E_glob=40, R_glob=4, D=5):
+    """A universe of id uid (a pure function of it, like seed0 + k): local -> global maps and tables."""
+    rng = np.random.default_rng(100 + uid)
+    E = int(rng.integers(3, 12))
+    R = int(rng.integers(1, R_glob + 1))
+    em = np.sort(rng.choice(E_glob, E, replace=False)).astype(np.int64)
+    rm = np.sort(rng.choice(R_glob, R, replace=False)).astype(np.int64)
+    nv = torch.from_numpy(rng.standard_normal((R, D)).astype(np.float32)) if uid % 2 else None
+    return {"ent": torch.from_numpy(rng.standard_normal((E, D)).astype(np.float32)),
+            "rel": torch.from_numpy(rng.standard_normal((R, D)).astype(np.float32)), "nv": nv, "em": em, "rm": rm,
+            "dim": D}
+
+
+def _toy_rows(unis, keys, E_glob=40):
+    """Key rows as the LP fold fills them: per (side, anchor, rel) key the MIN over every universe holding anchor and
+    rel of a score of each of its entities (here |anchor + rel - e|_1 over the universe's rows)."""
+    rows = torch.full((len(keys), E_glob), float("inf"))
+    for u in unis:
+        g2l = {int(g): i for i, g in enumerate(u["em"])}
+        r2l = {int(g): i for i, g in enumerate(u["rm"])}
+        for k, (side, anchor, r) in enumerate(keys):
+            if anchor in g2l and r in r2l:
+                a = u["ent"][g2l[anchor]] + (u["rel"][r2l[r]] if side else -u["rel"][r2l[r]])
+                s = (a[None, :] - u["ent"]).abs().sum(1)
+                idx = torch.from_numpy(u["em"])
+                rows[k, idx] = torch.minimum(rows[k, idx], s)
+    return rows
+
+
+def _toy_ranks(rows, truths):
+    val = rows.gather(1, truths[:, None])
+    return [((rows < val).sum(1)).numpy().astype(np.int64)]
+
+
+def _gather_worker(rank, world, port, n_univ, out_dir):
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = [_synthetic_universe(u) for u in range(n_univ) if u % world == rank]
+        got = bench.gather_universes(mine, world)
+        rng = np.random.default_rng(7)
+        keys = [(int(rng.integers(0, 2)), int(rng.integers(0, 40)), int(rng.integers(0, 4))) for _ in range(25)]
+        truths = torch.from_numpy(rng.integers(0, 40, 25))
+        rows = _toy_rows(mine, keys)
+        min_combine([rows])
+        d_dist = bench.rank_digest(_toy_ranks(rows, truths))
+        d_n1 = bench.rank_digest(_toy_ranks(_toy_rows(got, keys), truths))
+        np.save(os.path.join(out_dir, "order%d.npy" % rank),
+                np.array([int(u["em"][0]) * 1000 + u["ent"].shape[0] for u in got]))
+        with open(os.path.join(out_dir, "digest%d.txt" % rank), "w") as f:
+            f.write("%s %s %d" % (d_dist, d_n1, len(got)))
+        for u in got:   # every gathered universe equals its source
+            src = [v for v in (_synthetic_universe(k) for k in range(n_univ)) if np.array_equal(v["em"], u["em"])
+                   and np.array_equal(v["rm"], u["rm"])]
+            assert len(src) == 1
+            for k in ("ent", "rel", "nv"):
+                assert (src[0][k] is None) == (u[k] is None)
+                if u[k] is not None:
+                    assert torch.equal(src[0][k], u[k])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pu_c4_lp_gather_and_digest(world, tmp_path):
+    """bench.py's pu_c4_lp check (N > 1): every rank's universes gathered to every rank (gather_universes, padded
+    all_gathers of sizes, tables and remaps), and the ranks from the MIN-combined rows of each rank's own universes
+    equal, digest for digest, the ranks an N = 1 recomputation over the gathered universes gives."""
+    n_univ = 7
+    mp.spawn(_gather_worker, args=(world, _free_port(), n_univ, str(tmp_path)), nprocs=world, join=True)
+    digests = [open(os.path.join(tmp_path, "digest%d.txt" % r)).read().split() for r in range(world)]
+    for d_dist, d_n1, n in digests:
+        assert d_dist == d_n1 and int(n) == n_univ
+    assert len({d[0] for d in digests}) == 1
+    orders = [np.load(os.path.join(tmp_path, "order%d.npy" % r)) for r in range(world)]
+    for o in orders[1:]:
+        np.testing.assert_array_equal(o, orders[0])

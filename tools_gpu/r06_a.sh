@@ -13,3 +13,5 @@ PT_UNI_PROF=1 timeout -k 10 400 python bench.py --workload c4 --steps 2 --warmup
   --no-dropin --deterministic-timing 0 > gpurun_out/${T}_c4.log 2>&1 || exit $?
 PT_UNI_PROF=1 timeout -k 10 400 python bench.py --workload c5 --steps 2 --warmup 1 --place-world 8 --no-cpu-baseline \
   --no-dropin --deterministic-timing 0 > gpurun_out/${T}_c5.log 2>&1 || exit $?
+PT_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline \
+  --deterministic-timing 0 --no-ref-scale > gpurun_out/${T}_dist2.log 2>&1 || exit $?
