@@ -319,10 +319,22 @@ def _xavier(rng, rows, dim):
     return rng.uniform(-b, b, (rows, dim)).astype(np.float32)
 
 
-def chain_profile(L, us, reset, idx, time_set, mid, name, prof_on):
+def team_info(row):
+    """A profiled universe's team (pt_universe_set_profile words 60-61; None: one workgroup)."""
+    w = int(row[60]) >> 32
+    if w <= 1:
+        return None
+    steps = max(float(row[3]), 1.0)
+    return {"width": w, "one_xcd": bool(int(row[60]) & 1), "barrier_cycles_per_step": float(row[61]) / steps}
+
+
+def chain_profile(L, us, reset, idx, time_set, mid, name, prof_on, rel_of=None):
     """One extra (untimed) training of the set with the per-universe cycle counters on: the longest universe's
     measured cycles per step, its phases and phase-B rows, against chain_floor. VALU issue joins the floor when
-    profiles/pmc_<name>_chain.json holds rocprofv3 counters of that universe alone on this library build."""
+    profiles/pmc_<name>_chain.json holds rocprofv3 counters of that universe alone on this library build.
+    Phase-B rows: a team universe counts member 0's (profile word 62); a one-workgroup universe's are the expected
+    distinct rows of a step - bs * (2 + neg) entity draws over E rows and bs relation draws over R (rel_of[(bs, D,
+    E)]), E (1 - exp(-n / E)) each (uniform draws: an estimate; the kernel keeps no counter)."""
     from openke import _native
     if not prof_on:
         _native.check(L.pt_universe_set_profiling(us, 1))
@@ -336,21 +348,28 @@ def chain_profile(L, us, reset, idx, time_set, mid, name, prof_on):
     i = int(np.argmax(span))
     steps = max(pr[i, 3], 1.0)
     bs, D, E = int(pr[i, 4]), int(pr[i, 5]), int(pr[i, 6])
-    rows = pr[i, 62] / steps
+    R = (rel_of or {}).get((bs, D, E), 0)
+    rows_estimated = pr[i, 62] == 0
+    if rows_estimated:
+        rows = E * (1.0 - np.exp(-bs * 3.0 / max(E, 1))) + (R * (1.0 - np.exp(-bs / R)) if R else 0.0)
+    else:
+        rows = pr[i, 62] / steps
     pmc, _ = load_pmc("%s_chain" % name)
     valu = None
     if pmc and pmc.get("longest") == {"bs": bs, "dim": D, "ent": E, "steps": int(steps)}:
         valu = pmc["valu_per_step"]
     fl = chain_floor(mid, D, bs, rows, valu)
     achieved = span[i] / steps
+    team = team_info(pr[i])
     return {"achieved": achieved, "floor": fl["floor_cycles"], "frac": fl["floor_cycles"] / achieved,
             "unit": "cycles/step", "longest_universe": {"bs": bs, "dim": D, "ent": E, "steps": int(steps),
-                                                        "rows_per_step": rows, "cycles": span[i],
+                                                        "rows_per_step": rows, "rows_estimated": bool(rows_estimated),
+                                                        "cycles": span[i],
                                                         "ms_at_2.4GHz": span[i] / 2.4e6,
                                                         "cycles_per_step": {"presample": pr[i, 0] / steps,
                                                                             "phase_a": pr[i, 1] / steps,
                                                                             "phase_b": pr[i, 2] / steps}},
-            "floor_model": fl, "valu_counted": valu is not None}
+            "floor_model": fl, "valu_counted": valu is not None, "team": team}
 
 
 def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check_lp=False):
@@ -505,7 +524,9 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
     uset, reset = make_set(every)
     el = time_set(uset, reset, every, args.c3_steps, args.c3_warmup)
     class_launches = launch_times(uset)
-    chain = chain_profile(L, uset, reset, every, time_set, mid, name, prof_on) if every else None
+    rel_of = {(int(jobs[i].batch_size), int(jobs[i].dim), int(unis[i]["ent"].shape[0])): int(unis[i]["rel"].shape[0])
+              for i in every}
+    chain = chain_profile(L, uset, reset, every, time_set, mid, name, prof_on, rel_of) if every else None
     tot = torch.tensor([el, float(slots_step), float(bytes_step)], dtype=torch.float64, device=dev)
     if ws > 1:
         import torch.distributed as dist
@@ -557,7 +578,7 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
         # as Parallel_Universe_Config places a wave) trained alone, from the initial state
         pw = args.place_world
         po = place_universes({k: universe_cost(all_draws[k][3], all_draws[k][0], all_dims[k]) for k in own}, pw)
-        shares, spans = [], []
+        shares, spans, teams_r = [], [], []
         for r in range(pw):
             idx = [i for i, k in enumerate(own) if po[k] == r]
             us, rs = make_set(idx)
@@ -566,12 +587,20 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
             shares.append(time_set(us, rs, idx, args.c3_steps, 1) / args.c3_steps)
             pr = np.zeros(64 * max(len(idx), 1), dtype=np.uint64)
             _native.check(L.pt_universe_set_profile(us, pr.ctypes.data))
-            spans.append(float(pr.reshape(-1, 64)[:, :3].astype(np.float64).sum(axis=1).max()) if idx else 0.0)
+            prr = pr.reshape(-1, 64)
+            span_r = prr[:, :3].astype(np.float64).sum(axis=1)
+            spans.append(float(span_r.max()) if idx else 0.0)
+            if idx:
+                il = int(np.argmax(span_r))
+                st = max(float(prr[il, 3]), 1.0)
+                teams_r.append({"team": team_info(prr[il].astype(np.float64)), "cycles_per_step": {
+                    "presample": float(prr[il, 0]) / st, "phase_a": float(prr[il, 1]) / st,
+                    "phase_b": float(prr[il, 2]) / st}})
             _native.check(L.pt_universe_set_free(us))
         placement = {"world": pw, "universes_per_rank": [sum(1 for k in own if po[k] == r) for r in range(pw)],
                      "share_s": shares, "max_share_s": max(shares), "rank0_share_s": shares[0],
                      "full_set_s": el / args.c3_steps, "max_share_over_full": max(shares) / (el / args.c3_steps),
-                     "longest_universe_cycles_per_share": spans,
+                     "longest_universe_cycles_per_share": spans, "longest_universe_per_share": teams_r,
                      "note": "one GPU: rank r's LPT share of a %d-way placement trained alone (the N = %d per-rank "
                              "critical path); longest-universe spans in shader-clock cycles" % (pw, pw)}
     for i in range(len(own)):
@@ -886,6 +915,9 @@ def main():
     ap.add_argument("--slot-scale", type=int, default=-1,
                     help="C2 / C1: 1 = slot-scale mode (per-slot records + positive base rows instead of contribution "
                          "rows; pt_trainer_set_slot_scale), 0 = contribution rows, -1 = the library's default")
+    ap.add_argument("--team-width", type=int, default=0,
+                    help="universe workloads: widest team per universe when a GPU holds fewer universes than CUs "
+                         "(pt_set_universe_team_width: 1, 2 or 4; 0 = the library default)")
     ap.add_argument("--longest-only", action="store_true",
                     help="universe workloads: train only the set's longest universe (its chain alone)")
     ap.add_argument("--no-dropin", action="store_true",
@@ -917,6 +949,9 @@ def main():
         return
 
     ws, rank, local = dist_setup()
+    if args.team_width:
+        from openke import _native
+        _native.check(_native.lib().pt_set_universe_team_width(args.team_width))
     if args.workload in PU_WORKLOADS:
         dev = torch.device("cuda", torch.cuda.current_device())
         args.c3_steps, args.c3_warmup = args.steps, args.warmup

@@ -1242,6 +1242,8 @@ struct pt_universe_set {
     uint32_t *d_team_sync = nullptr;      // team universes' arrival counters (inside the arena, zeroed per call)
     int64_t n_team_sync = 0;
     pt::UniverseLaunch team_cfg;          // the team launches' LDS plan
+    pt::TeamDev *d_teams = nullptr;       // [host]: team universes' exchange state (inside the team arena)
+    std::vector<int> host_team_w;         // [host]: team width (1: a workgroup of its own)
     std::vector<Group> groups;            // runs of d_us with one shape class (one kernel launch each)
     std::vector<hipStream_t> streams;     // PT_UNI_STREAMS=0 only: per-set side streams (else the process pool's)
     std::vector<hipEvent_t> events;
@@ -1393,13 +1395,14 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
                         jobs[i].epochs * jobs[i].nbatches > 0;
             // the team launch's LDS with one presampled batch, over its universes' largest sizes (the launch gets as
             // many batches as then fit)
-            int64_t m_rel = 0, m_ent = 0, m_slots = 0, m_seq = 0, m_dim = 0;
+            int64_t m_rel = 0, m_ent = 0, m_slots = 0, m_seq = 0, m_rstep = 0, m_dim = 0;
             auto fits_with = [&](int64_t i) {
                 const pt::Graph &g = reinterpret_cast<const pt_graph *>(jobs[i].graph)->g;
                 const int64_t b = jobs[i].batch_size;
                 return pt::universe_team_lds_bytes(cap, std::max(m_rel, g.rel_total), std::max(m_ent, g.ent_total),
                                                    std::max(m_slots, b * (2 + jobs[i].neg)),
                                                    1, std::max(m_seq, b * (1 + jobs[i].neg)),
+                                                   std::max(m_rstep, std::min(b, g.rel_total)),
                                                    std::max(m_dim, jobs[i].dim)) <= lds_budget;
             };
             int64_t spare = (int64_t)cus_t - n;
@@ -1421,6 +1424,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
                     m_ent = std::max(m_ent, g.ent_total);
                     m_slots = std::max(m_slots, jobs[best].batch_size * (2 + jobs[best].neg));
                     m_seq = std::max(m_seq, jobs[best].batch_size * (1 + jobs[best].neg));
+                    m_rstep = std::max(m_rstep, std::min(jobs[best].batch_size, g.rel_total));
                     m_dim = std::max(m_dim, jobs[best].dim);
                 }
                 team_w[best] *= 2;
@@ -1568,13 +1572,10 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         U.threads = J.threads; U.bs = J.batch_size; U.nbatches = J.nbatches; U.epochs = J.epochs; U.dim = J.dim;
         U.lr = J.lr; U.margin = J.margin;
         U.shape = pt::universe_shape_id(J.dim, model);
-        U.team_w = team_w.empty() ? 1 : team_w[(size_t)i];
-        U.team_part = nullptr;
-        U.team_sync = nullptr;
-        U.team_err = nullptr;
         if (set->host_of_job.empty()) set->host_of_job.assign((size_t)n, -1);
         set->host_of_job[(size_t)i] = (int64_t)set->host.size();
         set->host.push_back(U);
+        set->host_team_w.push_back(team_w.empty() ? 1 : team_w[(size_t)i]);
         set->host_loss_off.push_back(loss_of[i]);
         max_bs = std::max(max_bs, J.batch_size);
         max_relg = std::max(max_relg, g.rel_total * J.dim);
@@ -1629,7 +1630,12 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     // members on blocks of one residue mod 8 (the dispatcher's round-robin over the XCDs: one L2 for the team -
     // performance only, the protocol does not depend on it)
     {
-        int64_t t_rel = 0, t_ent = 0, t_slots = 0, t_seq = 0, t_dim = 0, t_nb = 0, part_b = 0, n_team = 0, map_b = 0;
+        int64_t t_rel = 0, t_ent = 0, t_slots = 0, t_seq = 0, t_nb = 0, t_rstep = 0, t_dim = 0, part_b = 0, n_team = 0,
+                map_b = 0;
+        // a team universe's partials: [W][R][D] relation rows, [W][epochs] losses, [W] XCD ids
+        auto part_bytes = [&](const pt::UniverseDev &U, int w) {
+            return al(4 * (w * U.g.rel_total * U.dim + w * U.epochs + w));
+        };
         std::vector<int64_t> grid_of(set->groups.size(), 0);
         std::vector<std::vector<int32_t>> maps(set->groups.size());
         for (size_t k = 0; k < set->groups.size(); ++k) {
@@ -1638,14 +1644,16 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
             std::vector<std::pair<int, int64_t>> teams;   // (members, index from off)
             for (int64_t q = gr.off; q < gr.off + gr.n; ++q) {
                 const pt::UniverseDev &U = set->host[(size_t)q];
-                teams.push_back({U.team_w, q - gr.off});
+                const int w = set->host_team_w[(size_t)q];
+                teams.push_back({w, q - gr.off});
                 t_rel = std::max(t_rel, U.g.rel_total);
                 t_ent = std::max(t_ent, U.g.ent_total);
                 t_slots = std::max(t_slots, U.bs * (2 + set->neg));
                 t_seq = std::max(t_seq, U.bs * (1 + set->neg));
-                t_dim = std::max(t_dim, U.dim);
                 t_nb = std::max(t_nb, U.nbatches);
-                part_b += al(4 * (U.team_w * U.g.rel_total * U.dim + U.team_w * U.epochs));
+                t_rstep = std::max(t_rstep, std::min(U.bs, U.g.rel_total));
+                t_dim = std::max(t_dim, U.dim);
+                part_b += part_bytes(U, w);
                 ++n_team;
             }
             std::stable_sort(teams.begin(), teams.end(), [](const std::pair<int, int64_t> &a,
@@ -1672,31 +1680,36 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
         if (n_team > 0) {
             auto &T = set->team_cfg;
             T = C;
-            const int64_t fixed = pt::universe_team_lds_bytes(C.list_cap, t_rel, t_ent, t_slots, 0, t_seq, t_dim);
+            const int64_t fixed = pt::universe_team_lds_bytes(C.list_cap, t_rel, t_ent, t_slots, 0, t_seq, t_rstep, t_dim);
             T.pchunk = std::min<int64_t>(t_nb, (lds_budget - fixed) / std::max<int64_t>(12 * t_seq, 1));
             PT_CHECK(T.pchunk >= 1, PT_EINVAL, "team universes: LDS plan does not fit");
-            T.lds_bytes = pt::universe_team_lds_bytes(C.list_cap, t_rel, t_ent, t_slots, T.pchunk, t_seq, t_dim);
+            T.lds_bytes = pt::universe_team_lds_bytes(C.list_cap, t_rel, t_ent, t_slots, T.pchunk, t_seq, t_rstep, t_dim);
             const int64_t sync_b = al(4 * (n_team + 1));   // + the error word
-            PT_HIP(hipMalloc(&set->team_arena, (size_t)(part_b + sync_b + map_b)));
+            const int64_t teams_b = al((int64_t)sizeof(pt::TeamDev) * (int64_t)set->host.size());
+            PT_HIP(hipMalloc(&set->team_arena, (size_t)(part_b + sync_b + map_b + teams_b)));
             char *tb = (char *)set->team_arena;
             set->d_team_sync = (uint32_t *)(tb + part_b);
             set->n_team_sync = n_team;
             int64_t po = 0, si = 0, mo = part_b + sync_b;
+            std::vector<pt::TeamDev> th(set->host.size(), pt::TeamDev{nullptr, nullptr, nullptr, 1});
             for (size_t k = 0; k < set->groups.size(); ++k) {
                 auto &gr = set->groups[k];
                 if (gr.shape < pt::kUniTeamBase) continue;
                 for (int64_t q = gr.off; q < gr.off + gr.n; ++q) {
-                    pt::UniverseDev &U = set->host[(size_t)q];
-                    U.team_part = (float *)(tb + po);
-                    po += al(4 * (U.team_w * U.g.rel_total * U.dim + U.team_w * U.epochs));
-                    U.team_sync = set->d_team_sync + si++;
-                    U.team_err = set->d_team_sync + n_team;
+                    pt::TeamDev &T = th[(size_t)q];
+                    T.w = set->host_team_w[(size_t)q];
+                    T.part = (float *)(tb + po);
+                    po += part_bytes(set->host[(size_t)q], T.w);
+                    T.sync = set->d_team_sync + si++;
+                    T.err = set->d_team_sync + n_team;
                 }
                 gr.d_map = (int32_t *)(tb + mo);
                 gr.grid = grid_of[k];
                 PT_HIP(hipMemcpy(gr.d_map, maps[k].data(), 4 * maps[k].size(), hipMemcpyHostToDevice));
                 mo += al(4 * (int64_t)maps[k].size());
             }
+            set->d_teams = (pt::TeamDev *)(tb + mo);
+            PT_HIP(hipMemcpy(set->d_teams, th.data(), sizeof(pt::TeamDev) * th.size(), hipMemcpyHostToDevice));
         }
     }
     *out = set.release();
@@ -1799,7 +1812,7 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
             return v && atoi(v) != 0;
         }();
         if (gr.shape >= pt::kUniTeamBase) {
-            const hipError_t e = pt::launch_universes_team(set->d_us + gr.off, gr.d_map, gr.grid,
+            const hipError_t e = pt::launch_universes_team(set->d_us + gr.off, set->d_teams + gr.off, gr.d_map, gr.grid,
                                                            gr.shape - pt::kUniTeamBase, set->p_norm, set->norm_flag,
                                                            set->opt, set->neg, (int)set->bern, (int)set->filter,
                                                            set->team_cfg, q);
@@ -1903,7 +1916,8 @@ extern "C" int pt_universe_set_profiling(pt_universe_set *set, int32_t on) {
 }
 
 // diagnostics: per universe (set order) 64 words: cycles in presampling / phase A / phase B, steps, batch size,
-// dim, entities, start / duration (100 MHz wall clock) of the last train call with profiling on; word 62 the rows
+// dim, entities, start / duration (100 MHz wall clock) of the last train call with profiling on; team universes: word
+// 60 (team width << 32 | one XCD), word 61 the cycles in team barriers; word 62 the rows
 // updated in phase B summed over the steps; the other words 8-63 phase stamps of one step (tuning build)
 extern "C" int pt_universe_set_profile(pt_universe_set *set, uint64_t *out) {
     PT_CHECK(set && out, PT_EINVAL, "null argument");

@@ -24,10 +24,16 @@ struct UniverseDev {
     int64_t threads, bs, nbatches, epochs, dim;
     float lr, margin;
     int32_t shape;                                  // universe_shape_id(dim)
-    int32_t team_w;                                 // workgroups training it (universes_team.h), 1: one
-    float *team_part;                               // team: [team_w][rel][dim] relation partials, [team_w][epochs] losses
-    uint32_t *team_sync;                            // team: arrival counter (zeroed before each launch)
-    uint32_t *team_err;                             // team: the set's error word (a bounded poll ran out)
+};
+
+// A team universe's exchange state (universes_team.h), beside its UniverseDev (kept apart: the class kernels hold
+// a register copy of their descriptor, whose size their SGPR spills follow)
+struct TeamDev {
+    float *part;                                    // [w][rel][dim] relation partials, [w][epochs] loss partials,
+                                                    // [w] the members' XCD ids
+    uint32_t *sync;                                 // arrival counter (zeroed before each launch)
+    uint32_t *err;                                  // the set's error word (a bounded poll ran out)
+    int32_t w;                                      // members
 };
 
 // workgroup size of each (model, shape class) kernel. TransE's narrow classes (<= 8 floats per lane) run 1,024
@@ -88,10 +94,10 @@ int universe_shape_class(int shape);
 // its launch, and the launch over `grid` workgroups (map: [grid][2] universe index into d_us, member or -1)
 bool universe_team_shape(int shape, int model);
 int64_t universe_team_lds_bytes(int64_t list_cap, int64_t rel, int64_t ent, int64_t slots, int64_t pchunk,
-                                int64_t seq, int64_t dim);
-hipError_t launch_universes_team(const UniverseDev *d_us, const int32_t *d_map, int64_t grid, int shape, int p_norm,
-                                 int norm_flag, int opt, int64_t neg, int bern, int filter, const UniverseLaunch &cfg,
-                                 hipStream_t st);
+                                int64_t seq, int64_t rel_step, int64_t dim);
+hipError_t launch_universes_team(const UniverseDev *d_us, const TeamDev *d_teams, const int32_t *d_map, int64_t grid,
+                                 int shape, int p_norm, int norm_flag, int opt, int64_t neg, int bern, int filter,
+                                 const UniverseLaunch &cfg, hipStream_t st);
 int universe_shape_groups(int shape, int model);
 int universe_shape_row_slots(int shape);
 

@@ -75,6 +75,10 @@ constexpr bool kUF = true;
 #ifndef PT_UNI_FAST_WIDE
 #define PT_UNI_FAST_WIDE 1
 #endif
+// PT_UNI_LIST_BATCH (measurement builds): the contribution rows a plan-2 relation row's phase-B walk keeps in flight
+#ifndef PT_UNI_LIST_BATCH
+#define PT_UNI_LIST_BATCH 4
+#endif
 constexpr bool uni_fast(int G, int floats) { return kUF && floats <= 8 && (PT_UNI_FAST_WIDE || G < 32); }
 
 // backward of F.normalize (vnormalize_bwd) without a branch on the norm: the rows of a wave's lane groups
@@ -162,6 +166,41 @@ __device__ __forceinline__ void ustore(const V<G, VEC, KCH> &o, float *row_, int
     }
 }
 
+// Adds the contribution rows of an LDS-linked list (slot c, next[c], ...) to gs, in list order. BATCH > 1: the next
+// BATCH slot ids are read down the LDS chain first and their rows loaded together - one load latency per BATCH rows
+// instead of one per row (a relation row of a plan-2 universe - C4's 121 relations, C5's TransH rows - collects tens
+// of contributions per step, walked one dependent load at a time before round 6). load(Vec &, slot).
+template <int BATCH, int G, int VEC, int KCH, typename Load>
+__device__ __forceinline__ void list_sum(V<G, VEC, KCH> &gs, int32_t c, const int32_t *next, Load load) {
+    using Vec = V<G, VEC, KCH>;
+    if constexpr (BATCH <= 1) {
+        for (; c >= 0; c = next[c]) {
+            Vec y;
+            load(y, c);
+#pragma unroll
+            for (int j = 0; j < Vec::N; ++j) gs.x[j] += y.x[j];
+        }
+    } else {
+        while (c >= 0) {
+            int32_t cc[BATCH];
+            cc[0] = c;
+#pragma unroll
+            for (int k = 1; k < BATCH; ++k) cc[k] = cc[k - 1] >= 0 ? next[cc[k - 1]] : -1;
+            Vec y[BATCH];
+#pragma unroll
+            for (int k = 0; k < BATCH; ++k)
+                if (cc[k] >= 0) load(y[k], cc[k]);
+#pragma unroll
+            for (int k = 0; k < BATCH; ++k)
+                if (cc[k] >= 0) {
+#pragma unroll
+                    for (int j = 0; j < Vec::N; ++j) gs.x[j] += y[k].x[j];
+                }
+            c = cc[BATCH - 1] >= 0 ? next[cc[BATCH - 1]] : -1;
+        }
+    }
+}
+
 // Gradient sink of one universe.
 //   contrib != null: entity rows go to contribution slots (plain stores) linked per row in LDS
 //   (head[row] -> c -> next[c] -> ... -> -1); otherwise float atomics into gent.
@@ -243,8 +282,8 @@ __device__ __forceinline__ void trow(V<G, VEC, KCH> &o, const float *table, int6
         uload(o, table + row * D, D, lane);
 }
 
-// ALWAYS (team universes): every entity row of the positive goes to its sink, a zero row for an inactive pair, so
-// each positive fills its static contribution slots (neg negatives, head, tail) whatever its margin decisions.
+// ALWAYS (team universes): every row of the positive goes to its sink, a zero row for an inactive pair, so each
+// positive fills its static contribution slots (neg negatives, relation, head, tail) whatever its margin decisions.
 template <int NP, int G, int VEC, int KCH, bool PF = false, bool ALWAYS = false, bool SC1 = false, typename Sink,
           typename NegFn>
 __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp)[NP], const int (&rp)[NP],
@@ -374,6 +413,7 @@ __device__ __forceinline__ float transe_step(const StepParams &P, const int (&hp
             PT_USTAMP(sk[0].trace, 6);
             sk[q].ent(tp[q], aT[q], D, lane);
         } else if constexpr (ALWAYS) {   // (no active pair: the accumulators are zero)
+            sk[q].rel(rp[q], aR, D, lane);
             sk[q].ent(hp[q], aH[q], D, lane);
             sk[q].ent(tp[q], aT[q], D, lane);
         }
@@ -600,6 +640,7 @@ struct UniShared {
     int *count, *ccount;
     float *loss;
     PreTables *pre;
+    int *rcount = nullptr;   // (team universes: the step's relation count)
 };
 
 // One universe's whole training run (all epochs x nbatches steps) by the calling workgroup.
@@ -703,7 +744,7 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
     const Presampler<NT> presample{g, s_states, S.pre, fm_n, fm_e, threads, bs, neg, bern, filter, dpp, per, seq,
                                    fastpre, s_bh, s_br, s_bt};
     float epoch_loss = 0.f;
-    uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0, rows_b = 0;
+    uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0;
     const uint64_t w_start = U.prof ? wall_clock64() : 0;   // (100 MHz wall clock: the set's schedule)
     __syncthreads();
     for (int epoch = 0; epoch < epochs; ++epoch) {
@@ -794,7 +835,6 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // ---- phase B: row updates of the touched rows, RB rows per lane group at a time (all their
             // loads in flight together: the pass is a chain of dependent memory round trips otherwise)
             const int n = s_count;
-            if (U.prof) rows_b += (uint64_t)n;
             // (TransH: 2 rows of 8 floats per lane in flight spill its step's registers; TransE keeps 2)
             // (1024-thread workgroups: half the rows per lane group, twice the lane groups; 128 VGPRs per lane)
             // (r04: two rows per lane group in the hot kernels' 5-6-float shapes spill 28-68 B per lane, phase B
@@ -838,11 +878,10 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     if (code[u] >= 0 && c1[u] >= 0) {
 #pragma unroll
                         for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
-                        for (int32_t c = s_next[c1[u]]; c >= 0; c = s_next[c]) {
-                            uload(y[u], U.contrib + c * D, (int)D, lane);
-#pragma unroll
-                            for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
-                        }
+                        // (plan 2: the relation rows' long lists, four rows in flight)
+                        list_sum<PLAN == 2 ? PT_UNI_LIST_BATCH : 1>(gs[u], s_next[c1[u]], s_next, [&](Vec &r, int32_t c) {
+                            uload(r, U.contrib + c * D, (int)D, lane);
+                        });
                     }
                 }
 #pragma unroll
@@ -913,7 +952,6 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
         U.prof[6] = (uint64_t)E;
         // the universe's start on the 100 MHz wall clock (low 32 bits) and its duration in those ticks
         U.prof[7] = (w_start << 32) | ((wall_clock64() - w_start) & 0xffffffffull);
-        U.prof[62] = rows_b;   // rows updated in phase B, summed over the steps (a slot the tuning stamps leave free)
     }
     if (tid < threads) U.states[tid] = s_states[tid];
 }

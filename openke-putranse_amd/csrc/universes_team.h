@@ -7,19 +7,25 @@
 //
 //   presample  every member draws the same batches into its own LDS (universe_run's Presampler: no exchange);
 //   link pass  every member links the step's entity rows to their STATIC contribution slots (slot b * (neg + 2) + k:
-//              negative k, then head, then tail of positive b) in its own LDS lists, from the batch alone, and
-//              collects the step's rows - the same sets on every member, each member also the rows it owns
-//              (entity / relation id mod W);
+//              negative k, then the head and tail rows of positive b) in its own LDS lists and maps the step's
+//              relations to LDS gradient rows, from the batch alone; it collects the step's rows - the same sets on
+//              every member, each member also the rows it owns (entity / relation id mod W);
 //   phase A    member m runs positives b = m, m + W, ... (transe_step with ALWAYS: every slot of a positive is
-//              written, zero for an inactive pair), relation gradients into its LDS rows, which it then publishes
-//              as its partial of each step relation;
+//              written, zero rows for an inactive pair), relation gradients into its LDS rows, which it publishes as
+//              its partials of the step's relations;
 //   barrier    (team_barrier)
-//   phase B    member m updates the rows it owns: an entity row sums its slots along its list, a relation row the W
-//              members' partials in member order; normalize Jacobian of the pre-step row, Adagrad / SGD;
+//   phase B    member m updates the rows it owns: an entity row the sum of its slots along its list (list_sum, four
+//              rows in flight), a relation row the W members' partials; normalize Jacobian of the pre-step row,
+//              Adagrad / SGD;
 //   barrier.
 // Every exchanged byte (contribution rows, relation partials, the universe's table rows and Adagrad state, loss
-// partials) is written with sc1 buffer stores, drained (vmcnt(0)) before the arrival atomic, and read with sc1 buffer
-// loads: the hand-off form of MI355X_MICROARCH.md ("Inter-workgroup visibility"), correct wherever the members run.
+// partials) is stored, drained (vmcnt(0)) before the arrival atomic, and read with sc1 buffer loads (past the CU's L1,
+// served by the XCD's L2). Where the members run decides the store form: the host places a team's members on blocks of
+// one residue mod 8 (the dispatcher's round-robin over the XCDs) and each member reads its XCD (HW_REG_XCC_ID) at the
+// start; when all members share one XCD - one L2 - the stores are plain (the lines stay in that L2), otherwise sc1
+// write-through stores, the hand-off form of MI355X_MICROARCH.md ("Inter-workgroup visibility") that holds wherever the
+// members run. (sc1 stores drop the line from the L2: every later read of a table row then crosses the fabric - the
+// all-sc1 form measured 2x slower per step, round 6.)
 // The counter is monotonic per train call (2 arrivals per member per step, zeroed by the host before the launch).
 // Each poll is bounded (team_barrier): a stuck team raises an error word the host checks, it never hangs the GPU.
 //
@@ -52,54 +58,71 @@ __device__ __forceinline__ void team_barrier(uint32_t *ctr, uint32_t target, uin
     __syncthreads();
 }
 
-// gradient sink of a team member: entity rows to the positive's static slots (sc1 stores), relation rows into the
-// member's LDS gradient rows (its partials)
+// a row store of a team member: plain when the team shares one L2 (coh), else sc1 write-through
+template <int G, int VEC, int KCH>
+__device__ __forceinline__ void tstore(bool coh, const V<G, VEC, KCH> &o, __amdgpu_buffer_rsrc_t rs, uint32_t off, int D,
+                                       int lane) {
+    if (coh)
+        bstore<G, VEC, KCH, 0>(o, rs, off, D, lane);
+    else
+        bstore<G, VEC, KCH, 16>(o, rs, off, D, lane);
+}
+
+// gradient sink of a team member: entity rows to the positive's next static slot, relation rows into the member's LDS
+// rows of the step's relations (its partials: published after phase A)
 struct TeamSink {
     __amdgpu_buffer_rsrc_t contrib;
-    float *grel;                 // LDS [R][D]
+    bool coh;                    // the team shares one XCD
+    float *grel;                 // LDS [rel_step][D]
+    const int32_t *rmap;         // LDS [R]: relation -> its row among the step's relations
     mutable int slot = 0;
     template <int G, int VEC, int KCH>
     __device__ __forceinline__ void ent(int, const V<G, VEC, KCH> &g, int D, int lane) const {
-        bstore<G, VEC, KCH, 16>(g, contrib, (uint32_t)(slot++ * D * 4), D, lane);
+        tstore(coh, g, contrib, (uint32_t)(slot++ * D * 4), D, lane);
     }
     template <int G, int VEC, int KCH>
     __device__ __forceinline__ void rel(int row, const V<G, VEC, KCH> &g, int D, int lane) const {
-        vatomic(g, grel + row * D, D, lane);
+        vatomic(g, (lfloat *)(grel + ((const lint32 *)rmap)[row] * D), D, lane);
     }
     uint64_t *trace = nullptr;   // (transe_step's tuning stamps: none)
 };
 
-// member `member` of the team training universe U (U.team_w members)
+// member `member` of the team training universe U (T.w members). A positive b owns the static entity slots
+// b * (neg + 2) + k: its negatives k < neg, then its head and tail rows (transe_step's sink order).
 template <int G, int VEC, int KCH, int NT>
-__device__ __forceinline__ void universe_run_team(const UniverseDev &U, int member, int p_norm, int norm_flag, int opt,
-                                                  int neg, int bern, int filter, const UniverseLaunch &cfg,
-                                                  const UniShared &S) {
+__device__ __forceinline__ void universe_run_team(const UniverseDev &U, const TeamDev &T, int member, int p_norm,
+                                                  int norm_flag, int opt, int neg, int bern, int filter,
+                                                  const UniverseLaunch &cfg, const UniShared &S) {
     using Vec = V<G, VEC, KCH>;
     constexpr int GPB = NT / G;
     constexpr bool PF = G >= 32;
     constexpr bool kFastUpd = uni_fast(G, VEC * KCH);
-    const int W = (int)U.team_w;
+    const int W = (int)T.w;
     const int tid = threadIdx.x, lane = tid % G, grp = tid / G;
     const int bs = (int)U.bs, threads = (int)U.threads, D = (int)U.dim;
     const int E = (int)U.g.ent_total, R = (int)U.g.rel_total;
     const int seq = bs * (1 + neg), per_pos = neg + 2, nslots = bs * per_pos;
+    const int rstep = R < bs ? R : bs;   // the step's relations, at most
     const int nbatches = (int)U.nbatches, epochs = (int)U.epochs;
     const int pchunk = (int)(cfg.pchunk < U.nbatches ? cfg.pchunk : U.nbatches);
     int &s_count = *S.count;
     int &s_mcount = *S.ccount;
     float &s_loss = *S.loss;
     uint64_t *s_states = S.states;
-    // LDS: list[list_cap] | mine[list_cap] | rflag[R] | head[E] | next[nslots] | batches [3][pchunk][seq] | grel [R][D]
+    // LDS: list[cap] | mine[cap] | head[E] | rmap[R] | rlist[rstep] | next[nslots] | batches [3][pchunk][seq] |
+    //      grel [rstep][D]
     auto a4 = [](int v) { return (v + 3) & ~3; };
     int32_t *p = S.dyn;
     int32_t *s_list = p;
     p += a4((int)cfg.list_cap);
     int32_t *s_mine = p;
     p += a4((int)cfg.list_cap);
-    int32_t *s_rflag = p;
-    p += a4(R);
     int32_t *s_head = p;
     p += a4(E);
+    int32_t *s_rmap = p;
+    p += a4(R);
+    int32_t *s_rlist = p;
+    p += a4(rstep);
     int32_t *s_next = p;
     p += a4(nslots);
     int32_t *s_bh = p, *s_br = p + pchunk * seq, *s_bt = p + 2 * pchunk * seq;
@@ -112,18 +135,18 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, int memb
     const int dpp = 1 + 2 * neg;
     const bool fastpre = per <= kPreJ && pchunk <= kPreC;
     if (fastpre) {
-        PreTables &T = *S.pre;
+        PreTables &PT = *S.pre;
         if (tid < kPreJ) {
-            T.j[tid] = lcg_power((uint64_t)tid * (uint64_t)dpp);
+            PT.j[tid] = lcg_power((uint64_t)tid * (uint64_t)dpp);
         } else if (tid < kPreJ + 2 * kPreC) {
             const int c = (tid - kPreJ) >> 1, w = (tid - kPreJ) & 1;
-            T.c[c][w] = lcg_power((uint64_t)c * (uint64_t)(w ? rem : per) * (uint64_t)dpp);
+            PT.c[c][w] = lcg_power((uint64_t)c * (uint64_t)(w ? rem : per) * (uint64_t)dpp);
         }
     }
     const FastMod fm_n = fastmod_make((uint64_t)U.g.train_total), fm_e = fastmod_make((uint64_t)(E - 1));
-    for (int i = tid; i < R; i += NT) s_rflag[i] = 0;
     for (int i = tid; i < E; i += NT) s_head[i] = -1;
-    for (int i = tid; i < R * D; i += NT) s_grel[i] = 0.f;
+    for (int i = tid; i < R; i += NT) s_rmap[i] = -1;
+    for (int i = tid; i < rstep * D; i += NT) s_grel[i] = 0.f;
     StepParams P{};
     P.model = 0; P.p_norm = p_norm; P.norm_flag = norm_flag; P.opt = opt;
     P.lr = U.lr; P.margin = U.margin;
@@ -136,16 +159,29 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, int memb
     const __amdgpu_buffer_rsrc_t r_eacc = make_rsrc(U.ent_acc, (uint32_t)(E * D * 4));
     const __amdgpu_buffer_rsrc_t r_racc = make_rsrc(U.rel_acc, (uint32_t)(R * D * 4));
     const __amdgpu_buffer_rsrc_t r_con = make_rsrc(U.contrib, (uint32_t)(nslots * D * 4));
-    // team_part: [W][R][D] relation partials, then [W][epochs] loss partials
-    const __amdgpu_buffer_rsrc_t r_part = make_rsrc(U.team_part, (uint32_t)(W * R * D * 4));
-    float *loss_part = U.team_part + (int64_t)W * R * D;
-    const TeamSink sink0{r_con, s_grel};
+    const __amdgpu_buffer_rsrc_t r_part = make_rsrc(T.part, (uint32_t)(W * R * D * 4));
+    float *loss_part = T.part + W * R * D;
+    uint32_t *xcc_tab = reinterpret_cast<uint32_t *>(loss_part + W * epochs);
+    uint32_t arrivals = 0;
+    // the members' XCDs: plain stores when the whole team shares one L2 (see the file comment)
+    if (tid == 0)
+        __hip_atomic_store(xcc_tab + member, (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    arrivals += (uint32_t)W;
+    team_barrier(T.sync, arrivals, T.err);
+    bool coh = true;
+    {
+        const uint32_t x0 = __hip_atomic_load(xcc_tab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int m = 1; m < W; ++m)
+            coh = coh && __hip_atomic_load(xcc_tab + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == x0;
+    }
+    coh = __builtin_amdgcn_readfirstlane((int)coh) != 0;
+    const TeamSink sink0{r_con, coh, s_grel, s_rmap};
     const DeviceGraph &g = U.g;
     const Presampler<NT> presample{g, s_states, S.pre, fm_n, fm_e, threads, bs, neg, bern, filter, dpp, per, seq,
                                    fastpre, s_bh, s_br, s_bt};
-    uint32_t arrivals = 0;
     float epoch_loss = 0.f;
-    uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0, rows_b = 0;
+    uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0, rows_b = 0, t_bar = 0;
     const bool prof = U.prof && member == 0;
     const uint64_t w_start = prof ? wall_clock64() : 0;
     __syncthreads();
@@ -157,11 +193,13 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, int memb
             if (tid == 0) {
                 s_count = 0;
                 s_mcount = 0;
+                *S.rcount = 0;
                 s_loss = 0.f;
             }
             __syncthreads();
             const int32_t *bh = s_bh + cs * seq, *br = s_br + cs * seq, *bt = s_bt + cs * seq;
-            // link pass: the step's entity rows -> their static slots, the step's rows, this member's rows
+            // link pass: the step's entity rows -> their static slots; the step's relations -> their LDS rows; the
+            // step's rows and this member's rows (entity / relation id mod W)
             for (int q = tid; q < nslots; q += NT) {
                 const int b = q / per_pos, k = q - b * per_pos;
                 const int hp = bh[b];
@@ -181,7 +219,10 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, int memb
             }
             for (int b = tid; b < bs; b += NT) {
                 const int r = br[b];
-                if (atomicExch(s_rflag + r, 1) == 0) {
+                if (atomicCAS(s_rmap + r, -1, -2) == -1) {
+                    const int ix = atomicAdd(S.rcount, 1);
+                    s_rmap[r] = ix;
+                    s_rlist[ix] = r;
                     s_list[atomicAdd(&s_count, 1)] = (r << 2) | 1;
                     if (r % W == member) s_mine[atomicAdd(&s_mcount, 1)] = (r << 2) | 1;
                 }
@@ -212,60 +253,55 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, int memb
             }
             if (lane == 0 && grp * W + member < bs) atomicAdd(&s_loss, lacc);
             __syncthreads();
-            // this member's partial of every relation row of the step (zero where its positives did not touch it)
-            const int n = s_count;
-            for (int i = grp; i < n; i += GPB) {
-                const int32_t code = s_list[i];
-                if ((code & 3) != 1) continue;
-                const int r = code >> 2;
+            // this member's partial of each of the step's relation rows (zero where its positives did not touch it)
+            const int nr = *S.rcount;
+            for (int ix = grp; ix < nr; ix += GPB) {
+                const int r = s_rlist[ix];
                 Vec gr;
-                vload(gr, (const lfloat *)(s_grel + r * D), D, lane);
-                bstore<G, VEC, KCH, 16>(gr, r_part, (uint32_t)((member * R + r) * D * 4), D, lane);
+                vload(gr, (const lfloat *)(s_grel + ix * D), D, lane);
+                tstore(coh, gr, r_part, (uint32_t)((member * R + r) * D * 4), D, lane);
                 Vec z;
                 vzero(z);
-                vstore(z, (lfloat *)(s_grel + r * D), D, lane);
+                vstore(z, (lfloat *)(s_grel + ix * D), D, lane);
             }
             arrivals += (uint32_t)W;
-            team_barrier(U.team_sync, arrivals, U.team_err);
+            const uint64_t tb0 = prof ? clock64() : 0;
+            team_barrier(T.sync, arrivals, T.err);
             if (prof) {
                 const uint64_t t1 = clock64();
+                t_bar += t1 - tb0;
                 t_a += t1 - t0;
                 t0 = t1;
             }
-            // ---- phase B: the rows this member owns
-            const int nm = s_mcount;
+            // ---- phase B: the rows this member owns - an entity row the sum of its slots along its list (four rows
+            // in flight), a relation row the members' partials in member order
+            const int n = s_count, nm = s_mcount;
             if (prof) rows_b += (uint64_t)nm;
             for (int i = grp; i < nm; i += GPB) {
                 const int32_t code = s_mine[i];
                 const int table = code & 3, row = code >> 2;
                 const __amdgpu_buffer_rsrc_t rw = table == 0 ? r_ent : r_rel, ra = table == 0 ? r_eacc : r_racc;
                 const uint32_t off = (uint32_t)(row * D * 4);
-                Vec x, a, gs, y;
+                Vec x, a, gs;
                 bload<G, VEC, KCH, 16>(x, rw, off, D, lane);
                 if (opt != 0) bload<G, VEC, KCH, 16>(a, ra, off, D, lane);
                 if (table == 0) {
-                    // the row's slots along its list, the first two loaded with the row
-                    const int32_t c0 = s_head[row];
-                    bload<G, VEC, KCH, 16>(gs, r_con, (uint32_t)(c0 * D * 4), D, lane);
-                    int32_t c = s_next[c0];
-                    if (c >= 0) {
-                        bload<G, VEC, KCH, 16>(y, r_con, (uint32_t)(c * D * 4), D, lane);
-#pragma unroll
-                        for (int j = 0; j < Vec::N; ++j) gs.x[j] += y.x[j];
-                        for (c = s_next[c]; c >= 0; c = s_next[c]) {
-                            bload<G, VEC, KCH, 16>(y, r_con, (uint32_t)(c * D * 4), D, lane);
-#pragma unroll
-                            for (int j = 0; j < Vec::N; ++j) gs.x[j] += y.x[j];
-                        }
-                    }
+                    vzero(gs);
+                    list_sum<4>(gs, s_head[row], s_next, [&](Vec &rr, int32_t c) {
+                        bload<G, VEC, KCH, 16>(rr, r_con, (uint32_t)(c * D * 4), D, lane);
+                    });
                 } else {
-                    // the members' partials, in member order
+                    Vec y[4];
                     bload<G, VEC, KCH, 16>(gs, r_part, (uint32_t)(row * D * 4), D, lane);
-                    for (int m = 1; m < W; ++m) {
-                        bload<G, VEC, KCH, 16>(y, r_part, (uint32_t)((m * R + row) * D * 4), D, lane);
 #pragma unroll
-                        for (int j = 0; j < Vec::N; ++j) gs.x[j] += y.x[j];
-                    }
+                    for (int m = 1; m < 4; ++m)
+                        if (m < W) bload<G, VEC, KCH, 16>(y[m], r_part, (uint32_t)((m * R + row) * D * 4), D, lane);
+#pragma unroll
+                    for (int m = 1; m < 4; ++m)
+                        if (m < W) {
+#pragma unroll
+                            for (int j = 0; j < Vec::N; ++j) gs.x[j] += y[m].x[j];
+                        }
                 }
                 // TransE: entity and relation rows carry normalized-space gradients
                 Vec gg;
@@ -287,20 +323,22 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, int memb
                         else
                             x.x[j] = x.x[j] + (-U.lr) * gg.x[j] / (sqrtf(a.x[j]) + 1e-10f);
                     }
-                    bstore<G, VEC, KCH, 16>(a, ra, off, D, lane);
+                    tstore(coh, a, ra, off, D, lane);
                 }
-                bstore<G, VEC, KCH, 16>(x, rw, off, D, lane);
+                tstore(coh, x, rw, off, D, lane);
             }
             __syncthreads();   // (the heads are read above by other lane groups)
             for (int i = tid; i < n; i += NT) {
                 const int32_t code = s_list[i];
-                if ((code & 3) == 0) s_head[code >> 2] = -1; else s_rflag[code >> 2] = 0;
+                if ((code & 3) == 0) s_head[code >> 2] = -1; else s_rmap[code >> 2] = -1;
             }
             if (tid == 0) epoch_loss += s_loss * P.inv_count + (member == 0 ? U.margin : 0.f);
             arrivals += (uint32_t)W;
-            team_barrier(U.team_sync, arrivals, U.team_err);
+            const uint64_t tb1 = prof ? clock64() : 0;
+            team_barrier(T.sync, arrivals, T.err);
             if (prof) {
                 const uint64_t t1 = clock64();
+                t_bar += t1 - tb1;
                 t_b += t1 - t0;
             }
         }
@@ -311,13 +349,13 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, int memb
         epoch_loss = 0.f;
     }
     arrivals += (uint32_t)W;
-    team_barrier(U.team_sync, arrivals, U.team_err);
+    team_barrier(T.sync, arrivals, T.err);
     if (member == 0) {
-        if (tid < epochs && U.losses) {
+        for (int e = tid; U.losses && e < epochs; e += NT) {
             float l = 0.f;
             for (int m = 0; m < W; ++m)
-                l += __hip_atomic_load(loss_part + m * epochs + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            U.losses[tid] = l;
+                l += __hip_atomic_load(loss_part + m * epochs + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            U.losses[e] = l;
         }
         if (tid < threads) U.states[tid] = s_states[tid];
         if (prof && tid == 0) {
@@ -329,6 +367,8 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, int memb
             U.prof[5] = (uint64_t)D;
             U.prof[6] = (uint64_t)E;
             U.prof[7] = (w_start << 32) | ((wall_clock64() - w_start) & 0xffffffffull);
+            U.prof[60] = ((uint64_t)W << 32) | (coh ? 1u : 0u);   // team width, one XCD
+            U.prof[61] = t_bar;    // cycles member 0 spent in the two team barriers of its steps
             U.prof[62] = rows_b;   // (member 0's rows)
         }
     }
@@ -337,20 +377,22 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, int memb
 // One launch of team universes of one row shape: workgroup b is member map[2b + 1] of universe map[2b] (-1: idle)
 template <int NT, int SHAPE, int G, int VEC, int KCH>
 __global__ __launch_bounds__(NT, NT / 512 * 2) void k_universes_team(const UniverseDev *__restrict__ us,
+                                                                       const TeamDev *__restrict__ teams,
                                                                        const int32_t *__restrict__ map, int p_norm,
                                                                        int norm_flag, int opt, int64_t neg, int bern,
                                                                        int filter, UniverseLaunch cfg) {
     extern __shared__ int32_t s_dyn[];
     __shared__ uint64_t s_states[64];
-    __shared__ int s_count, s_ccount;
+    __shared__ int s_count, s_ccount, s_rcount;
     __shared__ float s_loss;
     __shared__ PreTables s_pre;
     const int u = __builtin_amdgcn_readfirstlane(map[2 * blockIdx.x]);
     const int member = __builtin_amdgcn_readfirstlane(map[2 * blockIdx.x + 1]);
     if (member < 0) return;
-    const UniShared S{s_dyn, s_states, &s_count, &s_ccount, &s_loss, &s_pre};
+    const UniShared S{s_dyn, s_states, &s_count, &s_ccount, &s_loss, &s_pre, &s_rcount};
     const UniverseDev U = us[u];
-    universe_run_team<G, VEC, KCH, NT>(U, member, p_norm, norm_flag, opt, (int)neg, bern, filter, cfg, S);
+    const TeamDev T = teams[u];
+    universe_run_team<G, VEC, KCH, NT>(U, T, member, p_norm, norm_flag, opt, (int)neg, bern, filter, cfg, S);
 }
 
 }  // namespace dev

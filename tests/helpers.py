@@ -177,7 +177,15 @@ EPS32 = 2.0 ** -24   # float32 unit roundoff
 # (PT_KAPPA_LOG; profiles/r05_parity_bound_summary.json: 0.161 at KAPPA_C = 1) so that the largest observed error uses about a third
 # of it. On top, every compared (non-exempt) element obeys an absolute cap.
 KAPPA_C = 0.5
-KAPPA_CAP = 2e-5
+# north_star's fp32 tolerance. It binds every compared element except the ill-conditioned ones: components whose
+# calibrated rounding bound itself exceeds it - an Adagrad step whose accumulator is still tiny (|d delta / d g| =
+# lr * acc / (acc + g^2)^1.5 in the thousands) on a gradient that cancelled to ~1e-4 of its absolute mass, where two
+# correct float32 evaluations differ by more than 1e-5 (round 6: the suite's largest error, 1.2e-5, C4 universe 2 step
+# 24: acc 7.6e-11, g -7.2e-6 of mass 0.038, |d delta / d g| = 3.5e3). An element whose error passes KAPPA_CAP is
+# accepted only within that uncapped bound, and such elements must be rare (ILL_MAX_FRAC of a table, at least 4);
+# every other element is held to KAPPA_CAP.
+KAPPA_CAP = 1e-5
+ILL_MAX_FRAC = 1e-3
 
 
 def kappa_bound(before, want, gm, lr, acc_before=None, atol=2e-6):
@@ -237,9 +245,16 @@ def assert_step_close(ours, want, atol, mask=None, max_frac=1e-2, what="", befor
         assert mask.sum() <= max(4, max_frac * mask.size), "%s: %d noise-decided components" % (what,
                                                                                               int(mask.sum()))
         keep &= ~mask
-    ratio, ties = 0.0, 0
+    ratio, ties, ill_n = 0.0, 0, 0
     if gm is not None:
         tol, unit, k = kappa_bound(before, want, gm, lr, acc_before, atol)
+        d_abs = np.abs(want - np.asarray(before, dtype=np.float64))
+        uncapped = atol + KAPPA_C * np.sqrt(k) * unit + 4.0 * EPS32 * d_abs
+        # over the cap but within its own (uncapped) rounding bound: the ill-conditioned components
+        ill = keep & (err > tol) & (uncapped > KAPPA_CAP) & (err <= uncapped)
+        ill_n = int(np.count_nonzero(ill))
+        assert ill_n <= max(4, ILL_MAX_FRAC * err.size), "%s: %d ill-conditioned components" % (what, ill_n)
+        tol = np.where(ill, uncapped, tol)
         tie_rows = np.asarray(gm["tie"], dtype=bool)
         ties = int(np.count_nonzero(tie_rows))
         assert ties <= max(8, 0.02 * len(tie_rows)), "%s: %d rows with near-tie decisions" % (what, ties)
@@ -257,6 +272,8 @@ def assert_step_close(ours, want, atol, mask=None, max_frac=1e-2, what="", befor
         sel = keep & (unit > 0)
         ratio = float(over[sel].max()) if sel.any() else 0.0
         rec = {"ratio": ratio, "tie_rows": ties, "noise": int(mask.sum()) if mask is not None else 0,
+               "ill_conditioned": ill_n, "max_err_well_conditioned": float(err[keep & ~ill].max())
+               if (keep & ~ill).any() else 0.0,
                "max_err": float(err[keep].max()) if keep.any() else 0.0,
                "max_allowed": float(tol[keep].max()) if keep.any() else 0.0,
                "compared": int(keep.sum())}
@@ -269,7 +286,8 @@ def assert_step_close(ours, want, atol, mask=None, max_frac=1e-2, what="", befor
                                           delta[r_, c_]),
                        max_g=float(np.asarray(gm["g"])[r_, c_]), max_abs=float(np.asarray(gm["abs"])[r_, c_]),
                        max_delta=float(delta[r_, c_]), max_ours=float(ours[r_, c_]), max_want=float(want[r_, c_]),
-                       max_acc=None if acc_before is None else float(np.asarray(acc_before)[r_, c_]))
+                       max_acc=None if acc_before is None else float(np.asarray(acc_before)[r_, c_]),
+                       max_lr=None if lr is None else float(lr), max_before=float(np.asarray(before)[r_, c_]))
         if sel.any():   # the worst element: its error, its allowed bound and what the bound is made of
             w = np.argmax(np.where(sel, over, -np.inf))
             rec.update(worst_err=float(err.flat[w]), worst_allowed=float(tol.flat[w]), worst_k=float(k.flat[w] if

@@ -661,8 +661,9 @@ def test_multi_rank_pu_flow_matches_single_process(tmp_path):
 @pytest.mark.parametrize("width", [2, 4])
 def test_universe_teams_equal_one_workgroup_and_oracle(width):
     """Team universes (universes_team.h): a set of fewer universes than CUs trains its longest TransE universes with
-    teams of `width` workgroups (pt_universe_set_teams > 0). Under SGD (no noise amplification), over whole runs of 3
-    epochs x 10 steps: the team-trained tables equal the one-workgroup tables and the oracle's trajectory within 5e-5,
+    teams of `width` workgroups (pt_universe_set_teams > 0). Under SGD with p = 2 (no noise amplification, no sign
+    decisions), over whole runs of 3 epochs x 10 steps: the team-trained tables equal the one-workgroup tables and the
+    oracle's trajectory within 5e-5,
     the sampler streams end where the oracle's do, the per-epoch losses agree within 1e-5; and under Adagrad each
     team step equals the oracle's step from the same state (teacher forcing, test_universe_kernel_matches_oracle's
     bound) - with the default width the other universe tests take teams too."""
@@ -702,7 +703,7 @@ def test_universe_teams_equal_one_workgroup_and_oracle(width):
                 keep.append((dev, seeds))
             arr = (_native.UniverseJob * len(jobs))(*jobs)
             uset = ctypes.c_void_p()
-            _native.check(L.pt_universe_set_create(arr, len(jobs), 0, 1, 1, _native.PT_SGD, 0, 0, ctypes.byref(uset)))
+            _native.check(L.pt_universe_set_create(arr, len(jobs), 0, 2, 1, _native.PT_SGD, 0, 0, ctypes.byref(uset)))
             try:
                 nt, nw = ctypes.c_int64(), ctypes.c_int64()
                 _native.check(L.pt_universe_set_teams(uset, ctypes.byref(nt), ctypes.byref(nw)))
@@ -728,7 +729,7 @@ def test_universe_teams_equal_one_workgroup_and_oracle(width):
             ent, rel = c["tabs"][0].copy(), c["tabs"][1].copy()
             for _ in range(c["epochs"] * c["nbatches"]):
                 hh, tt, rr, _ = c["ug"].sample(st, 8, c["bs"], 1, 0, 0)
-                oracle.train_step("TransE", 1, True, "sgd", c["lr"], c["margin"], ent, rel, None, (None, None, None),
+                oracle.train_step("TransE", 2, True, "sgd", c["lr"], c["margin"], ent, rel, None, (None, None, None),
                                   hh, tt, rr, c["bs"], 1)
             np.testing.assert_array_equal(st_t[i], st)
             np.testing.assert_array_equal(st_1[i], st)
