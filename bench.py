@@ -328,6 +328,36 @@ def team_info(row):
     return {"width": w, "one_xcd": bool(int(row[60]) & 1), "barrier_cycles_per_step": float(row[61]) / steps}
 
 
+def residency(pr, i):
+    """Where universe i of a profiled set ran against the others (pt_universe_set_profile word 7: start / duration on
+    the 100 MHz wall clock; word 63: XCD and HW_REG_HW_ID - SE, SH, CU fields): the time-averaged count of other
+    universes running beside it on its CU and on its XCD (the XCD's L2), and the set's average per XCD."""
+    w7 = pr[:, 7].astype(np.uint64)
+    start = (w7 >> np.uint64(32)).astype(np.float64)
+    dur = (w7 & np.uint64(0xffffffff)).astype(np.float64)
+    w63 = pr[:, 63].astype(np.uint64)
+    xcc = (w63 >> np.uint64(32)).astype(np.int64)
+    hw = (w63 & np.uint64(0xffffffff)).astype(np.int64)
+    cu = xcc * 4096 + ((hw >> 13) & 7) * 512 + ((hw >> 12) & 1) * 256 + ((hw >> 8) & 15)
+    if dur[i] <= 0:
+        return None
+    ov = np.clip(np.minimum(start + dur, start[i] + dur[i]) - np.maximum(start, start[i]), 0, None) / dur[i]
+    ov[i] = 0.0
+    return {"xcd": int(xcc[i]), "same_cu": float(ov[cu == cu[i]].sum()), "same_xcd": float(ov[xcc == xcc[i]].sum()),
+            "universes_per_xcd": [int((xcc == x).sum()) for x in range(8)],
+            "note": "time-averaged other universes beside the longest one on its CU / its XCD (profile words 7, 63)"}
+
+
+def isolated(L, us):
+    """Universes of a set that train on an XCD of their own (pt_universe_set_isolated; None: an older build)."""
+    if not hasattr(L, "pt_universe_set_isolated"):
+        return None
+    n, m = ctypes.c_int64(0), ctypes.c_uint32(0)
+    from openke import _native
+    _native.check(L.pt_universe_set_isolated(us, ctypes.byref(n), ctypes.byref(m)))
+    return {"universes": int(n.value), "xcd_mask": int(m.value)}
+
+
 def chain_profile(L, us, reset, idx, time_set, mid, name, prof_on, rel_of=None):
     """One extra (untimed) training of the set with the per-universe cycle counters on: the longest universe's
     measured cycles per step, its phases and phase-B rows, against chain_floor. VALU issue joins the floor when
@@ -369,7 +399,7 @@ def chain_profile(L, us, reset, idx, time_set, mid, name, prof_on, rel_of=None):
                                                         "cycles_per_step": {"presample": pr[i, 0] / steps,
                                                                             "phase_a": pr[i, 1] / steps,
                                                                             "phase_b": pr[i, 2] / steps}},
-            "floor_model": fl, "valu_counted": valu is not None, "team": team}
+            "floor_model": fl, "valu_counted": valu is not None, "team": team, "residency": residency(pr, i)}
 
 
 def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check_lp=False):
@@ -522,6 +552,7 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
         slots_step = int(jobs[i_long].epochs) * 20 * int(jobs[i_long].batch_size) * 2
         bytes_step = slots_step * algorithmic_bytes_per_slot(model, "adagrad", int(jobs[i_long].dim))
     uset, reset = make_set(every)
+    n_iso = isolated(L, uset)
     el = time_set(uset, reset, every, args.c3_steps, args.c3_warmup)
     class_launches = launch_times(uset)
     rel_of = {(int(jobs[i].batch_size), int(jobs[i].dim), int(unis[i]["ent"].shape[0])): int(unis[i]["rel"].shape[0])
@@ -559,7 +590,8 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
         if os.environ.get("PT_UNI_PROF_DUMP"):   # every universe's phase cycles + its job (time-model fits)
             np.savez(os.environ["PT_UNI_PROF_DUMP"], prof=prof, dims=np.array([int(j.dim) for j in jobs]),
                      bs=np.array([int(j.batch_size) for j in jobs]), epochs=np.array([int(j.epochs) for j in jobs]),
-                     E=np.array([u["ent"].shape[0] for u in unis]), run_s=el / args.c3_steps,
+                     E=np.array([u["ent"].shape[0] for u in unis]), R=np.array([u["rel"].shape[0] for u in unis]),
+                     run_s=el / args.c3_steps,
                      start_ms=w_start, dur_ms=w_dur)
         tot_p = prof[:, :3].sum(axis=0) / max(prof[:, 3].sum(), 1)
         print("universe-prof all: cycles/step presample %.0f A %.0f B %.0f" % tuple(tot_p), file=sys.stderr)
@@ -589,13 +621,25 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
             _native.check(L.pt_universe_set_profile(us, pr.ctypes.data))
             prr = pr.reshape(-1, 64)
             span_r = prr[:, :3].astype(np.float64).sum(axis=1)
+            if os.environ.get("PT_UNI_PROF_DUMP") and idx:   # the share's universes (time-model fits)
+                np.savez(os.environ["PT_UNI_PROF_DUMP"].replace(".npz", "_share%d.npz" % r), prof=prr,
+                         dims=np.array([int(jobs[i].dim) for i in idx]), bs=np.array([int(jobs[i].batch_size) for i in idx]),
+                         epochs=np.array([int(jobs[i].epochs) for i in idx]),
+                         E=np.array([unis[i]["ent"].shape[0] for i in idx]),
+                         R=np.array([unis[i]["rel"].shape[0] for i in idx]))
             spans.append(float(span_r.max()) if idx else 0.0)
             if idx:
                 il = int(np.argmax(span_r))
                 st = max(float(prr[il, 3]), 1.0)
-                teams_r.append({"team": team_info(prr[il].astype(np.float64)), "cycles_per_step": {
-                    "presample": float(prr[il, 0]) / st, "phase_a": float(prr[il, 1]) / st,
-                    "phase_b": float(prr[il, 2]) / st}})
+                t0w = min(int(w) >> 32 for w in prr[:, 7])
+                # the share's longest universes: [universe, cycles, XCD, start (10 ns wall-clock ticks)]
+                top = [[int(j), float(span_r[j]), int(prr[j, 63]) >> 32, (int(prr[j, 7]) >> 32) - t0w]
+                       for j in np.argsort(-span_r)[:6]]
+                teams_r.append({"team": team_info(prr[il].astype(np.float64)), "private_l2": isolated(L, us),
+                                "top_spans": top,
+                                "residency": residency(prr.astype(np.float64), il), "cycles_per_step": {
+                                    "presample": float(prr[il, 0]) / st, "phase_a": float(prr[il, 1]) / st,
+                                    "phase_b": float(prr[il, 2]) / st}})
             _native.check(L.pt_universe_set_free(us))
         placement = {"world": pw, "universes_per_rank": [sum(1 for k in own if po[k] == r) for r in range(pw)],
                      "share_s": shares, "max_share_s": max(shares), "rank0_share_s": shares[0],
@@ -612,7 +656,7 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
                                         tc_range[0], tc_range[1]),
            "value": slots_all * args.c3_steps / el, "unit": "triples/s", "scaling": "weak" if per_gpu else "strong",
            "steps": args.c3_steps, "warmup": args.c3_warmup, "s_per_step": el / args.c3_steps,
-           "universes_per_gpu": len(own), "host_universe_build_s": build_s,
+           "universes_per_gpu": len(own), "host_universe_build_s": build_s, "private_l2_universes": n_iso,
            "note_runs": "every timed run trains every universe from its initial tables, Adagrad state and sampler "
                         "streams (restored before the run, outside the timed region)",
            "roofline": dict(chain or {}, bound="chain", algorithmic_GBps_per_gpu=achieved,
@@ -620,9 +664,9 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
                                  "= that universe's measured shader cycles per step (pt_universe_set_profiling, one "
                                  "extra untimed training), floor = chain_floor's model of it (bench.py: L2 / LDS round "
                                  "trips, lane-group reductions, barriers, + VALU issue when its rocprofv3 counters are "
-                                 "committed for this build), frac = floor / achieved. algorithmic_GBps_per_gpu (SURVEY "
-                                 "8(d) bytes per wall second) is not an HBM measurement: the universes' working sets "
-                                 "are cache- and LDS-resident")}
+                                 "committed for this build), frac = floor / achieved; the floor takes L2 hits, which a "
+                                 "universe alone gets (hit rate 0.997) and a full set does not (C4: 0.27, "
+                                 "profiles/r06_c4_l2.txt). algorithmic_GBps_per_gpu: SURVEY 8(d) bytes per wall second")}
     if class_launches is not None:
         out["class_launches"] = class_launches
     if det_s is not None:
@@ -918,6 +962,9 @@ def main():
     ap.add_argument("--team-width", type=int, default=0,
                     help="universe workloads: widest team per universe when a GPU holds fewer universes than CUs "
                          "(pt_set_universe_team_width: 1, 2 or 4; 0 = the library default)")
+    ap.add_argument("--isolation", type=int, default=-1,
+                    help="universe workloads: most XCDs a set may reserve for its longest universes "
+                         "(pt_set_universe_isolation: 0..7, 0 = none; -1 = the library default)")
     ap.add_argument("--longest-only", action="store_true",
                     help="universe workloads: train only the set's longest universe (its chain alone)")
     ap.add_argument("--no-dropin", action="store_true",
@@ -952,6 +999,9 @@ def main():
     if args.team_width:
         from openke import _native
         _native.check(_native.lib().pt_set_universe_team_width(args.team_width))
+    if args.isolation >= 0:
+        from openke import _native
+        _native.check(_native.lib().pt_set_universe_isolation(args.isolation))
     if args.workload in PU_WORKLOADS:
         dev = torch.device("cuda", torch.cuda.current_device())
         args.c3_steps, args.c3_warmup = args.steps, args.warmup

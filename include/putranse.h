@@ -228,17 +228,27 @@ int pt_universe_set_free(pt_universe_set *s);
 /* per-universe cycle counters of the fast kernel (on = 1; off by default) and their readout: out[n][64], per
  * universe (in the set's launch order) shader-clock cycles spent in epoch presampling, phase A, phase B, the
  * step count, batch size, dim and entity count (last train call); out[.][7]: the universe's start on the 100 MHz
- * wall clock (low 32 bits, in the high word) and its duration in those ticks (low word); out[.][62]: the rows updated
- * in phase B summed over the steps; the other words of out[.][8..63]: phase stamps
- * of one step of lane group 0 in the measurement build (make TUNING=1), zero otherwise */
+ * wall clock (low 32 bits, in the high word) and its duration in those ticks (low word); out[.][63]: where it ran -
+ * its XCD (high word) and the workgroup's HW_REG_HW_ID (low word: CU, SH, SE fields); team universes: out[.][60]
+ * width << 32 | one-XCD flag, [61] member 0's barrier cycles, [62] member 0's phase-B rows summed over the steps; the
+ * other words of out[.][8..59]: phase stamps of one step of lane group 0 in the measurement build (make TUNING=1),
+ * zero otherwise */
 int pt_universe_set_profiling(pt_universe_set *s, int32_t on);
 /* Team universes (csrc/universes_team.h), process-wide and read when a set is created: when a set holds fewer
  * universes than the GPU has CUs, the spare CUs train its longest universes with teams of up to `w` workgroups
- * (one step's positives and row updates split over the members; 1, 2 or 4; default 4; 1: one workgroup each) */
+ * (one step's positives and row updates split over the members; 1, 2 or 4; default 1: one workgroup each - teams
+ * measured slower than one workgroup, round 6) */
 int pt_set_universe_team_width(int32_t w);
 int32_t pt_get_universe_team_width(void);
 /* universes of set s trained by teams, and the workgroups their launches take */
 int pt_universe_set_teams(const pt_universe_set *s, int64_t *team_universes, int64_t *team_workgroups);
+/* Private-L2 universes (csrc/universes_kern.h k_universes), process-wide and read when a set is created: when a set
+ * holds no more universes than the GPU has CUs, up to `max_xcds` whole XCDs (0..7; 0: none, the default - measured
+ * neutral) are reserved, one each for its longest universes, so that universe's tables have an XCD's L2 to themselves */
+int pt_set_universe_isolation(int32_t max_xcds);
+int32_t pt_get_universe_isolation(void);
+/* universes of set s that train on a reserved XCD, and the reserved XCDs (bit x: XCD x; may be null) */
+int pt_universe_set_isolated(const pt_universe_set *s, int64_t *n_isolated, uint32_t *xcd_mask);
 int pt_universe_set_profile(pt_universe_set *s, uint64_t *out);
 /* the current LCG states of job `job` (input order) of a set: `threads` values (host copy; synchronizes) */
 int pt_universe_set_states(pt_universe_set *s, int64_t job, uint64_t *out);

@@ -952,6 +952,9 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
         U.prof[6] = (uint64_t)E;
         // the universe's start on the 100 MHz wall clock (low 32 bits) and its duration in those ticks
         U.prof[7] = (w_start << 32) | ((wall_clock64() - w_start) & 0xffffffffull);
+        // where the workgroup ran: XCD (HW_REG_XCC_ID) and HW_REG_HW_ID (SE / SH / CU / SIMD / wave fields)
+        U.prof[63] = ((uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |
+                     (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     }
     if (tid < threads) U.states[tid] = s_states[tid];
 }
@@ -993,6 +996,47 @@ constexpr bool shape_reachable(int model, int G, int VEC, int KCH) {
 // kernel is register-allocated for its own widest shape (one kernel over all shapes spills the narrow
 // ones' state too), and two launches still run concurrently (a launch per shape would need more
 // hardware queues than a process gets).
+// The next universe of a k_universes workgroup (thread 0; -1: none left for it). q = the launch's queue words
+// (kUniQueueWords): [0] the queue, [1 + k] isolated universe k claimed, [9] workgroups done, and, set once by the host,
+// [16] the reserved-XCD mask, [17] iso_n, [18 + k] isolated universe k's XCD.
+// Private-L2 universes (round 6; pt_set_universe_isolation): a set's tables overflow the XCDs' L2s (C4: L2 hit rate
+// 0.27 in the set, 0.997 for its longest universe alone, which then steps 2.5x faster), and with fewer universes than
+// CUs the set ends with its longest chains. The host reserves whole XCDs for the longest ones: a workgroup on a
+// reserved XCD (HW_REG_XCC_ID) claims its launch's universe for that XCD, if unclaimed, and otherwise leaves - that
+// XCD's L2 then holds the one universe; the other workgroups take the launch's other universes (its first iso_n are
+// the isolated ones) from the queue. The last workgroup of the launch to run out of work claims and runs any isolated
+// universe still unclaimed (no workgroup of the launch landed on its XCD), so every universe runs exactly once
+// wherever the dispatcher puts the workgroups. (The state lives in memory, not in registers held across a universe's
+// run: the hot kernels' allocation is at its limit.)
+__device__ __noinline__ int next_universe_of(int *q, int n, int round, int *state) {
+    const uint32_t mask = (uint32_t)__hip_atomic_load(q + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int iso_n = mask ? __hip_atomic_load(q + 17, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);
+    // state: bit 0 the queue is drained for this workgroup, bit 1 counted as done, bit 2 the launch's last one
+    int st = *state;
+    int v = -1;
+    if ((mask >> xcc) & 1u) {
+        if (round == 0)
+            for (int k = 0; k < iso_n; ++k)
+                if ((uint32_t)__hip_atomic_load(q + 18 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == xcc &&
+                    atomicCAS(q + 1 + k, 0, 1) == 0)
+                    return k;
+    } else if (!(st & 1)) {
+        v = atomicAdd(q, 1) + iso_n;
+        if (v < n) return v;
+        st |= 1;
+    }
+    if (!(st & 2)) {
+        st |= 2;
+        if (atomicAdd(q + 9, 1) == (int)gridDim.x - 1) st |= 4;
+    }
+    *state = st;
+    if (st & 4)
+        for (int k = 0; k < iso_n; ++k)
+            if (atomicCAS(q + 1 + k, 0, 1) == 0) return k;
+    return -1;
+}
+
 template <int MODEL, int NT, int WPE, int CLS, int PLAN>
 __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__restrict__ us, int64_t n,
                                                        int *__restrict__ next_universe, int p_norm, int norm_flag,
@@ -1004,14 +1048,16 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
     __shared__ float s_loss;
     __shared__ PreTables s_pre;
     const UniShared S{s_dyn, s_states, &s_count, &s_ccount, &s_loss, &s_pre};
-    for (;;) {
-        if (threadIdx.x == 0) s_u = atomicAdd(next_universe, 1);
+    __shared__ int s_state;   // (thread 0's queue state, see next_universe_of)
+    if (threadIdx.x == 0) s_state = 0;
+    for (int round = 0;; ++round) {
+        if (threadIdx.x == 0) s_u = next_universe_of(next_universe, (int)n, round, &s_state);
         __syncthreads();
         // uniform: readfirstlane makes the descriptor loads below scalar (its fields live in SGPRs, not in
         // the VGPRs the step's rows need)
         const int64_t u = __builtin_amdgcn_readfirstlane(s_u);
         __syncthreads();
-        if (u >= n) break;   // every wave of the workgroup reads the same u: the whole group exits
+        if (u < 0) break;   // every wave of the workgroup reads the same u: the whole group exits
         // the 16-float class reads the descriptor's fields where they are used (fewer live scalars: C4 113 ->
         // 104 ms); the narrower classes keep a register copy (C3 65 vs 68 ms)
         const UniverseDev Uc = CLS == 2 ? UniverseDev{} : us[u];
@@ -1054,8 +1100,9 @@ hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int64_t cu
     if (per_cu < 1) per_cu = 1;
     int64_t grid = cus * per_cu;
     if (grid > n) grid = n;
+    if (cfg.grid > 0) grid = cfg.grid;   // (private-L2 universes: sized by the host)
     if (grid < 1) grid = 1;
-    e = hipMemsetAsync(counter, 0, sizeof(int), st);
+    e = hipMemsetAsync(counter, 0, sizeof(int) * kUniQueueZeroed, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), (size_t)cfg.lds_bytes, st, d_us, n, counter, p_norm,
                        norm_flag, opt, neg, bern, filter, cfg);

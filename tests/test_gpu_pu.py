@@ -658,84 +658,107 @@ def test_multi_rank_pu_flow_matches_single_process(tmp_path):
         assert a[k] == b[k], k
 
 
+def _sgd_set_runs(L, cases, modes):
+    """Trains `cases` (from _universe_case, TransE, SGD, p = 2) as one universe set per mode; a mode is
+    (configure(), check(set handle)). Returns per mode (tables, per-epoch losses, final LCG states)."""
+    import ctypes
+    from openke import _native
+    runs = []
+    for configure, check in modes:
+        configure()
+        jobs, keep = [], []
+        for c in cases:
+            dev = [None if a is None else torch.from_numpy(a.copy()).cuda() for a in c["tabs"]]
+            seeds = c["st"].copy()
+            j = _native.UniverseJob()
+            j.graph = L.pt_universe_graph(c["h"])
+            j.seeds = seeds.ctypes.data
+            j.threads, j.batch_size, j.epochs, j.nbatches, j.neg = 8, c["bs"], c["epochs"], c["nbatches"], 1
+            j.lr, j.margin = c["lr"], c["margin"]
+            j.ent, j.rel, j.normv = dev[0].data_ptr(), dev[1].data_ptr(), None
+            j.dim = c["tabs"][0].shape[1]
+            jobs.append(j)
+            keep.append((dev, seeds))
+        arr = (_native.UniverseJob * len(jobs))(*jobs)
+        uset = ctypes.c_void_p()
+        _native.check(L.pt_universe_set_create(arr, len(jobs), 0, 2, 1, _native.PT_SGD, 0, 0, ctypes.byref(uset)))
+        try:
+            check(uset)
+            losses = torch.zeros(sum(c["epochs"] for c in cases), device="cuda")
+            _native.check(L.pt_universe_set_train(uset, _native.ptr(losses), _native.stream()))
+            torch.cuda.synchronize()
+            states = []
+            for i in range(len(cases)):
+                got = np.zeros(8, dtype=np.uint64)
+                _native.check(L.pt_universe_set_states(uset, i, got.ctypes.data))
+                states.append(got)
+        finally:
+            L.pt_universe_set_free(uset)
+        runs.append(([[t.cpu().numpy() for t in k[0][:2]] for k in keep], losses.cpu().numpy(), states))
+    return runs
+
+
+def _check_sgd_runs(cases, runs):
+    """Two runs of _sgd_set_runs against each other and the oracle's trajectory: tables within 5e-5, losses within
+    1e-5, the sampler streams ending where the oracle's do."""
+    (tab_t, loss_t, st_t), (tab_1, loss_1, st_1) = runs
+    np.testing.assert_allclose(loss_t, loss_1, rtol=1e-5, atol=1e-6)
+    for i, c in enumerate(cases):
+        st = c["st"].copy()
+        ent, rel = c["tabs"][0].copy(), c["tabs"][1].copy()
+        for _ in range(c["epochs"] * c["nbatches"]):
+            hh, tt, rr, _ = c["ug"].sample(st, 8, c["bs"], 1, 0, 0)
+            oracle.train_step("TransE", 2, True, "sgd", c["lr"], c["margin"], ent, rel, None, (None, None, None),
+                              hh, tt, rr, c["bs"], 1)
+        np.testing.assert_array_equal(st_t[i], st)
+        np.testing.assert_array_equal(st_1[i], st)
+        for g_t, g_1, want in zip(tab_t[i], tab_1[i], (ent, rel)):
+            np.testing.assert_allclose(g_t, g_1, rtol=0, atol=5e-5)
+            np.testing.assert_allclose(g_t, want, rtol=0, atol=5e-5)
+
+
+def _small_set_cases(L, graph, kg, seed):
+    rs = np.random.default_rng(seed)
+    cases = []
+    for i, dim in enumerate([200, 69, 20, 200, 12, 69]):
+        tc, bal = int(rs.integers(300, 900)), float(rs.uniform(0.25, 0.5))
+
+        def tabs(E, R, dim=dim):
+            bound = np.sqrt(6.0 / (E + dim))
+            return [rs.uniform(-bound, bound, (E, dim)).astype(np.float32),
+                    rs.uniform(-bound, bound, (R, dim)).astype(np.float32), None]
+        cases.append(_universe_case(L, graph, kg, 2000 + i, tc, bal, tabs, 0.3, 2.0, 3, 10))
+    return cases
+
+
 @pytest.mark.parametrize("width", [2, 4])
 def test_universe_teams_equal_one_workgroup_and_oracle(width):
-    """Team universes (universes_team.h): a set of fewer universes than CUs trains its longest TransE universes with
-    teams of `width` workgroups (pt_universe_set_teams > 0). Under SGD with p = 2 (no noise amplification, no sign
-    decisions), over whole runs of 3 epochs x 10 steps: the team-trained tables equal the one-workgroup tables and the
-    oracle's trajectory within 5e-5,
-    the sampler streams end where the oracle's do, the per-epoch losses agree within 1e-5; and under Adagrad each
-    team step equals the oracle's step from the same state (teacher forcing, test_universe_kernel_matches_oracle's
-    bound) - with the default width the other universe tests take teams too."""
+    """Team universes (universes_team.h; off by default since round 6 - measured slower than one workgroup): a set of
+    fewer universes than CUs trains its longest TransE universes with teams of `width` workgroups
+    (pt_universe_set_teams > 0). Under SGD with p = 2 (no noise amplification, no sign decisions), over whole runs of
+    3 epochs x 10 steps: the team-trained tables equal the one-workgroup tables and the oracle's trajectory within
+    5e-5, the sampler streams end where the oracle's do, the per-epoch losses agree within 1e-5; and under Adagrad
+    each team step equals the oracle's step from the same state (teacher forcing, test_universe_kernel_matches_oracle's
+    bound)."""
     import ctypes
     from openke import _native
     L = _native.lib()
     kg = oracle.KG.load(KG_SMALL)
     graph = ctypes.c_void_p()
     _native.check(L.pt_graph_load(KG_SMALL.encode(), ctypes.byref(graph)))
-    rs = np.random.default_rng(31 + width)
-    cases = []
     default_w = L.pt_get_universe_team_width()
+    cases = _small_set_cases(L, graph, kg, 31 + width)
     try:
-        for i, dim in enumerate([200, 69, 20, 200, 12, 69]):
-            tc, bal = int(rs.integers(300, 900)), float(rs.uniform(0.25, 0.5))
-
-            def tabs(E, R, dim=dim):
-                bound = np.sqrt(6.0 / (E + dim))
-                return [rs.uniform(-bound, bound, (E, dim)).astype(np.float32),
-                        rs.uniform(-bound, bound, (R, dim)).astype(np.float32), None]
-            cases.append(_universe_case(L, graph, kg, 2000 + i, tc, bal, tabs, 0.3, 2.0, 3, 10))
-        runs = []
-        for w in (width, 1):
-            _native.check(L.pt_set_universe_team_width(w))
-            jobs, keep = [], []
-            for c in cases:
-                dev = [None if a is None else torch.from_numpy(a.copy()).cuda() for a in c["tabs"]]
-                seeds = c["st"].copy()
-                j = _native.UniverseJob()
-                j.graph = L.pt_universe_graph(c["h"])
-                j.seeds = seeds.ctypes.data
-                j.threads, j.batch_size, j.epochs, j.nbatches, j.neg = 8, c["bs"], c["epochs"], c["nbatches"], 1
-                j.lr, j.margin = c["lr"], c["margin"]
-                j.ent, j.rel, j.normv = dev[0].data_ptr(), dev[1].data_ptr(), None
-                j.dim = c["tabs"][0].shape[1]
-                jobs.append(j)
-                keep.append((dev, seeds))
-            arr = (_native.UniverseJob * len(jobs))(*jobs)
-            uset = ctypes.c_void_p()
-            _native.check(L.pt_universe_set_create(arr, len(jobs), 0, 2, 1, _native.PT_SGD, 0, 0, ctypes.byref(uset)))
-            try:
+        def teams(w):
+            def check(uset):
                 nt, nw = ctypes.c_int64(), ctypes.c_int64()
                 _native.check(L.pt_universe_set_teams(uset, ctypes.byref(nt), ctypes.byref(nw)))
                 if w > 1:
                     assert nt.value > 0 and nw.value >= 2 * nt.value, (nt.value, nw.value)
                 else:
                     assert nt.value == 0
-                losses = torch.zeros(sum(c["epochs"] for c in cases), device="cuda")
-                _native.check(L.pt_universe_set_train(uset, _native.ptr(losses), _native.stream()))
-                torch.cuda.synchronize()
-                states = []
-                for i in range(len(cases)):
-                    got = np.zeros(8, dtype=np.uint64)
-                    _native.check(L.pt_universe_set_states(uset, i, got.ctypes.data))
-                    states.append(got)
-            finally:
-                L.pt_universe_set_free(uset)
-            runs.append(([[t.cpu().numpy() for t in k[0][:2]] for k in keep], losses.cpu().numpy(), states))
-        (tab_t, loss_t, st_t), (tab_1, loss_1, st_1) = runs
-        np.testing.assert_allclose(loss_t, loss_1, rtol=1e-5, atol=1e-6)
-        for i, c in enumerate(cases):
-            st = c["st"].copy()
-            ent, rel = c["tabs"][0].copy(), c["tabs"][1].copy()
-            for _ in range(c["epochs"] * c["nbatches"]):
-                hh, tt, rr, _ = c["ug"].sample(st, 8, c["bs"], 1, 0, 0)
-                oracle.train_step("TransE", 2, True, "sgd", c["lr"], c["margin"], ent, rel, None, (None, None, None),
-                                  hh, tt, rr, c["bs"], 1)
-            np.testing.assert_array_equal(st_t[i], st)
-            np.testing.assert_array_equal(st_1[i], st)
-            for g_t, g_1, want in zip(tab_t[i], tab_1[i], (ent, rel)):
-                np.testing.assert_allclose(g_t, g_1, rtol=0, atol=5e-5)
-                np.testing.assert_allclose(g_t, want, rtol=0, atol=5e-5)
+            return (lambda: _native.check(L.pt_set_universe_team_width(w))), check
+        _check_sgd_runs(cases, _sgd_set_runs(L, cases, [teams(width), teams(1)]))
         # Adagrad, teacher-forced step by step with teams of `width`
         _native.check(L.pt_set_universe_team_width(width))
         for c in cases:
@@ -743,6 +766,39 @@ def test_universe_teams_equal_one_workgroup_and_oracle(width):
         _teacher_forced_universes(L, cases, "TransE", 1, "adagrad", 1, 0, 0)
     finally:
         _native.check(L.pt_set_universe_team_width(default_w))
+        for c in cases:
+            L.pt_universe_free(c["h"])
+        L.pt_graph_free(graph)
+
+
+def test_private_l2_universes_equal_shared_and_oracle():
+    """Private-L2 universes (k_universes; pt_set_universe_isolation): a set of fewer universes than CUs trains its
+    longest universes on XCDs reserved for them (pt_universe_set_isolated > 0 with up to 7 XCDs, 0 with none) - the
+    claim / exit / leftover-claim protocol runs every universe exactly once. Under SGD with p = 2 over 3 epochs x 10
+    steps the tables equal those of the set without isolation and the oracle's trajectory within 5e-5, the sampler
+    streams end where the oracle's do and the losses agree within 1e-5; Adagrad steps teacher-forced with isolation."""
+    import ctypes
+    from openke import _native
+    L = _native.lib()
+    kg = oracle.KG.load(KG_SMALL)
+    graph = ctypes.c_void_p()
+    _native.check(L.pt_graph_load(KG_SMALL.encode(), ctypes.byref(graph)))
+    default_k = L.pt_get_universe_isolation()
+    cases = _small_set_cases(L, graph, kg, 77)
+    try:
+        def iso(k):
+            def check(uset):
+                n = ctypes.c_int64()
+                _native.check(L.pt_universe_set_isolated(uset, ctypes.byref(n), None))
+                assert (n.value > 0) == (k > 0), n.value
+            return (lambda: _native.check(L.pt_set_universe_isolation(k))), check
+        _check_sgd_runs(cases, _sgd_set_runs(L, cases, [iso(7), iso(0)]))
+        _native.check(L.pt_set_universe_isolation(7))
+        for c in cases:
+            c["lr"], c["epochs"], c["nbatches"] = 0.05, 1, 6
+        _teacher_forced_universes(L, cases, "TransE", 1, "adagrad", 1, 0, 0)
+    finally:
+        _native.check(L.pt_set_universe_isolation(default_k))
         for c in cases:
             L.pt_universe_free(c["h"])
         L.pt_graph_free(graph)
