@@ -358,10 +358,13 @@ def isolated(L, us):
     return {"universes": int(n.value), "xcd_mask": int(m.value)}
 
 
-def chain_profile(L, us, reset, idx, time_set, mid, name, prof_on, rel_of=None):
-    """One extra (untimed) training of the set with the per-universe cycle counters on: the longest universe's
-    measured cycles per step, its phases and phase-B rows, against chain_floor. VALU issue joins the floor when
-    profiles/pmc_<name>_chain.json holds rocprofv3 counters of that universe alone on this library build.
+def chain_profile(L, us, reset, idx, time_set, mid, name, prof_on, rel_of=None, target=None):
+    """One extra (untimed) training of the set with the per-universe cycle counters on. The roofline universe is
+    `target` - the (bs, dim, ent, steps) of the set's longest universe by the placement cost model, the one
+    `--longest-only` trains and tools_gpu/pmc_chain.sh counts - its measured cycles per step in the set against
+    chain_floor, with VALU issue in the floor when profiles/pmc_<name>_chain.json holds its rocprofv3 counts on this
+    library build; `set_longest` is the universe that ran longest in this training (which one that is varies with
+    where the universes land: DESIGN.md section 6), against its floor without VALU unless it is the target.
     Phase-B rows: a team universe counts member 0's (profile word 62); a one-workgroup universe's are the expected
     distinct rows of a step - bs * (2 + neg) entity draws over E rows and bs relation draws over R (rel_of[(bs, D,
     E)]), E (1 - exp(-n / E)) each (uniform draws: an estimate; the kernel keeps no counter)."""
@@ -375,31 +378,41 @@ def chain_profile(L, us, reset, idx, time_set, mid, name, prof_on, rel_of=None):
         _native.check(L.pt_universe_set_profiling(us, 0))
     pr = pr.reshape(-1, 64).astype(np.float64)
     span = pr[:, :3].sum(axis=1)
-    i = int(np.argmax(span))
-    steps = max(pr[i, 3], 1.0)
-    bs, D, E = int(pr[i, 4]), int(pr[i, 5]), int(pr[i, 6])
-    R = (rel_of or {}).get((bs, D, E), 0)
-    rows_estimated = pr[i, 62] == 0
-    if rows_estimated:
-        rows = E * (1.0 - np.exp(-bs * 3.0 / max(E, 1))) + (R * (1.0 - np.exp(-bs / R)) if R else 0.0)
-    else:
-        rows = pr[i, 62] / steps
     pmc, _ = load_pmc("%s_chain" % name)
-    valu = None
-    if pmc and pmc.get("longest") == {"bs": bs, "dim": D, "ent": E, "steps": int(steps)}:
-        valu = pmc["valu_per_step"]
-    fl = chain_floor(mid, D, bs, rows, valu)
-    achieved = span[i] / steps
-    team = team_info(pr[i])
-    return {"achieved": achieved, "floor": fl["floor_cycles"], "frac": fl["floor_cycles"] / achieved,
-            "unit": "cycles/step", "longest_universe": {"bs": bs, "dim": D, "ent": E, "steps": int(steps),
-                                                        "rows_per_step": rows, "rows_estimated": bool(rows_estimated),
-                                                        "cycles": span[i],
-                                                        "ms_at_2.4GHz": span[i] / 2.4e6,
-                                                        "cycles_per_step": {"presample": pr[i, 0] / steps,
-                                                                            "phase_a": pr[i, 1] / steps,
-                                                                            "phase_b": pr[i, 2] / steps}},
-            "floor_model": fl, "valu_counted": valu is not None, "team": team, "residency": residency(pr, i)}
+
+    def entry(i):
+        steps = max(pr[i, 3], 1.0)
+        bs, D, E = int(pr[i, 4]), int(pr[i, 5]), int(pr[i, 6])
+        R = (rel_of or {}).get((bs, D, E), 0)
+        rows_estimated = pr[i, 62] == 0
+        if rows_estimated:
+            rows = E * (1.0 - np.exp(-bs * 3.0 / max(E, 1))) + (R * (1.0 - np.exp(-bs / R)) if R else 0.0)
+        else:
+            rows = pr[i, 62] / steps
+        key = {"bs": bs, "dim": D, "ent": E, "steps": int(steps)}
+        valu = pmc["valu_per_step"] if pmc and pmc.get("longest") == key else None
+        fl = chain_floor(mid, D, bs, rows, valu)
+        achieved = span[i] / steps
+        return {"achieved": achieved, "floor": fl["floor_cycles"], "frac": fl["floor_cycles"] / achieved,
+                "universe": dict(key, rows_per_step=rows, rows_estimated=bool(rows_estimated), cycles=span[i],
+                                 **{"ms_at_2.4GHz": span[i] / 2.4e6},
+                                 cycles_per_step={"presample": pr[i, 0] / steps, "phase_a": pr[i, 1] / steps,
+                                                  "phase_b": pr[i, 2] / steps}),
+                "floor_model": fl, "valu_counted": valu is not None, "team": team_info(pr[i]),
+                "residency": residency(pr, i)}
+    i_long = int(np.argmax(span))
+    hit = [j for j in range(len(pr)) if target is not None and
+           (int(pr[j, 4]), int(pr[j, 5]), int(pr[j, 6]), int(pr[j, 3])) == target]
+    i_t = hit[0] if hit else i_long
+    out = entry(i_t)
+    out["unit"] = "cycles/step"
+    out["roofline_universe"] = ("the set's longest by the placement cost model (the universe pmc_chain.sh counts)"
+                                if hit else "the universe that ran longest")
+    out["longest_universe"] = out.pop("universe")
+    lg = entry(i_long)
+    out["set_longest"] = {"universe": lg["universe"], "achieved": lg["achieved"], "floor": lg["floor"],
+                          "frac": lg["frac"], "valu_counted": lg["valu_counted"], "residency": lg["residency"]}
+    return out
 
 
 def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check_lp=False):
@@ -557,7 +570,12 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
     class_launches = launch_times(uset)
     rel_of = {(int(jobs[i].batch_size), int(jobs[i].dim), int(unis[i]["ent"].shape[0])): int(unis[i]["rel"].shape[0])
               for i in every}
-    chain = chain_profile(L, uset, reset, every, time_set, mid, name, prof_on, rel_of) if every else None
+    # the roofline universe: the longest by the placement cost model (the one --longest-only and pmc_chain.sh take)
+    i_m = max(every, key=lambda i: universe_cost(int(jobs[i].epochs), int(jobs[i].batch_size) * 20,
+                                                 int(jobs[i].dim))) if every else None
+    target = (int(jobs[i_m].batch_size), int(jobs[i_m].dim), int(unis[i_m]["ent"].shape[0]),
+              int(jobs[i_m].epochs) * 20) if every else None
+    chain = chain_profile(L, uset, reset, every, time_set, mid, name, prof_on, rel_of, target) if every else None
     tot = torch.tensor([el, float(slots_step), float(bytes_step)], dtype=torch.float64, device=dev)
     if ws > 1:
         import torch.distributed as dist
