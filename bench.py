@@ -348,16 +348,6 @@ def residency(pr, i):
             "note": "time-averaged other universes beside the longest one on its CU / its XCD (profile words 7, 63)"}
 
 
-def isolated(L, us):
-    """Universes of a set that train on an XCD of their own (pt_universe_set_isolated; None: an older build)."""
-    if not hasattr(L, "pt_universe_set_isolated"):
-        return None
-    n, m = ctypes.c_int64(0), ctypes.c_uint32(0)
-    from openke import _native
-    _native.check(L.pt_universe_set_isolated(us, ctypes.byref(n), ctypes.byref(m)))
-    return {"universes": int(n.value), "xcd_mask": int(m.value)}
-
-
 def chain_profile(L, us, reset, idx, time_set, mid, name, prof_on, rel_of=None, target=None):
     """One extra (untimed) training of the set with the per-universe cycle counters on. The roofline universe is
     `target` - the (bs, dim, ent, steps) of the set's longest universe by the placement cost model, the one
@@ -565,7 +555,6 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
         slots_step = int(jobs[i_long].epochs) * 20 * int(jobs[i_long].batch_size) * 2
         bytes_step = slots_step * algorithmic_bytes_per_slot(model, "adagrad", int(jobs[i_long].dim))
     uset, reset = make_set(every)
-    n_iso = isolated(L, uset)
     el = time_set(uset, reset, every, args.c3_steps, args.c3_warmup)
     class_launches = launch_times(uset)
     rel_of = {(int(jobs[i].batch_size), int(jobs[i].dim), int(unis[i]["ent"].shape[0])): int(unis[i]["rel"].shape[0])
@@ -653,8 +642,7 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
                 # the share's longest universes: [universe, cycles, XCD, start (10 ns wall-clock ticks)]
                 top = [[int(j), float(span_r[j]), int(prr[j, 63]) >> 32, (int(prr[j, 7]) >> 32) - t0w]
                        for j in np.argsort(-span_r)[:6]]
-                teams_r.append({"team": team_info(prr[il].astype(np.float64)), "private_l2": isolated(L, us),
-                                "top_spans": top,
+                teams_r.append({"team": team_info(prr[il].astype(np.float64)), "top_spans": top,
                                 "residency": residency(prr.astype(np.float64), il), "cycles_per_step": {
                                     "presample": float(prr[il, 0]) / st, "phase_a": float(prr[il, 1]) / st,
                                     "phase_b": float(prr[il, 2]) / st}})
@@ -674,7 +662,7 @@ def run_universes(args, ws, rank, dev, name="c3", cpu=True, per_gpu=False, check
                                         tc_range[0], tc_range[1]),
            "value": slots_all * args.c3_steps / el, "unit": "triples/s", "scaling": "weak" if per_gpu else "strong",
            "steps": args.c3_steps, "warmup": args.c3_warmup, "s_per_step": el / args.c3_steps,
-           "universes_per_gpu": len(own), "host_universe_build_s": build_s, "private_l2_universes": n_iso,
+           "universes_per_gpu": len(own), "host_universe_build_s": build_s,
            "note_runs": "every timed run trains every universe from its initial tables, Adagrad state and sampler "
                         "streams (restored before the run, outside the timed region)",
            "roofline": dict(chain or {}, bound="chain", algorithmic_GBps_per_gpu=achieved,
@@ -980,9 +968,6 @@ def main():
     ap.add_argument("--team-width", type=int, default=0,
                     help="universe workloads: widest team per universe when a GPU holds fewer universes than CUs "
                          "(pt_set_universe_team_width: 1, 2 or 4; 0 = the library default)")
-    ap.add_argument("--isolation", type=int, default=-1,
-                    help="universe workloads: most XCDs a set may reserve for its longest universes "
-                         "(pt_set_universe_isolation: 0..7, 0 = none; -1 = the library default)")
     ap.add_argument("--longest-only", action="store_true",
                     help="universe workloads: train only the set's longest universe (its chain alone)")
     ap.add_argument("--no-dropin", action="store_true",
@@ -1017,9 +1002,6 @@ def main():
     if args.team_width:
         from openke import _native
         _native.check(_native.lib().pt_set_universe_team_width(args.team_width))
-    if args.isolation >= 0:
-        from openke import _native
-        _native.check(_native.lib().pt_set_universe_isolation(args.isolation))
     if args.workload in PU_WORKLOADS:
         dev = torch.device("cuda", torch.cuda.current_device())
         args.c3_steps, args.c3_warmup = args.steps, args.warmup

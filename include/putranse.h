@@ -242,13 +242,6 @@ int pt_set_universe_team_width(int32_t w);
 int32_t pt_get_universe_team_width(void);
 /* universes of set s trained by teams, and the workgroups their launches take */
 int pt_universe_set_teams(const pt_universe_set *s, int64_t *team_universes, int64_t *team_workgroups);
-/* Private-L2 universes (csrc/universes_kern.h k_universes), process-wide and read when a set is created: when a set
- * holds no more universes than the GPU has CUs, up to `max_xcds` whole XCDs (0..7; 0: none, the default - measured
- * neutral) are reserved, one each for its longest universes, so that universe's tables have an XCD's L2 to themselves */
-int pt_set_universe_isolation(int32_t max_xcds);
-int32_t pt_get_universe_isolation(void);
-/* universes of set s that train on a reserved XCD, and the reserved XCDs (bit x: XCD x; may be null) */
-int pt_universe_set_isolated(const pt_universe_set *s, int64_t *n_isolated, uint32_t *xcd_mask);
 int pt_universe_set_profile(pt_universe_set *s, uint64_t *out);
 /* the current LCG states of job `job` (input order) of a set: `threads` values (host copy; synchronizes) */
 int pt_universe_set_states(pt_universe_set *s, int64_t job, uint64_t *out);

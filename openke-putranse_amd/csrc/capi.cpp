@@ -1214,10 +1214,6 @@ hipError_t class_streams(int device, int mode, size_t n, std::vector<hipStream_t
 // reference's global state; read when a set is created
 namespace {
 std::atomic<int> g_team_width{1};
-// Private-L2 universes (k_universes): the most XCDs a set may reserve for its longest universes (0: none - the
-// default: measured neutral, round 6 - the universes left share fewer L2s, and the universes that end C4's shares are
-// not the model's longest but chains running 2-3x the median step time wherever they land)
-std::atomic<int> g_iso_xcds{0};
 }
 extern "C" int pt_set_universe_team_width(int32_t w) {
     PT_CHECK(w == 1 || w == 2 || w == 4, PT_EINVAL, "pt_set_universe_team_width: 1, 2 or 4");
@@ -1226,13 +1222,6 @@ extern "C" int pt_set_universe_team_width(int32_t w) {
 }
 extern "C" int32_t pt_get_universe_team_width(void) { return g_team_width.load(); }
 
-extern "C" int pt_set_universe_isolation(int32_t max_xcds) {
-    PT_CHECK(max_xcds >= 0 && max_xcds <= 7, PT_EINVAL, "pt_set_universe_isolation: 0..7 XCDs");
-    g_iso_xcds.store(max_xcds);
-    return PT_OK;
-}
-
-extern "C" int32_t pt_get_universe_isolation(void) { return g_iso_xcds.load(); }
 
 // Train many universes with the persistent multi-universe kernel (universes.hip).
 struct pt_universe_set {
@@ -1249,12 +1238,8 @@ struct pt_universe_set {
         int64_t share = 1;   // workgroups (= CUs) of its launch
         // team launch (shape class >= kUniTeamBase): [grid][2] universe (index from off) and member (-1: idle)
         int32_t *d_map = nullptr;
-        int64_t grid = 0;   // (team launch, or a launch of a set with private-L2 universes: its workgroups)
-        // private-L2 universes of this launch: its first iso_n, universe k on XCD iso_xcd[k]
-        int iso_n = 0;
-        int8_t iso_xcd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int64_t grid = 0;
     };
-    uint32_t iso_mask = 0;                // XCDs reserved for private-L2 universes (k_universes)
     uint32_t *d_team_sync = nullptr;      // team universes' arrival counters (inside the arena, zeroed per call)
     int64_t n_team_sync = 0;
     pt::UniverseLaunch team_cfg;          // the team launches' LDS plan
@@ -1334,7 +1319,7 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
     const int64_t us_off = total;
     total += al((int64_t)sizeof(pt::UniverseDev) * std::max<int64_t>(n, 1));
     const int64_t counter_off = total;
-    total += al(sizeof(int) * pt::kUniQueueWords * 64);   // one work queue per row shape (kUniQueueWords words)
+    total += al(sizeof(int) * 64);   // one work-queue counter per row shape
     PT_HIP(hipMalloc(&set->arena, (size_t)total));
     char *base = (char *)set->arena;
     PT_HIP(hipMemset(base, 0, (size_t)us_off));
@@ -1516,60 +1501,8 @@ extern "C" int pt_universe_set_create(const pt_universe_job *jobs, int64_t n, in
             ms[best] = makespan(best, set->groups[best].share);
         }
     }
-    // Private-L2 universes (k_universes): with no more universes than CUs the set ends with its longest chains, and
-    // a chain steps ~2.5x faster with an XCD's L2 to itself (C4's longest universe alone 16.7k cycles per step, beside
-    // 15 others on its XCD 42k). Reserve whole XCDs for the longest universes, one each, while the k-th longest
-    // still outlasts the longest at that speed-up (kIsoGain) and the others keep a CU each on the XCDs left; each
-    // launch then gets enough workgroups that its share on the unreserved XCDs covers its other universes.
-    {
-        int cus = 0;
-        PT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, set->device));
-        constexpr int kXcds = 8;
-        constexpr double kIsoGain = 2.5;
-        const int per_xcd = cus / kXcds;
-        bool teams = false;
-        for (const auto &gr : set->groups) teams = teams || gr.shape >= pt::kUniTeamBase;
-        const int kmax = std::min(g_iso_xcds.load(), kXcds - 1);
-        if (kmax > 0 && !teams && n > 1 && n <= cus) {
-            std::vector<int64_t> top(order);   // jobs, longest first
-            std::stable_sort(top.begin(), top.end(), [&](int64_t a, int64_t b) { return work(a) > work(b); });
-            int k = 0;
-            while (k < kmax && k < n - 1 && n - (k + 1) <= (int64_t)(kXcds - (k + 1)) * per_xcd &&
-                   work(top[(size_t)k]) > work(top[0]) / kIsoGain)
-                ++k;
-            if (k > 0) {
-                // each launch isolates as many of its first (longest) universes as the top k holds of it (ties in
-                // the model's time may pick another of equal time), on XCDs 7, 6, ...
-                std::vector<int64_t> group_of((size_t)n);
-                for (size_t g = 0; g < set->groups.size(); ++g)
-                    for (int64_t q = set->groups[g].off; q < set->groups[g].off + set->groups[g].n; ++q)
-                        group_of[(size_t)order[q]] = (int64_t)g;
-                int x = kXcds - 1;
-                for (int t = 0; t < k; ++t) {
-                    auto &gr = set->groups[(size_t)group_of[(size_t)top[(size_t)t]]];
-                    gr.iso_xcd[gr.iso_n++] = (int8_t)x;
-                    set->iso_mask |= 1u << x--;
-                }
-                for (auto &gr : set->groups) {
-                    const int64_t rest = gr.n - gr.iso_n;
-                    const int64_t g8 = (rest * kXcds + (kXcds - k) - 1) / (kXcds - k);
-                    gr.grid = std::max<int64_t>(kXcds, (g8 + kXcds - 1) / kXcds * kXcds);
-                }
-            }
-        }
-    }
     set->d_us = (pt::UniverseDev *)(base + us_off);
     set->d_counter = (int *)(base + counter_off);
-    {   // each launch's private-L2 configuration words (next_universe_of; zero: none)
-        std::vector<int32_t> words((size_t)pt::kUniQueueWords * set->groups.size(), 0);
-        for (size_t k = 0; k < set->groups.size(); ++k) {
-            int32_t *w = words.data() + pt::kUniQueueWords * k + pt::kUniQueueZeroed;
-            w[0] = (int32_t)set->iso_mask;
-            w[1] = set->groups[k].iso_n;
-            for (int j = 0; j < set->groups[k].iso_n; ++j) w[2 + j] = set->groups[k].iso_xcd[j];
-        }
-        PT_HIP(hipMemcpy(set->d_counter, words.data(), 4 * words.size(), hipMemcpyHostToDevice));
-    }
     set->host.reserve((size_t)n);
     int64_t loss_off = 0;
     std::vector<int64_t> loss_of((size_t)n);
@@ -1888,12 +1821,10 @@ extern "C" int pt_universe_set_train(pt_universe_set *set, float *d_losses, void
             PT_HIP(hipEventRecord(set->t_stop[k], q));
             continue;
         }
-        pt::UniverseLaunch cfg = set->cfg;   // (a set with private-L2 universes: the launch's own grid)
-        cfg.grid = set->iso_mask ? gr.grid : 0;
-        const hipError_t e = pt::launch_universes(set->d_us + gr.off, gr.n, set->d_counter + pt::kUniQueueWords * k,
-                                                  gr.shape, per_universe ? gr.n : share,
+        const hipError_t e = pt::launch_universes(set->d_us + gr.off, gr.n, set->d_counter + k, gr.shape,
+                                                  per_universe ? gr.n : share,
                                                   set->model, set->p_norm, set->norm_flag, set->opt, set->neg,
-                                                  (int)set->bern, (int)set->filter, cfg, q);
+                                                  (int)set->bern, (int)set->filter, set->cfg, q);
         if (e != hipSuccess) return pt::fail(PT_EHIP, std::string("launch_universes: ") + hipGetErrorString(e));
         PT_HIP(hipEventRecord(set->t_stop[k], q));
     }
@@ -1935,15 +1866,6 @@ extern "C" int pt_universe_set_launch_times(pt_universe_set *set, int64_t cap, f
         out[3 * k] -= lo;
         out[3 * k + 1] -= lo;
     }
-    return PT_OK;
-}
-
-// universes of the set that train with an XCD to themselves (private-L2 universes)
-extern "C" int pt_universe_set_isolated(const pt_universe_set *set, int64_t *n_isolated, uint32_t *xcd_mask) {
-    PT_CHECK(set && n_isolated, PT_EINVAL, "pt_universe_set_isolated: null argument");
-    *n_isolated = 0;
-    for (const auto &gr : set->groups) *n_isolated += gr.iso_n;
-    if (xcd_mask) *xcd_mask = set->iso_mask;
     return PT_OK;
 }
 

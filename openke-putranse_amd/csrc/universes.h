@@ -69,14 +69,7 @@ struct UniverseLaunch {
     int rel_list = 0;           // relation / norm_vector rows as contribution lists (when their rows do not fit)
     int agent_fence = 1;        // agent-scope fences around the phase barriers (global atomics in use)
     int64_t lds_bytes = 0;      // dynamic LDS per workgroup
-    // grid > 0: the launch's workgroups (a set with private-L2 universes: sized so that its other universes still find
-    // a CU each on the XCDs left)
-    int64_t grid = 0;
 };
-// work-queue words per launch (k_universes' next_universe_of): [0, 16) zeroed before each launch - the queue, the
-// claims, the done count; [16, 32) the launch's private-L2 configuration, set once by the host
-constexpr int kUniQueueWords = 32;
-constexpr int kUniQueueZeroed = 16;
 
 // lane-group shape of the universe kernel for dim D (narrower groups than pick_shape) and its id in
 // the kernel's shape switch (-1: unsupported)

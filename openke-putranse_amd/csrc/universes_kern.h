@@ -570,65 +570,59 @@ struct PreTables {
 // calls) drawn at once into LDS, lane-parallel - batch j of the chunk is sampler call j after the chunk-start stream
 // states - then the streams advanced past them
 template <int NT>
-struct Presampler {
-    const DeviceGraph &g;
-    uint64_t *s_states;
-    const PreTables *pre;
-    FastMod fm_n, fm_e;
-    int threads, bs, neg, bern, filter, dpp, per, seq;
-    bool fastpre;
-    int32_t *s_bh, *s_br, *s_bt;
-    __device__ __forceinline__ void draw(int nb) const {
-        const int tid = threadIdx.x;
-        for (int q = tid; q < nb * bs; q += NT) {
-            const int s = q / bs, b = q - s * bs;
-            if (fastpre && !filter) {
-                // the same draws as draw_positive / draw_negative (bit-identical streams and values):
-                // table jumps, 32-bit slice arithmetic, rand_max by fastmod
-                const int id = b / per, j = b - id * per;
-                const PreTables &T = *pre;
-                const Affine m1 = T.j[j], m2 = T.c[s][bs - id * per >= per ? 0 : 1];
-                uint64_t st = m1.a * s_states[id] + m1.c;
-                st = m2.a * st + m2.c;
-                const int i = (int)fastmod(lcg_next(st), fm_n);
-                i32x4 ra, rc;
-                graph_rec(g, i, ra, rc);
-                int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
-                bh[b] = ra.x; br[b] = ra.y; bt[b] = ra.z;
-                const float prob = bern ? g.bern_prob[ra.y] : 500.f;
-                for (int k = 0; k < neg; ++k) {
-                    // coin, then the corruption (Corrupt.h:18-25, 68-74: skips the passed entity)
-                    const bool tail = (float)(lcg_next(st) % 1000ULL) < prob;
-                    const int tmp = (int)fastmod(lcg_next(st), fm_e);
-                    const int skip = tail ? ra.x : ra.z;
-                    const int e = tmp < skip ? tmp : tmp + 1;
-                    const int o = (k + 1) * bs + b;
-                    bh[o] = tail ? ra.x : e;
-                    bt[o] = tail ? e : ra.z;
-                    br[o] = ra.y;
-                }
-                continue;
-            }
-            const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp, s);
+__device__ __forceinline__ void presample_draw(int nb, const DeviceGraph &g, uint64_t *s_states,
+                                               const PreTables *pre, const FastMod &fm_n, const FastMod &fm_e,
+                                               int threads, int bs, int neg, int bern, int filter, int dpp, int per,
+                                               int seq, bool fastpre, int32_t *s_bh, int32_t *s_br, int32_t *s_bt) {
+    const int tid = threadIdx.x;
+    for (int q = tid; q < nb * bs; q += NT) {
+        const int s = q / bs, b = q - s * bs;
+        if (fastpre && !filter) {
+            // the same draws as draw_positive / draw_negative (bit-identical streams and values):
+            // table jumps, 32-bit slice arithmetic, rand_max by fastmod
+            const int id = b / per, j = b - id * per;
+            const PreTables &T = *pre;
+            const Affine m1 = T.j[j], m2 = T.c[s][bs - id * per >= per ? 0 : 1];
+            uint64_t st = m1.a * s_states[id] + m1.c;
+            st = m2.a * st + m2.c;
+            const int i = (int)fastmod(lcg_next(st), fm_n);
+            i32x4 ra, rc;
+            graph_rec(g, i, ra, rc);
             int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
-            bh[b] = (int32_t)pd.h; br[b] = (int32_t)pd.r; bt[b] = (int32_t)pd.t;
+            bh[b] = ra.x; br[b] = ra.y; bt[b] = ra.z;
+            const float prob = bern ? g.bern_prob[ra.y] : 500.f;
             for (int k = 0; k < neg; ++k) {
-                int side;
-                const int e = (int)draw_negative(g, pd, k, bern, filter, &side);
+                // coin, then the corruption (Corrupt.h:18-25, 68-74: skips the passed entity)
+                const bool tail = (float)(lcg_next(st) % 1000ULL) < prob;
+                const int tmp = (int)fastmod(lcg_next(st), fm_e);
+                const int skip = tail ? ra.x : ra.z;
+                const int e = tmp < skip ? tmp : tmp + 1;
                 const int o = (k + 1) * bs + b;
-                bh[o] = (int32_t)(side ? pd.h : e);
-                bt[o] = (int32_t)(side ? e : pd.t);
-                br[o] = (int32_t)pd.r;
+                bh[o] = tail ? ra.x : e;
+                bt[o] = tail ? e : ra.z;
+                br[o] = ra.y;
             }
+            continue;
         }
-        __syncthreads();
-        if (tid < threads) {   // the chunk consumed nb calls of the streams
-            int len = bs - tid * per;
-            len = len < 0 ? 0 : (len > per ? per : len);
-            s_states[tid] = lcg_jump(s_states[tid], (uint64_t)len * (uint64_t)dpp * (uint64_t)nb);
+        const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp, s);
+        int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
+        bh[b] = (int32_t)pd.h; br[b] = (int32_t)pd.r; bt[b] = (int32_t)pd.t;
+        for (int k = 0; k < neg; ++k) {
+            int side;
+            const int e = (int)draw_negative(g, pd, k, bern, filter, &side);
+            const int o = (k + 1) * bs + b;
+            bh[o] = (int32_t)(side ? pd.h : e);
+            bt[o] = (int32_t)(side ? e : pd.t);
+            br[o] = (int32_t)pd.r;
         }
     }
-};
+    __syncthreads();
+    if (tid < threads) {   // the chunk consumed nb calls of the streams
+        int len = bs - tid * per;
+        len = len < 0 ? 0 : (len > per ? per : len);
+        s_states[tid] = lcg_jump(s_states[tid], (uint64_t)len * (uint64_t)dpp * (uint64_t)nb);
+    }
+}
 
 // Dynamic LDS layout (int32 units; the host sizes it for the largest universe of the launch):
 //   list[list_cap] | flags[E + 2R] or [2R] | head[E] + next[ccap] (contrib) |
@@ -741,8 +735,6 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
         sink.gnorm = s_grel + R * D;
     }
     const DeviceGraph &g = U.g;
-    const Presampler<NT> presample{g, s_states, S.pre, fm_n, fm_e, threads, bs, neg, bern, filter, dpp, per, seq,
-                                   fastpre, s_bh, s_br, s_bt};
     float epoch_loss = 0.f;
     uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0;
     const uint64_t w_start = U.prof ? wall_clock64() : 0;   // (100 MHz wall clock: the set's schedule)
@@ -753,7 +745,59 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
             // tuning build: stamps of step 5 of epoch 1 (phase A rounds [8 + 8r, +8), phase B rounds [48 + r])
             uint64_t *const tr = U.prof && epoch == 1 && step == 5 && grp == 0 ? U.prof : nullptr;
             const int cs = pchunk > 0 ? step % pchunk : 0;
-            if (presampled && cs == 0) presample.draw(nbatches - step < pchunk ? nbatches - step : pchunk);
+            if (presampled && cs == 0) {
+                // the next min(pchunk, left) batches drawn at once into LDS: batch j of the chunk is
+                // sampler call j after the chunk-start stream states (presample_draw's draws, written out here:
+                // as a call the class kernels' allocation spills more, round 6)
+                const int nb = nbatches - step < pchunk ? nbatches - step : pchunk;
+                for (int q = tid; q < nb * bs; q += NT) {
+                    const int s = q / bs, b = q - s * bs;
+                    if (fastpre && !filter) {
+                        // the same draws as draw_positive / draw_negative (bit-identical streams and values):
+                        // table jumps, 32-bit slice arithmetic, rand_max by fastmod
+                        const int id = b / per, j = b - id * per;
+                        const PreTables &T = *S.pre;
+                        const Affine m1 = T.j[j], m2 = T.c[s][bs - id * per >= per ? 0 : 1];
+                        uint64_t st = m1.a * s_states[id] + m1.c;
+                        st = m2.a * st + m2.c;
+                        const int i = (int)fastmod(lcg_next(st), fm_n);
+                        i32x4 ra, rc;
+                        graph_rec(g, i, ra, rc);
+                        int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
+                        bh[b] = ra.x; br[b] = ra.y; bt[b] = ra.z;
+                        const float prob = bern ? g.bern_prob[ra.y] : 500.f;
+                        for (int k = 0; k < neg; ++k) {
+                            // coin, then the corruption (Corrupt.h:18-25, 68-74: skips the passed entity)
+                            const bool tail = (float)(lcg_next(st) % 1000ULL) < prob;
+                            const int tmp = (int)fastmod(lcg_next(st), fm_e);
+                            const int skip = tail ? ra.x : ra.z;
+                            const int e = tmp < skip ? tmp : tmp + 1;
+                            const int o = (k + 1) * bs + b;
+                            bh[o] = tail ? ra.x : e;
+                            bt[o] = tail ? e : ra.z;
+                            br[o] = ra.y;
+                        }
+                        continue;
+                    }
+                    const PosDraw pd = draw_positive(g, s_states, threads, bs, b, dpp, s);
+                    int32_t *bh = s_bh + s * seq, *br = s_br + s * seq, *bt = s_bt + s * seq;
+                    bh[b] = (int32_t)pd.h; br[b] = (int32_t)pd.r; bt[b] = (int32_t)pd.t;
+                    for (int k = 0; k < neg; ++k) {
+                        int side;
+                        const int e = (int)draw_negative(g, pd, k, bern, filter, &side);
+                        const int o = (k + 1) * bs + b;
+                        bh[o] = (int32_t)(side ? pd.h : e);
+                        bt[o] = (int32_t)(side ? e : pd.t);
+                        br[o] = (int32_t)pd.r;
+                    }
+                }
+                __syncthreads();
+                if (tid < threads) {   // the chunk consumed nb calls of the streams
+                    int len = bs - tid * per;
+                    len = len < 0 ? 0 : (len > per ? per : len);
+                    s_states[tid] = lcg_jump(s_states[tid], (uint64_t)len * (uint64_t)dpp * (uint64_t)nb);
+                }
+            }
             if (tid == 0) {
                 s_count = 0;
                 s_ccount = 0;
@@ -878,10 +922,17 @@ __device__ __forceinline__ void universe_run(const UniverseDev &U, int p_norm, i
                     if (code[u] >= 0 && c1[u] >= 0) {
 #pragma unroll
                         for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
-                        // (plan 2: the relation rows' long lists, four rows in flight)
-                        list_sum<PLAN == 2 ? PT_UNI_LIST_BATCH : 1>(gs[u], s_next[c1[u]], s_next, [&](Vec &r, int32_t c) {
-                            uload(r, U.contrib + c * D, (int)D, lane);
-                        });
+                        if constexpr (PLAN == 2) {   // (the relation rows' long lists, four rows in flight)
+                            list_sum<PT_UNI_LIST_BATCH>(gs[u], s_next[c1[u]], s_next, [&](Vec &r, int32_t c) {
+                                uload(r, U.contrib + c * D, (int)D, lane);
+                            });
+                        } else {
+                            for (int32_t c = s_next[c1[u]]; c >= 0; c = s_next[c]) {
+                                uload(y[u], U.contrib + c * D, (int)D, lane);
+#pragma unroll
+                                for (int j = 0; j < Vec::N; ++j) gs[u].x[j] += y[u].x[j];
+                            }
+                        }
                     }
                 }
 #pragma unroll
@@ -996,47 +1047,6 @@ constexpr bool shape_reachable(int model, int G, int VEC, int KCH) {
 // kernel is register-allocated for its own widest shape (one kernel over all shapes spills the narrow
 // ones' state too), and two launches still run concurrently (a launch per shape would need more
 // hardware queues than a process gets).
-// The next universe of a k_universes workgroup (thread 0; -1: none left for it). q = the launch's queue words
-// (kUniQueueWords): [0] the queue, [1 + k] isolated universe k claimed, [9] workgroups done, and, set once by the host,
-// [16] the reserved-XCD mask, [17] iso_n, [18 + k] isolated universe k's XCD.
-// Private-L2 universes (round 6; pt_set_universe_isolation): a set's tables overflow the XCDs' L2s (C4: L2 hit rate
-// 0.27 in the set, 0.997 for its longest universe alone, which then steps 2.5x faster), and with fewer universes than
-// CUs the set ends with its longest chains. The host reserves whole XCDs for the longest ones: a workgroup on a
-// reserved XCD (HW_REG_XCC_ID) claims its launch's universe for that XCD, if unclaimed, and otherwise leaves - that
-// XCD's L2 then holds the one universe; the other workgroups take the launch's other universes (its first iso_n are
-// the isolated ones) from the queue. The last workgroup of the launch to run out of work claims and runs any isolated
-// universe still unclaimed (no workgroup of the launch landed on its XCD), so every universe runs exactly once
-// wherever the dispatcher puts the workgroups. (The state lives in memory, not in registers held across a universe's
-// run: the hot kernels' allocation is at its limit.)
-__device__ __noinline__ int next_universe_of(int *q, int n, int round, int *state) {
-    const uint32_t mask = (uint32_t)__hip_atomic_load(q + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int iso_n = mask ? __hip_atomic_load(q + 17, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-    const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);
-    // state: bit 0 the queue is drained for this workgroup, bit 1 counted as done, bit 2 the launch's last one
-    int st = *state;
-    int v = -1;
-    if ((mask >> xcc) & 1u) {
-        if (round == 0)
-            for (int k = 0; k < iso_n; ++k)
-                if ((uint32_t)__hip_atomic_load(q + 18 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == xcc &&
-                    atomicCAS(q + 1 + k, 0, 1) == 0)
-                    return k;
-    } else if (!(st & 1)) {
-        v = atomicAdd(q, 1) + iso_n;
-        if (v < n) return v;
-        st |= 1;
-    }
-    if (!(st & 2)) {
-        st |= 2;
-        if (atomicAdd(q + 9, 1) == (int)gridDim.x - 1) st |= 4;
-    }
-    *state = st;
-    if (st & 4)
-        for (int k = 0; k < iso_n; ++k)
-            if (atomicCAS(q + 1 + k, 0, 1) == 0) return k;
-    return -1;
-}
-
 template <int MODEL, int NT, int WPE, int CLS, int PLAN>
 __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__restrict__ us, int64_t n,
                                                        int *__restrict__ next_universe, int p_norm, int norm_flag,
@@ -1048,16 +1058,14 @@ __global__ __launch_bounds__(NT, WPE) void k_universes(const UniverseDev *__rest
     __shared__ float s_loss;
     __shared__ PreTables s_pre;
     const UniShared S{s_dyn, s_states, &s_count, &s_ccount, &s_loss, &s_pre};
-    __shared__ int s_state;   // (thread 0's queue state, see next_universe_of)
-    if (threadIdx.x == 0) s_state = 0;
-    for (int round = 0;; ++round) {
-        if (threadIdx.x == 0) s_u = next_universe_of(next_universe, (int)n, round, &s_state);
+    for (;;) {
+        if (threadIdx.x == 0) s_u = atomicAdd(next_universe, 1);
         __syncthreads();
         // uniform: readfirstlane makes the descriptor loads below scalar (its fields live in SGPRs, not in
         // the VGPRs the step's rows need)
         const int64_t u = __builtin_amdgcn_readfirstlane(s_u);
         __syncthreads();
-        if (u < 0) break;   // every wave of the workgroup reads the same u: the whole group exits
+        if (u >= n) break;   // every wave of the workgroup reads the same u: the whole group exits
         // the 16-float class reads the descriptor's fields where they are used (fewer live scalars: C4 113 ->
         // 104 ms); the narrower classes keep a register copy (C3 65 vs 68 ms)
         const UniverseDev Uc = CLS == 2 ? UniverseDev{} : us[u];
@@ -1100,9 +1108,8 @@ hipError_t launch_q(const UniverseDev *d_us, int64_t n, int *counter, int64_t cu
     if (per_cu < 1) per_cu = 1;
     int64_t grid = cus * per_cu;
     if (grid > n) grid = n;
-    if (cfg.grid > 0) grid = cfg.grid;   // (private-L2 universes: sized by the host)
     if (grid < 1) grid = 1;
-    e = hipMemsetAsync(counter, 0, sizeof(int) * kUniQueueZeroed, st);
+    e = hipMemsetAsync(counter, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), (size_t)cfg.lds_bytes, st, d_us, n, counter, p_norm,
                        norm_flag, opt, neg, bern, filter, cfg);

@@ -5,7 +5,7 @@
 // at 8 GPUs: C4 128, C3 64, C5 32 universes per GPU on 256 CUs - the set's makespan is its longest chain and most
 // CUs idle. A team splits each step of one universe over its members:
 //
-//   presample  every member draws the same batches into its own LDS (universe_run's Presampler: no exchange);
+//   presample  every member draws the same batches into its own LDS (presample_draw, as universe_run: no exchange);
 //   link pass  every member links the step's entity rows to their STATIC contribution slots (slot b * (neg + 2) + k:
 //              negative k, then the head and tail rows of positive b) in its own LDS lists and maps the step's
 //              relations to LDS gradient rows, from the batch alone; it collects the step's rows - the same sets on
@@ -178,8 +178,6 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, const Te
     coh = __builtin_amdgcn_readfirstlane((int)coh) != 0;
     const TeamSink sink0{r_con, coh, s_grel, s_rmap};
     const DeviceGraph &g = U.g;
-    const Presampler<NT> presample{g, s_states, S.pre, fm_n, fm_e, threads, bs, neg, bern, filter, dpp, per, seq,
-                                   fastpre, s_bh, s_br, s_bt};
     float epoch_loss = 0.f;
     uint64_t t_pre = 0, t_a = 0, t_b = 0, t0 = 0, rows_b = 0, t_bar = 0;
     const bool prof = U.prof && member == 0;
@@ -189,7 +187,9 @@ __device__ __forceinline__ void universe_run_team(const UniverseDev &U, const Te
         for (int step = 0; step < nbatches; ++step) {
             if (prof) t0 = clock64();
             const int cs = step % pchunk;
-            if (cs == 0) presample.draw(nbatches - step < pchunk ? nbatches - step : pchunk);
+            if (cs == 0)
+                presample_draw<NT>(nbatches - step < pchunk ? nbatches - step : pchunk, g, s_states, S.pre, fm_n, fm_e,
+                                   threads, bs, neg, bern, filter, dpp, per, seq, fastpre, s_bh, s_br, s_bt);
             if (tid == 0) {
                 s_count = 0;
                 s_mcount = 0;

@@ -124,9 +124,6 @@ SIGNATURES = {
     "pt_set_universe_team_width": (ctypes.c_int, [c_i32]),
     "pt_get_universe_team_width": (c_i32, []),
     "pt_universe_set_teams": (ctypes.c_int, [c_vp, c_vp, c_vp]),
-    "pt_set_universe_isolation": (ctypes.c_int, [c_i32]),
-    "pt_get_universe_isolation": (c_i32, []),
-    "pt_universe_set_isolated": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "pt_universe_set_states": (ctypes.c_int, [c_vp, c_i64, c_vp]),
     "pt_universe_set_reset": (ctypes.c_int, [c_vp]),
     "pt_universe_set_launch_times": (ctypes.c_int, [c_vp, ctypes.c_int64, c_vp, c_vp]),

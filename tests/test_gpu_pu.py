@@ -769,36 +769,3 @@ def test_universe_teams_equal_one_workgroup_and_oracle(width):
         for c in cases:
             L.pt_universe_free(c["h"])
         L.pt_graph_free(graph)
-
-
-def test_private_l2_universes_equal_shared_and_oracle():
-    """Private-L2 universes (k_universes; pt_set_universe_isolation): a set of fewer universes than CUs trains its
-    longest universes on XCDs reserved for them (pt_universe_set_isolated > 0 with up to 7 XCDs, 0 with none) - the
-    claim / exit / leftover-claim protocol runs every universe exactly once. Under SGD with p = 2 over 3 epochs x 10
-    steps the tables equal those of the set without isolation and the oracle's trajectory within 5e-5, the sampler
-    streams end where the oracle's do and the losses agree within 1e-5; Adagrad steps teacher-forced with isolation."""
-    import ctypes
-    from openke import _native
-    L = _native.lib()
-    kg = oracle.KG.load(KG_SMALL)
-    graph = ctypes.c_void_p()
-    _native.check(L.pt_graph_load(KG_SMALL.encode(), ctypes.byref(graph)))
-    default_k = L.pt_get_universe_isolation()
-    cases = _small_set_cases(L, graph, kg, 77)
-    try:
-        def iso(k):
-            def check(uset):
-                n = ctypes.c_int64()
-                _native.check(L.pt_universe_set_isolated(uset, ctypes.byref(n), None))
-                assert (n.value > 0) == (k > 0), n.value
-            return (lambda: _native.check(L.pt_set_universe_isolation(k))), check
-        _check_sgd_runs(cases, _sgd_set_runs(L, cases, [iso(7), iso(0)]))
-        _native.check(L.pt_set_universe_isolation(7))
-        for c in cases:
-            c["lr"], c["epochs"], c["nbatches"] = 0.05, 1, 6
-        _teacher_forced_universes(L, cases, "TransE", 1, "adagrad", 1, 0, 0)
-    finally:
-        _native.check(L.pt_set_universe_isolation(default_k))
-        for c in cases:
-            L.pt_universe_free(c["h"])
-        L.pt_graph_free(graph)
