@@ -968,9 +968,6 @@ def main():
     ap.add_argument("--team-width", type=int, default=0,
                     help="universe workloads: widest team per universe when a GPU holds fewer universes than CUs "
                          "(pt_set_universe_team_width: 1, 2 or 4; 0 = the library default)")
-    ap.add_argument("--lp-scan-kernel", type=int, default=-1,
-                    help="link prediction: 1 = the LDS-row scan k_lp_scan_t, 0 = the register-row scan k_lp_scan_v "
-                         "where it applies (pt_set_lp_scan_kernel; -1 = the library default)")
     ap.add_argument("--longest-only", action="store_true",
                     help="universe workloads: train only the set's longest universe (its chain alone)")
     ap.add_argument("--no-dropin", action="store_true",
@@ -1005,9 +1002,6 @@ def main():
     if args.team_width:
         from openke import _native
         _native.check(_native.lib().pt_set_universe_team_width(args.team_width))
-    if args.lp_scan_kernel >= 0:
-        from openke import _native
-        _native.check(_native.lib().pt_set_lp_scan_kernel(args.lp_scan_kernel))
     if args.workload in PU_WORKLOADS:
         dev = torch.device("cuda", torch.cuda.current_device())
         args.c3_steps, args.c3_warmup = args.steps, args.warmup

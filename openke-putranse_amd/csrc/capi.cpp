@@ -1222,13 +1222,6 @@ extern "C" int pt_set_universe_team_width(int32_t w) {
 }
 extern "C" int32_t pt_get_universe_team_width(void) { return g_team_width.load(); }
 
-extern "C" int pt_set_lp_scan_kernel(int32_t k) {
-    PT_CHECK(k >= 0 && k <= 3, PT_EINVAL, "pt_set_lp_scan_kernel: 0 to 3");
-    pt::set_lp_scan_kernel(k);
-    return PT_OK;
-}
-extern "C" int32_t pt_get_lp_scan_kernel(void) { return pt::get_lp_scan_kernel(); }
-
 
 // Train many universes with the persistent multi-universe kernel (universes.hip).
 struct pt_universe_set {
@@ -2019,10 +2012,9 @@ extern "C" int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, i
     const int64_t keys_per_batch =
         std::max<int64_t>(1, (batch_mb << 20) / (4 * std::max<int64_t>(global_ent_total, 1)));
     const int64_t n_batches = (n_keys + keys_per_batch - 1) / keys_per_batch;
-    auto shape_key = [&](int64_t dim) {
+    auto shape_key = [](int64_t dim) {
         const pt::Shape s = pt::pick_shape(dim);
-        return (int64_t)pt::lp_scan_tier(dim, model, p_norm) * 10000000 + (int64_t)s.G * 10000 + (int64_t)s.VEC * 100 +
-               s.KCH;
+        return (int64_t)s.G * 10000 + (int64_t)s.VEC * 100 + s.KCH;
     };
     std::map<std::pair<int64_t, int64_t>, std::vector<std::vector<pt::LpPair>>> jobs_pairs;   // (shape, batch)
     for (int64_t i = 0; i < n_pairs; ++i) {

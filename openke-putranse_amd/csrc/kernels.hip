@@ -15,7 +15,6 @@
 // only to rows with a nonzero gradient (identical to the dense update).
 #include <hip/hip_runtime.h>
 
-#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 
@@ -858,9 +857,9 @@ __device__ __forceinline__ float add_abs(float acc, float v) {
 // NP sums of the sum8 form (the same partial sums and combination order for each) over one pass of d: the
 // caller's function f(q, d) for sum q reads shared operands (the LDS row) once for all of them. MODE 1: the terms
 // are |f(q, d)| (a + |v|, one add); MODE 2: the terms are f(q, d)^2, accumulated by an explicit fma(v, v, a).
-// (The TransE scans state every rounding explicitly - fma where the step is an fma, nothing left to the compiler's
-// contraction, which fused some of a loop's products and not others - so k_lp_scan_t and k_lp_scan_v compute the
-// same floats.)
+// (The TransE scan states every rounding explicitly - an fma where the step is an fma, nothing left to the
+// compiler's contraction, which had fused some of a loop's products and not others: the two-pair pass and the
+// one-pair remainder of k_lp_scan_t then rounded the same pair's score differently; tests/test_gpu_lp_scan.py.)
 template <int NP, int MODE = 0, typename F>
 __device__ __forceinline__ void sum8xn(int D, F f, float (&r)[NP]) {
     float a[NP][8];
@@ -1016,419 +1015,6 @@ __global__ __launch_bounds__(64 * NW) void k_lp_scan_t(const LpUniverseDev *__re
         }
     }
 }
-
-// k_lp_scan_v: the TransE scan with the entity row in REGISTERS and the pairs' base rows in LDS (round 6).
-// k_lp_scan_t reads the row from LDS (one ds_read2_b32 per 2 dims, shared by 2 pairs) and the base rows through
-// scalar loads. Its loop issues 16 dims of loads, waits lgkmcnt(0) and computes: the scalar loads miss the
-// scalar cache (every wave walks other pairs), and the wait couples them to the LDS reads, so the VALU issues a
-// third of the time. Here:
-//  * a wave owns 64 entities (one per lane) and holds each one's normalized row in VGPRs, as float pairs;
-//  * all NW waves of the workgroup walk the SAME pairs: SB pairs' base rows are copied verbatim into LDS, then
-//    every lane reads 4 dims of a base row with one broadcast ds_read_b128 (one address: conflict-free);
-//  * 2 dims of one pair per v_pk_fma_f32: {sg, sg} * {x_d, x_d+1} + {b_d, b_d+1} (sg = +-1: the product is
-//    exact, one rounding of the add, as the fma of k_lp_scan_t), then |.| added by the VOP3 abs modifier.
-// Every score keeps k_lp_scan_t's expression and its sum8 partial sums and order (dim d into a[d mod 8], in
-// increasing d), so the key rows are bit-identical to k_lp_scan_t's (tests/test_gpu_lp_scan.py).
-// DV: the largest dim the registers hold (the universe's own D <= DV, D % 4 == 0).
-typedef float pt_f2 __attribute__((ext_vector_type(2)));
-typedef float pt_f4 __attribute__((ext_vector_type(4)));
-
-template <int DV, int NW, int SB, int PN, int MINW = 2>
-__global__ __launch_bounds__(64 * NW, MINW) void k_lp_scan_v(const LpUniverseDev *__restrict__ us,
-                                                          const LpPair *__restrict__ pairs,
-                                                          const int64_t *__restrict__ uoff,
-                                                          const int32_t *__restrict__ uids, int p_norm, int norm_flag,
-                                                          int64_t global_E, int64_t ds, const float *__restrict__ base,
-                                                          float *__restrict__ rows) {
-#pragma clang fp contract(off)   // every fused step is an explicit fma below
-    static_assert(DV % 4 == 0, "DV: whole float4 steps");
-    __shared__ __attribute__((aligned(16))) float s_b[SB * DV];   // the block's base rows, DV floats apart
-    __shared__ int64_t s_key[SB];                                 // key * global_E
-    __shared__ float s_sg[SB];
-    const int lane = (int)threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int32_t u = uids[blockIdx.y];
-    const LpUniverseDev U = us[u];
-    const int D = (int)U.dim;
-    const int64_t e0 = (int64_t)blockIdx.x * 64 * NW;
-    if (e0 >= U.ent_total) return;   // (the whole workgroup: no barrier below is skipped by part of it)
-    const int64_t e = e0 + wave * 64 + lane;
-    const bool live = e < U.ent_total;
-    const bool wave_live = e0 + wave * 64 < U.ent_total;   // wave-uniform
-    // ---- the lane's row, normalized as k_lp_scan_t does (sum8 of squares, one reciprocal, x * inv)
-    pt_f2 x[DV / 2];
-    {
-        const float *src = U.ent + (live ? e : 0) * D;
-#pragma unroll
-        for (int j = 0; j < DV / 4; ++j) {
-            pt_f4 v = {0.f, 0.f, 0.f, 0.f};
-            if (4 * j < D) v = *reinterpret_cast<const pt_f4 *>(src + 4 * j);
-            x[2 * j] = pt_f2{v.x, v.y};
-            x[2 * j + 1] = pt_f2{v.z, v.w};
-        }
-        if (norm_flag) {
-            float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < DV / 4; ++j) {   // (dims past D: zeros, exact +0 terms)
-                const int k0 = (j & 1) * 4;
-                a[k0] = __builtin_fmaf(x[2 * j].x, x[2 * j].x, a[k0]);
-                a[k0 + 1] = __builtin_fmaf(x[2 * j].y, x[2 * j].y, a[k0 + 1]);
-                a[k0 + 2] = __builtin_fmaf(x[2 * j + 1].x, x[2 * j + 1].x, a[k0 + 2]);
-                a[k0 + 3] = __builtin_fmaf(x[2 * j + 1].y, x[2 * j + 1].y, a[k0 + 3]);
-            }
-            const float n = sqrtf(((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])));
-            const float inv = 1.0f / (n > kEps ? n : kEps);
-#pragma unroll
-            for (int j = 0; j < DV / 2; ++j) x[j] = x[j] * inv;
-        }
-    }
-    const int64_t col = live ? U.remap[e] : 0;
-    const int64_t p0 = uoff[2 * u], p1 = uoff[2 * u + 1];
-    const int q4 = D / 4;   // float4 steps of a row
-    for (int64_t s0 = p0; s0 < p1; s0 += SB) {
-        const int nb = p1 - s0 < SB ? (int)(p1 - s0) : SB;
-        __syncthreads();   // (the previous block's readers are done)
-        // rows DV floats apart, zero past D: the sums below run over all DV dims without a branch, and a dim
-        // past D adds |0 + 0| = +0 (or 0 * 0) to its partial sum, which leaves the sum's bits unchanged
-        for (int i = (int)threadIdx.x; i < nb * (DV / 4); i += 64 * NW) {
-            const int q = i / (DV / 4), c = i - q * (DV / 4);
-            pt_f4 v = {0.f, 0.f, 0.f, 0.f};
-            if (c < q4) v = *reinterpret_cast<const pt_f4 *>(base + (s0 + q) * ds + 4 * c);
-            *reinterpret_cast<pt_f4 *>(s_b + q * DV + 4 * c) = v;
-        }
-        if ((int)threadIdx.x < nb) {
-            const LpPair pr = pairs[s0 + threadIdx.x];
-            s_key[threadIdx.x] = (int64_t)pr.key * global_E;
-            s_sg[threadIdx.x] = pr.side == 0 ? 1.f : -1.f;   // side 0: x-hat + b; side 1: b - x-hat
-        }
-        __syncthreads();
-        if (!wave_live) continue;
-        for (int q = 0; q < nb; ++q) {
-            int *cell = reinterpret_cast<int *>(rows + s_key[q] + col);
-            const int old = live ? __builtin_nontemporal_load(cell) : 0;   // read before the sums
-            const float sg = s_sg[q];
-            const pt_f2 sg2 = {sg, sg};
-            const float *bq = s_b + q * DV;
-            float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            if constexpr (PN == 1) {
-#pragma unroll
-                for (int j = 0; j < DV / 4; ++j) {
-                    {
-                        const pt_f4 b = *reinterpret_cast<const pt_f4 *>(bq + 4 * j);
-                        const pt_f2 y0 = __builtin_elementwise_fma(sg2, x[2 * j], pt_f2{b.x, b.y});
-                        const pt_f2 y1 = __builtin_elementwise_fma(sg2, x[2 * j + 1], pt_f2{b.z, b.w});
-                        const int k0 = (j & 1) * 4;
-                        a[k0] = add_abs(a[k0], y0.x);
-                        a[k0 + 1] = add_abs(a[k0 + 1], y0.y);
-                        a[k0 + 2] = add_abs(a[k0 + 2], y1.x);
-                        a[k0 + 3] = add_abs(a[k0 + 3], y1.y);
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < DV / 4; ++j) {
-                    {
-                        const pt_f4 b = *reinterpret_cast<const pt_f4 *>(bq + 4 * j);
-                        const pt_f2 y0 = __builtin_elementwise_fma(sg2, x[2 * j], pt_f2{b.x, b.y});
-                        const pt_f2 y1 = __builtin_elementwise_fma(sg2, x[2 * j + 1], pt_f2{b.z, b.w});
-                        const int k0 = (j & 1) * 4;
-                        a[k0] = __builtin_fmaf(y0.x, y0.x, a[k0]);
-                        a[k0 + 1] = __builtin_fmaf(y0.y, y0.y, a[k0 + 1]);
-                        a[k0 + 2] = __builtin_fmaf(y1.x, y1.x, a[k0 + 2]);
-                        a[k0 + 3] = __builtin_fmaf(y1.y, y1.y, a[k0 + 3]);
-                    }
-                }
-            }
-            const float acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-            const float score = PN == 1 ? acc : sqrtf(acc);
-            const int bits = __float_as_int(score);
-            if (live && bits < old) atomicMin(cell, bits);
-        }
-    }
-}
-
-// k_lp_scan_g: the TransE scan tiled as a GEMM is (round 6): a workgroup owns 64 entities of a universe and walks
-// its pairs 32 at a time; the score tile (64 entities x 32 pairs) is accumulated over the dims in chunks of KC,
-// each chunk of both operands staged in LDS (double-buffered: the next chunk's global loads are in flight while
-// this one computes), rows S = KC + 4 floats apart (S / 4 odd: the 16-B reads of 16 different rows fall on
-// different banks). Lane l of wave w holds 2 entities (16 w + 2 (l & 7) + r) x 4 pairs (4 (l >> 3) + j) = 8
-// cells, so per 4 dims it reads 2 + 4 rows (ds_read_b128) for 32 cell-dims: two v_pk_fma_f32 per cell give
-// {sg, sg} * {x_d, x_d+1} + {b_d, b_d+1}, then |.| is added by the VOP3 abs modifier (p = 2: fma(y, y, a)).
-// Each score keeps k_lp_scan_t's explicit forms and order (x-hat = x * inv, inv from the sum8 tree of fma squares;
-// dim d into partial d mod 8, increasing d; the partials' tree), so the key rows are bit-identical.
-template <int PN, int KC, int MINW = 4>
-__global__ __launch_bounds__(256, MINW) void k_lp_scan_g(const LpUniverseDev *__restrict__ us,
-                                                      const LpPair *__restrict__ pairs,
-                                                      const int64_t *__restrict__ uoff,
-                                                      const int32_t *__restrict__ uids, int norm_flag,
-                                                      int64_t global_E, int64_t ds, const float *__restrict__ base,
-                                                      float *__restrict__ rows) {
-#pragma clang fp contract(off)   // every fused step is an explicit fma below
-    static_assert(KC % 8 == 0 && ((KC + 4) / 4) % 2 == 1, "KC: whole 8-dim groups, row stride 4 x odd");
-    constexpr int S = KC + 4, TE = 64, TP = 32;
-    __shared__ __attribute__((aligned(16))) float s_a[2][TE * S];
-    __shared__ __attribute__((aligned(16))) float s_b[2][TP * S];
-    __shared__ float s_inv[TE];
-    __shared__ int64_t s_key[TP];
-    __shared__ float s_sg[TP];
-    const int t = (int)threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int32_t u = uids[blockIdx.y];
-    const LpUniverseDev U = us[u];
-    const int D = (int)U.dim;
-    const int64_t e0 = (int64_t)blockIdx.x * TE;
-    if (e0 >= U.ent_total) return;   // (the whole workgroup)
-    const int ne = U.ent_total - e0 < TE ? (int)(U.ent_total - e0) : TE;
-    const int64_t p0 = uoff[2 * u], p1 = uoff[2 * u + 1];
-    const int nch = (D + KC - 1) / KC;
-    const float *ent = U.ent + e0 * D;
-    // ---- inv of the tile's rows: 4 threads per row, thread k4 the partial sums 2 k4, 2 k4 + 1 of sum8 (fma
-    // squares in increasing d), then the sum8 tree across the 4 threads
-    {
-        const int r = t >> 2, k4 = t & 3;
-        float a0 = 0.f, a1 = 0.f;
-        if (norm_flag && r < ne) {
-            const float *x = ent + (int64_t)r * D;
-            for (int d = 2 * k4; d < D; d += 8) {
-                a0 = __builtin_fmaf(x[d], x[d], a0);
-                if (d + 1 < D) a1 = __builtin_fmaf(x[d + 1], x[d + 1], a1);
-            }
-        }
-        // the tree: (a0 + a1), (a2 + a3), ... then their pair sums (a float add is commutative: the partner's
-        // value on either side gives the same bits); every lane shuffles, none inside a branch
-        float s2 = a0 + a1;
-        s2 = s2 + __shfl_xor(s2, 1, 64);
-        s2 = s2 + __shfl_xor(s2, 2, 64);
-        if (k4 == 0) {
-            const float n = sqrtf(s2);
-            s_inv[r] = norm_flag ? 1.0f / (n > kEps ? n : kEps) : 1.0f;
-        }
-    }
-    // lane's cells: entities ea + r (r < 2), pairs pb + j (j < 4)
-    const int ea = wave * 16 + 2 * (lane & 7), pb = 4 * (lane >> 3);
-    int64_t col[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) col[r] = ea + r < ne ? U.remap[e0 + ea + r] : -1;
-    constexpr int FA = TE * KC / 4, FB = TP * KC / 4;   // float4 pieces of a chunk
-    constexpr int LA = (FA + 255) / 256, LB = (FB + 255) / 256;
-    pt_f4 ra[LA], rb[LB];
-    for (int64_t s0 = p0; s0 < p1; s0 += TP) {
-        const int nb = p1 - s0 < TP ? (int)(p1 - s0) : TP;
-        __syncthreads();   // (the previous tile's readers of s_key / s_sg / the buffers are done; s_inv written)
-        if (t < TP) {
-            const LpPair pr = pairs[s0 + (t < nb ? t : 0)];
-            s_key[t] = (int64_t)pr.key * global_E;
-            s_sg[t] = pr.side == 0 ? 1.f : -1.f;   // side 0: x-hat + b; side 1: b - x-hat
-        }
-        auto load = [&](int c) {   // chunk c's pieces into registers (zeros past D, past the tile's rows)
-#pragma unroll
-            for (int i = 0; i < LA; ++i) {
-                const int f = t + 256 * i, row = f / (KC / 4), d = c * KC + 4 * (f - row * (KC / 4));
-                ra[i] = pt_f4{0.f, 0.f, 0.f, 0.f};
-                if (f < FA && row < ne && d < D) ra[i] = *reinterpret_cast<const pt_f4 *>(ent + (int64_t)row * D + d);
-            }
-#pragma unroll
-            for (int i = 0; i < LB; ++i) {
-                const int f = t + 256 * i, row = f / (KC / 4), d = c * KC + 4 * (f - row * (KC / 4));
-                rb[i] = pt_f4{0.f, 0.f, 0.f, 0.f};
-                if (f < FB && row < nb && d < D) rb[i] = *reinterpret_cast<const pt_f4 *>(base + (s0 + row) * ds + d);
-            }
-        };
-        auto store = [&](int buf) {   // registers -> LDS (the entity rows scaled by their inv: x-hat = x * inv)
-#pragma unroll
-            for (int i = 0; i < LA; ++i) {
-                const int f = t + 256 * i, row = f / (KC / 4), c4 = f - row * (KC / 4);
-                if (f < FA) *reinterpret_cast<pt_f4 *>(&s_a[buf][row * S + 4 * c4]) = ra[i] * s_inv[row];
-            }
-#pragma unroll
-            for (int i = 0; i < LB; ++i) {
-                const int f = t + 256 * i, row = f / (KC / 4), c4 = f - row * (KC / 4);
-                if (f < FB) *reinterpret_cast<pt_f4 *>(&s_b[buf][row * S + 4 * c4]) = rb[i];
-            }
-        };
-        load(0);
-        __syncthreads();   // (s_inv of this workgroup's rows is written before the first store reads it)
-        store(0);
-        float a[2][4][8];
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int k = 0; k < 8; ++k) a[r][j][k] = 0.f;
-        __syncthreads();
-        pt_f2 sg2[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float sg = s_sg[pb + j];
-            sg2[j] = pt_f2{sg, sg};
-        }
-        for (int c = 0; c < nch; ++c) {
-            const int buf = c & 1;
-            if (c + 1 < nch) load(c + 1);   // in flight while this chunk computes
-            const float *pa = &s_a[buf][ea * S], *pbb = &s_b[buf][pb * S];
-            // two 4-dim steps per iteration (an 8-dim group: the partial index k0 stays a constant), not unrolled
-            // further - a fully unrolled chunk hoists every step's LDS reads and spills
-#pragma nounroll
-            for (int i2 = 0; i2 < KC / 4; i2 += 2)
-#pragma unroll
-            for (int i = i2; i < i2 + 2; ++i) {
-                pt_f4 xa[2], xb[4];
-#pragma unroll
-                for (int r = 0; r < 2; ++r) xa[r] = *reinterpret_cast<const pt_f4 *>(pa + r * S + 4 * i);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) xb[j] = *reinterpret_cast<const pt_f4 *>(pbb + j * S + 4 * i);
-                const int k0 = (i - i2) * 4;
-#pragma unroll
-                for (int r = 0; r < 2; ++r)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const pt_f2 y0 = __builtin_elementwise_fma(sg2[j], pt_f2{xa[r].x, xa[r].y}, pt_f2{xb[j].x, xb[j].y});
-                        const pt_f2 y1 = __builtin_elementwise_fma(sg2[j], pt_f2{xa[r].z, xa[r].w}, pt_f2{xb[j].z, xb[j].w});
-                        float *aa = a[r][j];
-                        if constexpr (PN == 1) {
-                            aa[k0] = add_abs(aa[k0], y0.x);
-                            aa[k0 + 1] = add_abs(aa[k0 + 1], y0.y);
-                            aa[k0 + 2] = add_abs(aa[k0 + 2], y1.x);
-                            aa[k0 + 3] = add_abs(aa[k0 + 3], y1.y);
-                        } else {
-                            aa[k0] = __builtin_fmaf(y0.x, y0.x, aa[k0]);
-                            aa[k0 + 1] = __builtin_fmaf(y0.y, y0.y, aa[k0 + 1]);
-                            aa[k0 + 2] = __builtin_fmaf(y1.x, y1.x, aa[k0 + 2]);
-                            aa[k0 + 3] = __builtin_fmaf(y1.y, y1.y, aa[k0 + 3]);
-                        }
-                    }
-            }
-            if (c + 1 < nch) {
-                store(buf ^ 1);   // (buffer buf ^ 1 was last read in chunk c - 1, before the barrier below it)
-                __syncthreads();
-            }
-        }
-        // the key-row cells: read (all eight in flight), then an atomicMin where the score is lower
-        int old[2][4];
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                old[r][j] = col[r] >= 0 && pb + j < nb
-                                ? __builtin_nontemporal_load(reinterpret_cast<const int *>(rows + s_key[pb + j] + col[r]))
-                                : 0;
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float *aa = a[r][j];
-                const float acc = ((aa[0] + aa[1]) + (aa[2] + aa[3])) + ((aa[4] + aa[5]) + (aa[6] + aa[7]));
-                const float score = PN == 1 ? acc : sqrtf(acc);
-                const int bits = __float_as_int(score);
-                if (col[r] >= 0 && pb + j < nb && bits < old[r][j])
-                    atomicMin(reinterpret_cast<int *>(rows + s_key[pb + j] + col[r]), bits);
-            }
-    }
-}
-
-#ifdef PT_TUNING
-// Measurement-build variants of k_lp_scan_v (PT_LP_V_VARIANT):
-// k_lp_scan_s: the same register row, the base rows through scalar loads straight from memory (no LDS block: all
-// the workgroup's waves walk the same pairs, so the scalar cache serves the first wave's lines to the others).
-// NPP: pairs per pass over the row (2: two pairs' sums in flight, one row register read for both).
-template <int DV, int NW, int PN, int NPP>
-__global__ __launch_bounds__(64 * NW, 2) void k_lp_scan_s(const LpUniverseDev *__restrict__ us,
-                                                          const LpPair *__restrict__ pairs,
-                                                          const int64_t *__restrict__ uoff,
-                                                          const int32_t *__restrict__ uids, int p_norm, int norm_flag,
-                                                          int64_t global_E, int64_t ds, const float *__restrict__ base,
-                                                          float *__restrict__ rows) {
-#pragma clang fp contract(off)
-    const int lane = (int)threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int32_t u = uids[blockIdx.y];
-    const LpUniverseDev U = us[u];
-    const int D = (int)U.dim;
-    const int64_t e0 = (int64_t)blockIdx.x * 64 * NW + wave * 64;
-    if (e0 >= U.ent_total) return;   // (no barrier below)
-    const int64_t e = e0 + lane;
-    const bool live = e < U.ent_total;
-    pt_f2 x[DV / 2];
-    {
-        const float *src = U.ent + (live ? e : 0) * D;
-#pragma unroll
-        for (int j = 0; j < DV / 4; ++j) {
-            pt_f4 v = {0.f, 0.f, 0.f, 0.f};
-            if (4 * j < D) v = *reinterpret_cast<const pt_f4 *>(src + 4 * j);
-            x[2 * j] = pt_f2{v.x, v.y};
-            x[2 * j + 1] = pt_f2{v.z, v.w};
-        }
-        if (norm_flag) {
-            float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < DV / 4; ++j) {
-                const int k0 = (j & 1) * 4;
-                a[k0] = __builtin_fmaf(x[2 * j].x, x[2 * j].x, a[k0]);
-                a[k0 + 1] = __builtin_fmaf(x[2 * j].y, x[2 * j].y, a[k0 + 1]);
-                a[k0 + 2] = __builtin_fmaf(x[2 * j + 1].x, x[2 * j + 1].x, a[k0 + 2]);
-                a[k0 + 3] = __builtin_fmaf(x[2 * j + 1].y, x[2 * j + 1].y, a[k0 + 3]);
-            }
-            const float n = sqrtf(((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])));
-            const float inv = 1.0f / (n > kEps ? n : kEps);
-#pragma unroll
-            for (int j = 0; j < DV / 2; ++j) x[j] = x[j] * inv;
-        }
-    }
-    const int64_t col = live ? U.remap[e] : 0;
-    const int64_t p0 = uoff[2 * u], p1 = uoff[2 * u + 1];
-    const int q4 = D / 4;
-    for (int64_t pi = p0; pi < p1; pi += NPP) {
-        int *cell[NPP];
-        int old[NPP];
-        pt_f2 sg2[NPP];
-        const float *bq[NPP];
-        bool on[NPP];
-#pragma unroll
-        for (int q = 0; q < NPP; ++q) {
-            on[q] = pi + q < p1;
-            const LpPair pr = pairs[on[q] ? pi + q : pi];
-            cell[q] = reinterpret_cast<int *>(rows + (int64_t)pr.key * global_E + col);
-            old[q] = live && on[q] ? __builtin_nontemporal_load(cell[q]) : 0;
-            const float sg = pr.side == 0 ? 1.f : -1.f;
-            sg2[q] = pt_f2{sg, sg};
-            bq[q] = base + (on[q] ? pi + q : pi) * ds;
-        }
-        float a[NPP][8];
-#pragma unroll
-        for (int q = 0; q < NPP; ++q)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) a[q][k] = 0.f;
-#pragma unroll
-        for (int j = 0; j < DV / 4; ++j) {
-            if (j < q4) {   // (dims past D: the sums' bits are unchanged by them; skipped here, uniform)
-#pragma unroll
-                for (int q = 0; q < NPP; ++q) {
-                    const pt_f4 b = *reinterpret_cast<const pt_f4 *>(bq[q] + 4 * j);
-                    const pt_f2 y0 = __builtin_elementwise_fma(sg2[q], x[2 * j], pt_f2{b.x, b.y});
-                    const pt_f2 y1 = __builtin_elementwise_fma(sg2[q], x[2 * j + 1], pt_f2{b.z, b.w});
-                    const int k0 = (j & 1) * 4;
-                    if constexpr (PN == 1) {
-                        a[q][k0] = add_abs(a[q][k0], y0.x);
-                        a[q][k0 + 1] = add_abs(a[q][k0 + 1], y0.y);
-                        a[q][k0 + 2] = add_abs(a[q][k0 + 2], y1.x);
-                        a[q][k0 + 3] = add_abs(a[q][k0 + 3], y1.y);
-                    } else {
-                        a[q][k0] = __builtin_fmaf(y0.x, y0.x, a[q][k0]);
-                        a[q][k0 + 1] = __builtin_fmaf(y0.y, y0.y, a[q][k0 + 1]);
-                        a[q][k0 + 2] = __builtin_fmaf(y1.x, y1.x, a[q][k0 + 2]);
-                        a[q][k0 + 3] = __builtin_fmaf(y1.y, y1.y, a[q][k0 + 3]);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < NPP; ++q) {
-            const float acc = ((a[q][0] + a[q][1]) + (a[q][2] + a[q][3])) + ((a[q][4] + a[q][5]) + (a[q][6] + a[q][7]));
-            const float score = PN == 1 ? acc : sqrtf(acc);
-            const int bits = __float_as_int(score);
-            if (live && on[q] && bits < old[q]) atomicMin(cell[q], bits);
-        }
-    }
-}
-#endif
 
 }  // namespace dev
 
@@ -1625,72 +1211,12 @@ static int lp_waves() {
     }();
     return nw;
 }
-// The TransE scan kernel (pt_set_lp_scan_kernel: the bit-identity test and A/B timing): 0 = k_lp_scan_g where the
-// job's rows are whole float4s (D % 4 == 0), else k_lp_scan_t; 1 = always k_lp_scan_t; 2 = k_lp_scan_v where its
-// register tiers allow it (D % 4 == 0, D <= 200; p = 2: D <= 128), else k_lp_scan_t
-static std::atomic<int> g_lp_scan_kernel{0};
-void set_lp_scan_kernel(int k) { g_lp_scan_kernel.store(k); }
-int get_lp_scan_kernel() { return g_lp_scan_kernel.load(); }
-
-// registers per lane for the row (k_lp_scan_v's DV) of a job whose largest dim is `dim`; 0: not applicable
-// (TransH, dims not a multiple of 4, above 200; p = 2 above 128, where the squares' packed accumulators spill)
-int lp_scan_tier(int64_t dim, int model, int p_norm) {
-    if (model != 0 || dim <= 0 || dim % 4 != 0) return 0;
-    for (int dv : {32, 64, 128, 200})
-        if (dim <= dv) return p_norm != 1 && dv > 128 ? 0 : dv;
-    return 0;
-}
-
-#ifdef PT_TUNING
-// measurement variants of the DV = 200, p = 1 scan (PT_LP_V_VARIANT): 1 = k_lp_scan_v at one wave per SIMD (512
-// VGPRs), 2 / 3 = k_lp_scan_s with 1 / 2 pairs per pass (base rows by scalar loads); 0 = the product kernel
-static bool lpv_variant(dim3 gv, dim3 bv, hipStream_t st, const LpUniverseDev *us, const LpPair *pairs,
-                        const int64_t *uoff, const int32_t *uids, int p_norm, int norm_flag, int64_t global_E,
-                        int64_t ds, const float *base, float *rows) {
-    static const int v = [] {
-        const char *e = pt_tuning_env("PT_LP_V_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    if (v == 1)
-        hipLaunchKernelGGL((dev::k_lp_scan_v<200, 4, 32, 1, 1>), gv, bv, 0, st, us, pairs, uoff, uids, p_norm,
-                           norm_flag, global_E, ds, base, rows);
-    else if (v == 2)
-        hipLaunchKernelGGL((dev::k_lp_scan_s<200, 4, 1, 1>), gv, bv, 0, st, us, pairs, uoff, uids, p_norm, norm_flag,
-                           global_E, ds, base, rows);
-    else if (v == 3)
-        hipLaunchKernelGGL((dev::k_lp_scan_s<200, 4, 1, 2>), gv, bv, 0, st, us, pairs, uoff, uids, p_norm, norm_flag,
-                           global_E, ds, base, rows);
-    return v >= 1 && v <= 3;
-}
-#endif
-
-// k_lp_scan_g's dims per chunk for a job of largest dim `dim`: padded dims + 8 per chunk (a chunk's barrier and
-// staging) as small as possible, the larger chunk on ties
-static int lp_scan_kc(int64_t dim) {
-    int best = 32;
-    int64_t cost = -1;
-    for (int kc : {32, 24, 16, 8}) {   // (40: spills at the 168-VGPR cap)
-        const int64_t n = (dim + kc - 1) / kc, c = n * kc + 8 * n;
-        if (cost < 0 || c < cost) best = kc, cost = c;
-    }
-    return best;
-}
-
 hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, const int64_t *uoff,
                          const int32_t *uids, int64_t n_active, int64_t dim, int64_t max_ent, int model, int p_norm,
                          int norm_flag, int64_t global_E, int64_t ds, float *base, float *normal, float *rows,
                          float *tuple_min, hipStream_t st) {
     if (n_pairs <= 0) return hipSuccess;
     const Shape s = pick_shape(dim);
-    static const bool v_off = [] {   // (measurement build: PT_LP_SCAN_V=0 takes k_lp_scan_t)
-        const char *v = pt_tuning_env("PT_LP_SCAN_V");
-        return v && atoi(v) == 0;
-    }();
-    const int kmode = g_lp_scan_kernel.load();
-    // k_lp_scan_g (default): TransE with whole float4 rows (every universe of a VEC = 4 job has D % 4 == 0)
-    const int kc = kmode == 3 && !v_off && model == 0 && dim % 4 == 0 && ds % 4 == 0 ? lp_scan_kc(dim) : 0;
-    const int dv = kmode == 2 && ds % 4 == 0 ? lp_scan_tier(dim, model, p_norm) : 0;
-    constexpr int kVW = 4, kVSB = 32;   // k_lp_scan_v: waves per workgroup, pairs per LDS block
     // the transposed scan's tile of 64 rows in LDS (row stride dim + 1)
     const size_t lds_t = sizeof(float) * 64 * (size_t)(dim + 1);
     const int nw = lp_waves();
@@ -1721,34 +1247,6 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
             hipLaunchKernelGGL((dev::k_lp_scan_t<1, NW_>), gt, bt, lds_t, st, us, pairs, uoff, uids + y0, p_norm,    \
                                norm_flag, global_E, ds, base, normal, rows);                                       \
     }
-#ifdef PT_TUNING
-    static const bool lpg_w3 = [] {   // (measurement build: PT_LP_G_W=3 takes k_lp_scan_g at 3 waves per SIMD)
-        const char *v = pt_tuning_env("PT_LP_G_W");
-        return v && atoi(v) == 3;
-    }();
-#define PT_LPG_W3 lpg_w3
-#define PT_LPV_VARIANT(DV_) lpv_variant(gv, bv, st, us, pairs, uoff, uids + y0, p_norm, norm_flag, global_E, ds, base, rows)
-#else
-#define PT_LPV_VARIANT(DV_) false
-#define PT_LPG_W3 false
-#endif
-#define PT_LPG(KC_)                                                                                                \
-    if (kc == KC_ && p_norm == 1 && PT_LPG_W3)                                                                     \
-        hipLaunchKernelGGL((dev::k_lp_scan_g<1, KC_, 3>), gg, bg, 0, st, us, pairs, uoff, uids + y0, norm_flag,     \
-                           global_E, ds, base, rows);                                                              \
-    else if (kc == KC_ && p_norm == 1)                                                                             \
-        hipLaunchKernelGGL((dev::k_lp_scan_g<1, KC_>), gg, bg, 0, st, us, pairs, uoff, uids + y0, norm_flag,        \
-                           global_E, ds, base, rows);                                                              \
-    else if (kc == KC_)                                                                                            \
-        hipLaunchKernelGGL((dev::k_lp_scan_g<2, KC_>), gg, bg, 0, st, us, pairs, uoff, uids + y0, norm_flag,        \
-                           global_E, ds, base, rows);
-#define PT_LPV(DV_)                                                                                                \
-    if (dv == DV_ && p_norm == 1)                                                                                  \
-        hipLaunchKernelGGL((dev::k_lp_scan_v<DV_, kVW, kVSB, 1>), gv, bv, 0, st, us, pairs, uoff, uids + y0,       \
-                           p_norm, norm_flag, global_E, ds, base, rows);                                           \
-    else if (dv == DV_)                                                                                            \
-        hipLaunchKernelGGL((dev::k_lp_scan_v<DV_, kVW, kVSB, 2>), gv, bv, 0, st, us, pairs, uoff, uids + y0,       \
-                           p_norm, norm_flag, global_E, ds, base, rows);
 #define PT_LP(G_, V_, K_)                                                                                          \
     if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                                               \
         for (int64_t y0 = 0; y0 < n_active; y0 += 65535) {                                                         \
@@ -1761,16 +1259,7 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
                     hipLaunchKernelGGL((dev::k_lp_bases<1, G_, V_, K_>), gb, block, 0, st, us, pairs, n_pairs,    \
                                        p_norm, norm_flag, ds, base, normal, tuple_min);                            \
             }                                                                                                      \
-            if (kc) {                                                                                              \
-                const dim3 gg((unsigned)((max_ent + 63) / 64), gs.y), bg(256);                                     \
-                PT_LPG(32) PT_LPG(24) PT_LPG(16) PT_LPG(8)                                                         \
-            } else if (dv) {                                                                                       \
-                const dim3 gv((unsigned)((max_ent + 64 * kVW - 1) / (64 * kVW)), gs.y), bv(64 * kVW);              \
-                PT_LPV(32) PT_LPV(64) PT_LPV(128)                                                                  \
-                if (dv == 200 && !PT_LPV_VARIANT(200))   /* (p = 1 only: lp_scan_tier) */                         \
-                    hipLaunchKernelGGL((dev::k_lp_scan_v<200, kVW, kVSB, 1>), gv, bv, 0, st, us, pairs, uoff,       \
-                                       uids + y0, p_norm, norm_flag, global_E, ds, base, rows);                     \
-            } else if (PT_LP_SCAN_T && lds_t <= (160 << 10)) {                                                  \
+            if (PT_LP_SCAN_T && lds_t <= (160 << 10)) {                                                         \
                 const dim3 gt((unsigned)((max_ent + 63) / 64), gs.y), bt((unsigned)(64 * nw));                   \
                 PT_LPT(4) PT_LPT(8) PT_LPT(16)                                                                     \
             } else if (model == 0)                                                                                 \
@@ -1785,10 +1274,6 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
     PT_SHAPES(PT_LP)
 #undef PT_LP
 #undef PT_LPT
-#undef PT_LPV
-#undef PT_LPV_VARIANT
-#undef PT_LPG
-#undef PT_LPG_W3
     return hipErrorInvalidValue;
 }
 

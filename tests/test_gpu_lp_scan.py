@@ -1,14 +1,16 @@
-"""The two TransE link-prediction scan kernels give bit-identical key rows (pytest -m gpu).
+"""The TransE link-prediction scan rounds every pair's score the same way on each of its paths (pytest -m gpu).
 
 pt_lp_min_scores (global energy estimation, Parallel_Universe_Config.py:446-642) scores every local entity of a
-universe against each of its (key, universe) pairs and MINs the score into the key's row. Round 6 added
-k_lp_scan_v (entity row in registers, the pairs' base rows in LDS, two dims per v_pk_fma_f32) beside
-k_lp_scan_t (entity rows in LDS, base rows through scalar loads). Both keep the score's expression and its
-summation order (8 interleaved partial sums, dim d into partial d mod 8), so the rows must be equal bit for bit,
-for p 1 and 2, with and without normalization, at every register tier (dims up to 32 / 64 / 128 / 200), for a
-universe whose dim is below its launch's tier (zero-padded dims), and where k_lp_scan_v does not apply (dims
-not a multiple of 4, or above 200) - there both settings take k_lp_scan_t. The rows of both are checked
-against the oracle's scores elsewhere (test_gpu_pu, test_gpu_configs C4, test_gpu_realscale)."""
+universe against each of its (key, universe) pairs and MINs the score into the key's row. k_lp_scan_t's waves
+take a universe's pairs two at a time (one pass over the row feeds both sums) and the remainder one at a time.
+Until round 6 the compiler's fp contraction fused some of those loops' products into fmas and not others, so the
+same pair's score could differ by an ulp between the two paths. Every rounding is now explicit (x-hat = x * inv
+from the sum8 tree of fma squares; y = fma(sg, x-hat, b); |y| added, or fma(y, y, a); dim d into partial d mod 8),
+and a pair's score must not depend on the path: the rows of one call over all pairs equal, bit for bit, those of
+one call per pair (a universe with one pair takes the one-pair path). The rows of both are checked against the
+oracle's scores elsewhere (test_gpu_pu, test_gpu_configs C4, test_gpu_realscale)."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -21,49 +23,24 @@ def _need_gpu():
     assert torch.cuda.is_available(), "GPU tests need a visible HIP device"
 
 
-def _rows(L, n, unis, pairs, model, p, nf, E, n_keys, kernel):
+def _rows(n, unis, pairs, p, nf, E, n_keys):
+    L = n.lib()
     dev = torch.device("cuda")
     rows = torch.full((n_keys, E), float("inf"), device=dev)
     tup = torch.full((n_keys,), float("inf"), device=dev)
     lp_us = []
     for u in unis:
         U = n.LpUniverse()
-        U.ent, U.rel = u["ent"].data_ptr(), u["rel"].data_ptr()
-        U.normv = u["nv"].data_ptr() if u["nv"] is not None else None
+        U.ent, U.rel, U.normv = u["ent"].data_ptr(), u["rel"].data_ptr(), None
         U.ent_total, U.rel_total, U.dim = u["ent"].shape[0], u["rel"].shape[0], u["ent"].shape[1]
         U.d_ent_remap = u["remap"].data_ptr()
         lp_us.append(U)
     arr_u = (n.LpUniverse * len(lp_us))(*lp_us)
-    arr = np.ascontiguousarray(pairs, dtype=np.int32)
-    arr_p = arr.ctypes.data_as(__import__("ctypes").POINTER(n.LpPair))
-    old = L.pt_get_lp_scan_kernel()
-    n.check(L.pt_set_lp_scan_kernel(kernel))
-    try:
-        n.check(L.pt_lp_min_scores(arr_u, len(lp_us), model, p, nf, arr_p, len(arr), E, n.ptr(rows), n.ptr(tup),
-                                   n.stream()))
-        torch.cuda.synchronize()
-    finally:
-        n.check(L.pt_set_lp_scan_kernel(old))
+    arr = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 5)
+    arr_p = arr.ctypes.data_as(ctypes.POINTER(n.LpPair))
+    n.check(L.pt_lp_min_scores(arr_u, len(lp_us), 0, p, nf, arr_p, len(arr), E, n.ptr(rows), n.ptr(tup), n.stream()))
+    torch.cuda.synchronize()
     return rows.cpu(), tup.cpu()
-
-
-def _case(dims, E, n_keys, seed, model=0):
-    g = torch.Generator().manual_seed(seed)
-    rng = np.random.default_rng(seed)
-    dev = torch.device("cuda")
-    unis, pairs = [], []
-    for k, D in enumerate(dims):
-        Eu = int(rng.integers(40, 700))   # not a multiple of the 256-entity workgroup: partial waves and lanes
-        Ru = int(rng.integers(2, 9))
-        ent = (torch.rand(Eu, D, generator=g) * 2 - 1).to(dev)
-        rel = (torch.rand(Ru, D, generator=g) * 2 - 1).to(dev)
-        nv = (torch.rand(Ru, D, generator=g) * 2 - 1).to(dev) if model == 1 else None
-        remap = torch.from_numpy(np.sort(rng.choice(E, Eu, replace=False)).astype(np.int64)).to(dev)
-        unis.append({"ent": ent, "rel": rel, "nv": nv, "remap": remap})
-        for key in range(n_keys):
-            if rng.random() < 0.7:   # the universes holding the key's anchor and relation
-                pairs.append((key, k, int(rng.integers(Eu)), int(rng.integers(Ru)), key % 2))
-    return unis, np.array(pairs, dtype=np.int32).reshape(-1, 5)
 
 
 def _diff(a, b):
@@ -71,48 +48,33 @@ def _diff(a, b):
     bad = ai != bi
     if not bad.any():
         return None
-    fin = torch.isfinite(a) & torch.isfinite(b)
-    ulp = (ai.long() - bi.long()).abs()[bad & fin]
-    return "%d of %d cells differ (%d where one is inf), ulps max %d median %d; e.g. %s vs %s" % (
-        int(bad.sum()), bad.numel(), int((bad & ~fin).sum()), int(ulp.max()) if len(ulp) else -1,
-        int(ulp.median()) if len(ulp) else -1, a[bad][:4].tolist(), b[bad][:4].tolist())
-
-
-@pytest.mark.parametrize("p,nf", [(1, 1), (2, 0)])
-@pytest.mark.parametrize("D", [20, 64, 100, 152, 200])
-def test_scan_kernels_bit_identical_per_dim(D, p, nf):
-    from openke import _native as n
-    L = n.lib()
-    E, n_keys = 2000, 11
-    unis, pairs = _case([D], E, n_keys, seed=D + p)
-    r1, t1 = _rows(L, n, unis, pairs, 0, p, nf, E, n_keys, 1)
-    for k in (0, 2, 3):
-        r0, t0 = _rows(L, n, unis, pairs, 0, p, nf, E, n_keys, k)
-        d = _diff(r0, r1)
-        assert d is None, "kernel %d, D %d p %d nf %d: %s" % (k, D, p, nf, d)
+    ulp = (ai.long() - bi.long()).abs()[bad & torch.isfinite(a) & torch.isfinite(b)]
+    return "%d of %d cells differ, ulps max %d; e.g. %s vs %s" % (
+        int(bad.sum()), bad.numel(), int(ulp.max()) if len(ulp) else -1, a[bad][:4].tolist(), b[bad][:4].tolist())
 
 
 @pytest.mark.parametrize("p,nf", [(1, 1), (2, 1), (1, 0), (2, 0)])
-def test_scan_kernels_bit_identical(p, nf):
+@pytest.mark.parametrize("D", [20, 50, 64, 100, 200])
+def test_scan_paths_round_alike(D, p, nf):
     from openke import _native as n
-    L = n.lib()
-    E, n_keys = 3000, 37
-    # tiers: 20 -> 32, 64, 100 -> 128, 200 (p = 1); 152 and 196 share the 200 tier's launch with 200, below it
-    # (zero-padded dims); 50 and 204 (the same row shape as 200, a launch of its own): k_lp_scan_t under both
-    # settings, as every dim above 128 at p = 2
-    unis, pairs = _case([20, 64, 100, 152, 196, 200, 200, 50, 204], E, n_keys, seed=7 + p + 3 * nf)
-    r1, t1 = _rows(L, n, unis, pairs, 0, p, nf, E, n_keys, 1)
-    for k in (0, 2, 3):
-        r0, t0 = _rows(L, n, unis, pairs, 0, p, nf, E, n_keys, k)
-        assert torch.isfinite(r0).any()
-        d = _diff(r0, r1)
-        assert d is None, "kernel %d: %s" % (k, d)
-        assert torch.equal(t0.view(torch.int32), t1.view(torch.int32))
-
-
-def test_scan_kernel_switch_validates():
-    from openke import _native as n
-    L = n.lib()
-    assert L.pt_get_lp_scan_kernel() == 0   # the tiled kernel is the default
-    assert L.pt_set_lp_scan_kernel(4) != 0
-    assert L.pt_get_lp_scan_kernel() == 0
+    g = torch.Generator().manual_seed(D * 7 + p + 3 * nf)
+    rng = np.random.default_rng(D + 11 * p + nf)
+    dev = torch.device("cuda")
+    E, n_keys = 2000, 29
+    Eu, Ru = int(rng.integers(100, 700)), 5   # not a multiple of the 64-row tile: a partial last tile
+    uni = {"ent": (torch.rand(Eu, D, generator=g) * 2 - 1).to(dev),
+           "rel": (torch.rand(Ru, D, generator=g) * 2 - 1).to(dev),
+           "remap": torch.from_numpy(np.sort(rng.choice(E, Eu, replace=False)).astype(np.int64)).to(dev)}
+    # 29 keys, one pair each: the 8 waves take pairs (w, w + 8) through the two-pair pass, the rest one at a time
+    pairs = [(k, 0, int(rng.integers(Eu)), int(rng.integers(Ru)), k % 2) for k in range(n_keys)]
+    together, t_tog = _rows(n, [uni], pairs, p, nf, E, n_keys)
+    alone = torch.full((n_keys, E), float("inf"))
+    t_alone = torch.full((n_keys,), float("inf"))
+    for pr in pairs:   # one pair per call: the one-pair path
+        r1, t1 = _rows(n, [uni], [pr], p, nf, E, n_keys)
+        alone = torch.minimum(alone, r1)
+        t_alone = torch.minimum(t_alone, t1)
+    assert torch.isfinite(together).sum() == n_keys * Eu
+    d = _diff(together, alone)
+    assert d is None, "D %d p %d nf %d: %s" % (D, p, nf, d)
+    assert torch.equal(t_tog.view(torch.int32), t_alone.view(torch.int32))
