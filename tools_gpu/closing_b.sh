@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round 6 (t), closing evidence B on the final build: the driver's command (counted traffic from the committed
-# pmc_c2.json), the C4 / C3 / C5 lines with 8-way shares and drop-in legs and their kernel stats, the reference
-# experiment's scale, the N = 2 gloo rehearsal and smoke().
+# Closing evidence B on the final build (after closing_a.sh's pmc_c2.json and pmc_c*_chain.json are committed under
+# profiles/): the driver's command with counted traffic, the C4 / C3 / C5 lines with 8-way shares and drop-in legs
+# and their kernel stats, the reference experiment's scale, the N = 2 gloo rehearsal and smoke().
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-T=${TAG:-r06t}
+T=${TAG:-closingb}
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${T}_default.log 2>&1 || exit $?
 for w in c4 c3 c5; do
   timeout -k 10 400 python3 bench.py --workload $w --steps 2 --warmup 1 --place-world 8 --no-cpu-baseline \
