@@ -29,25 +29,67 @@ struct KeyHash {
 
 struct pt_known {
     std::unordered_set<Key, KeyHash> set;
+    std::vector<Key> triples;   // as given (duplicates included): the partner index is sorted from these
     bool has(int64_t h, int64_t t, int64_t r) const { return set.count(Key{h, t, r}) != 0; }
-    // (anchor, r) -> partner entities, per side (0: heads of (t, r); 1: tails of (h, r)); built on first use
-    struct PairHash {
-        size_t operator()(const std::pair<int64_t, int64_t> &p) const {
-            const uint64_t x = (uint64_t)p.first * 0x9E3779B97F4A7C15ULL ^ (uint64_t)p.second * 0xC2B2AE3D27D4EB4FULL;
-            return (size_t)(x ^ (x >> 29));
-        }
+    // (anchor, r, partner) rows per side (0: heads of (t, r); 1: tails of (h, r)), sorted, so a query's partners
+    // are one contiguous ascending run found by bisection; built on first use, the two sides on two threads (a
+    // sort of the known triples instead of a hash map of vectors: C4's 318 k triples)
+    struct Row {
+        int64_t a, r, p;
+        bool operator<(const Row &o) const { return a != o.a ? a < o.a : r != o.r ? r < o.r : p < o.p; }
     };
     mutable std::mutex mu;
     mutable bool indexed = false;
-    mutable std::unordered_map<std::pair<int64_t, int64_t>, std::vector<int64_t>, PairHash> by_side[2];
+    mutable std::vector<Row> by_side[2];
     void index() const {
         std::lock_guard<std::mutex> g(mu);
         if (indexed) return;
-        for (const Key &k : set) {
-            by_side[0][{k.t, k.r}].push_back(k.h);
-            by_side[1][{k.h, k.r}].push_back(k.t);
-        }
+        auto build = [this](int side) {
+            // a counting sort by anchor, then each anchor's few rows sorted by (r, partner)
+            auto &v = by_side[side];
+            int64_t amax = -1, amin = 0;
+            for (const Key &k : triples) {
+                amax = std::max(amax, side == 0 ? k.t : k.h);
+                amin = std::min(amin, side == 0 ? k.t : k.h);
+            }
+            if (amin < 0 || amax >= (int64_t(1) << 32)) {   // (ids a counting sort cannot index: a plain sort)
+                for (const Key &k : triples) v.push_back(side == 0 ? Row{k.t, k.r, k.h} : Row{k.h, k.r, k.t});
+                std::sort(v.begin(), v.end());
+                v.erase(std::unique(v.begin(), v.end(), [](const Row &x, const Row &y) {
+                            return x.a == y.a && x.r == y.r && x.p == y.p;
+                        }),
+                        v.end());
+                return;
+            }
+            std::vector<int64_t> start((size_t)(amax + 2), 0);
+            for (const Key &k : triples) ++start[(size_t)((side == 0 ? k.t : k.h) + 1)];
+            for (size_t a = 1; a < start.size(); ++a) start[a] += start[a - 1];
+            v.resize(triples.size());
+            {
+                std::vector<int64_t> fill(start.begin(), start.end() - 1);
+                for (const Key &k : triples)
+                    v[(size_t)fill[(size_t)(side == 0 ? k.t : k.h)]++] =
+                        side == 0 ? Row{k.t, k.r, k.h} : Row{k.h, k.r, k.t};
+            }
+            for (size_t a = 0; a + 1 < start.size(); ++a)
+                if (start[a + 1] - start[a] > 1) std::sort(v.begin() + start[a], v.begin() + start[a + 1]);
+            v.erase(std::unique(v.begin(), v.end(), [](const Row &x, const Row &y) {
+                        return x.a == y.a && x.r == y.r && x.p == y.p;
+                    }),
+                    v.end());   // (a triple listed twice is one known triple)
+        };
+        std::thread other(build, 1);
+        build(0);
+        other.join();
         indexed = true;
+    }
+    // the run of (a, r)'s partners in side `side`'s rows
+    std::pair<const Row *, const Row *> partners(int side, int64_t a, int64_t r) const {
+        const auto &v = by_side[side];
+        const auto lo = std::lower_bound(v.begin(), v.end(), Row{a, r, INT64_MIN});
+        auto hi = lo;
+        while (hi != v.end() && hi->a == a && hi->r == r) ++hi;
+        return {v.data() + (lo - v.begin()), v.data() + (hi - v.begin())};
     }
 };
 
@@ -84,7 +126,11 @@ extern "C" int pt_known_create(const int64_t *h, const int64_t *t, const int64_t
     if (!out || (n > 0 && (!h || !t || !r))) return pt::fail(PT_EINVAL, "pt_known_create: null argument");
     auto *k = new pt_known();
     k->set.reserve((size_t)n * 2 + 16);
-    for (int64_t i = 0; i < n; ++i) k->set.insert(Key{h[i], t[i], r[i]});
+    k->triples.resize((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        k->triples[(size_t)i] = Key{h[i], t[i], r[i]};
+        k->set.insert(k->triples[(size_t)i]);
+    }
     *out = k;
     return PT_OK;
 }
@@ -121,18 +167,12 @@ extern "C" int pt_known_partners(const pt_known *k, int32_t side, int64_t n, con
     if (!k || (n > 0 && (!anchor || !rel)) || !off || (side != 0 && side != 1))
         return pt::fail(PT_EINVAL, "pt_known_partners: bad argument");
     k->index();
-    const auto &m = k->by_side[side];
     off[0] = 0;
     for (int64_t q = 0; q < n; ++q) {
-        const auto it = m.find({anchor[q], rel[q]});
-        int64_t c = 0;
-        if (it != m.end()) {
-            for (int64_t e : it->second) {
-                if (list) list[off[q] + c] = e;
-                ++c;
-            }
-        }
-        if (list) std::sort(list + off[q], list + off[q] + c);   // ascending: pt_rank_types bisects it
+        const auto run = k->partners(side, anchor[q], rel[q]);   // ascending: pt_rank_types bisects it
+        const int64_t c = run.second - run.first;
+        if (list)
+            for (int64_t i = 0; i < c; ++i) list[off[q] + i] = run.first[i].p;
         off[q + 1] = off[q] + c;
     }
     return PT_OK;
