@@ -316,11 +316,6 @@ int pt_lp_min_scores(const pt_lp_universe *us, int64_t n_universes, int32_t mode
 /* d_key_tuple (optional, [n_keys], init +inf): MIN over the pairs' universes of the null_vector score
  * _calc(anchor, 0, r) / _calc(0, anchor, r) on the raw anchor row (calc_tuple_score,
  * Parallel_Universe_Config.py:405-416, transmit_tuple_max_score :494-514) */
-/* The TransH scan kernel of pt_lp_min_scores, process-wide: 0 (default) = k_lp_scan_h (the entity row in registers)
- * where the launch's largest dim is at most 32, else k_lp_scan_t; 1 = always k_lp_scan_t. Both give bit-identical
- * key rows; the switch exists for that test and for A/B timing. */
-int pt_set_lp_scan_kernel(int32_t k);
-int32_t pt_get_lp_scan_kernel(void);
 
 /* Ranks straight from global-order score rows (device): query q is ranked on row d_row_of[q] with
  * truth entity d_truth[q]; +inf entries are replaced by d_repl[q] when d_repl is non-NULL

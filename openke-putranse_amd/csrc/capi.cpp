@@ -1222,13 +1222,6 @@ extern "C" int pt_set_universe_team_width(int32_t w) {
 }
 extern "C" int32_t pt_get_universe_team_width(void) { return g_team_width.load(); }
 
-extern "C" int pt_set_lp_scan_kernel(int32_t k) {
-    PT_CHECK(k == 0 || k == 1, PT_EINVAL, "pt_set_lp_scan_kernel: 0 or 1");
-    pt::set_lp_scan_kernel(k);
-    return PT_OK;
-}
-extern "C" int32_t pt_get_lp_scan_kernel(void) { return pt::get_lp_scan_kernel(); }
-
 
 // Train many universes with the persistent multi-universe kernel (universes.hip).
 struct pt_universe_set {

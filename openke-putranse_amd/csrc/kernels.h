@@ -156,9 +156,6 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
                          const int32_t *uids, int64_t n_active, int64_t dim, int64_t max_ent, int model, int p_norm,
                          int norm_flag, int64_t global_E, int64_t ds, float *base, float *normal, float *rows,
                          float *tuple_min, hipStream_t st);
-// the TransH scan kernel of launch_lp_min: 0 = k_lp_scan_h where it applies (default), 1 = k_lp_scan_t
-void set_lp_scan_kernel(int k);
-int get_lp_scan_kernel();
 
 hipError_t launch_torch_init(const pt_torch_init_job *d_jobs, int64_t n, hipStream_t st);
 hipError_t launch_rank_rows(const float *rows, int64_t E, const int64_t *row_of, const int64_t *truth,

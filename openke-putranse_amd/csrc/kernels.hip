@@ -15,7 +15,6 @@
 // only to rows with a nonzero gradient (identical to the dense update).
 #include <hip/hip_runtime.h>
 
-#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 
@@ -1000,7 +999,7 @@ __global__ __launch_bounds__(64 * NW) void k_lp_scan_t(const LpUniverseDev *__re
                     sum8xn<1, 2>(D, [&](int, int d) { return __builtin_fmaf(sg, xr[d] * inv, b[d]); }, a1);
                 acc = a1[0];
             } else {
-                // TransH (_transfer, TransH.py:52-58, then F.normalize), every rounding explicit as k_lp_scan_h's:
+                // TransH (_transfer, TransH.py:52-58, then F.normalize), every rounding explicit:
                 // xd = x . w; t = fma(-xd, w, x); sc = 1 / max(|t|, eps); y = fma(sg, t * sc, b)
                 const float *nw = normal + pi * ds;
                 const float xd = sum8_fma(D, [&](int d) { return xr[d]; }, [&](int d) { return nw[d]; });
@@ -1024,77 +1023,6 @@ __global__ __launch_bounds__(64 * NW) void k_lp_scan_t(const LpUniverseDev *__re
                 if (bits < *cell) atomicMin(cell, bits);
             }
         }
-    }
-}
-
-// k_lp_scan_h: the TransH scan for small dims with each lane's entity row in VGPRs (round 6). k_lp_scan_t reads
-// the row from its LDS tile three times per pair (the projection's dot product, the projected norm, the score) and
-// waits on each 8-dim group's scalar and LDS loads together; here the row is registers, the pair's normal and base
-// words come by scalar loads shared by the wave's 64 entities, and no LDS is used, so a wave's only waits are
-// those scalar loads and the key-row cells. Dims past the universe's D are zeros (x, w and b), whose terms are exact
-// +0s: the sums keep k_lp_scan_t's explicit forms and order, and the rows are bit-identical
-// (tests/test_gpu_lp_scan.py).
-template <int DV, int NW>
-__global__ __launch_bounds__(64 * NW) void k_lp_scan_h(const LpUniverseDev *__restrict__ us, const LpPair *__restrict__ pairs,
-                                                   const int64_t *__restrict__ uoff, const int32_t *__restrict__ uids,
-                                                   int p_norm, int norm_flag, int64_t global_E, int64_t ds,
-                                                   const float *__restrict__ base, const float *__restrict__ normal,
-                                                   float *__restrict__ rows) {
-#pragma clang fp contract(off)   // every fused step is an explicit fma below
-    const int lane = (int)threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int32_t u = uids[blockIdx.y];
-    const LpUniverseDev U = us[u];
-    const int D = (int)U.dim;
-    const int64_t e0 = ((int64_t)blockIdx.x * NW + wave) * 64;
-    if (e0 >= U.ent_total) return;   // (no barrier in this kernel: a wave may leave alone)
-    const int64_t e = e0 + lane;
-    const bool live = e < U.ent_total;
-    float x[DV];
-    const float *src = U.ent + (live ? e : 0) * D;
-#pragma unroll
-    for (int d = 0; d < DV; ++d) x[d] = d < D ? src[d] : 0.f;
-    const int64_t col = live ? U.remap[e] : 0;
-    const int64_t p0 = uoff[2 * u], p1 = uoff[2 * u + 1];
-    auto tree = [](const float (&a)[8]) { return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])); };
-    for (int64_t pi = p0; pi < p1; ++pi) {
-        const LpPair pr = pairs[pi];
-        int *cell = reinterpret_cast<int *>(rows + (int64_t)pr.key * global_E + col);
-        const int old = live ? __builtin_nontemporal_load(cell) : 0;   // read before the sums
-        const float *nw = normal + pi * ds, *b = base + pi * ds;
-        float w[DV], bb[DV];
-#pragma unroll
-        for (int d = 0; d < DV; ++d) {
-            w[d] = d < D ? nw[d] : 0.f;
-            bb[d] = d < D ? b[d] : 0.f;
-        }
-        const float sg = pr.side == 0 ? 1.f : -1.f;   // side 0: x-hat + b; side 1: b - x-hat
-        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int d = 0; d < DV; ++d) a[d & 7] = __builtin_fmaf(x[d], w[d], a[d & 7]);
-        const float xd = tree(a);
-        float t[DV];
-#pragma unroll
-        for (int d = 0; d < DV; ++d) t[d] = __builtin_fmaf(-xd, w[d], x[d]);
-        float sc = 1.f;
-        if (norm_flag) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) a[k] = 0.f;
-#pragma unroll
-            for (int d = 0; d < DV; ++d) a[d & 7] = __builtin_fmaf(t[d], t[d], a[d & 7]);
-            const float n = sqrtf(tree(a));
-            sc = 1.0f / (n > kEps ? n : kEps);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) a[k] = 0.f;
-#pragma unroll
-        for (int d = 0; d < DV; ++d) {
-            const float y = __builtin_fmaf(sg, t[d] * sc, bb[d]);
-            a[d & 7] = p_norm == 1 ? add_abs(a[d & 7], y) : __builtin_fmaf(y, y, a[d & 7]);
-        }
-        const float acc = tree(a);
-        const float score = p_norm == 1 ? acc : sqrtf(acc);
-        const int bits = __float_as_int(score);
-        if (live && bits < old) atomicMin(cell, bits);
     }
 }
 
@@ -1293,24 +1221,12 @@ static int lp_waves() {
     }();
     return nw;
 }
-// The TransH scan of a job: 0 = k_lp_scan_h where the job's largest dim fits its registers (<= 32), else
-// k_lp_scan_t; 1 = always k_lp_scan_t (pt_set_lp_scan_kernel: the bit-identity test and A/B timing)
-static std::atomic<int> g_lp_scan_kernel{0};
-void set_lp_scan_kernel(int k) { g_lp_scan_kernel.store(k); }
-int get_lp_scan_kernel() { return g_lp_scan_kernel.load(); }
-static int lp_scan_h_dv(int64_t dim) {
-    for (int dv : {8, 16, 20, 24, 32})
-        if (dim <= dv) return dv;
-    return 0;
-}
-
 hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n_pairs, const int64_t *uoff,
                          const int32_t *uids, int64_t n_active, int64_t dim, int64_t max_ent, int model, int p_norm,
                          int norm_flag, int64_t global_E, int64_t ds, float *base, float *normal, float *rows,
                          float *tuple_min, hipStream_t st) {
     if (n_pairs <= 0) return hipSuccess;
     const Shape s = pick_shape(dim);
-    const int hdv = model == 1 && g_lp_scan_kernel.load() == 0 ? lp_scan_h_dv(dim) : 0;
     // the transposed scan's tile of 64 rows in LDS (row stride dim + 1)
     const size_t lds_t = sizeof(float) * 64 * (size_t)(dim + 1);
     const int nw = lp_waves();
@@ -1341,10 +1257,6 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
             hipLaunchKernelGGL((dev::k_lp_scan_t<1, NW_>), gt, bt, lds_t, st, us, pairs, uoff, uids + y0, p_norm,    \
                                norm_flag, global_E, ds, base, normal, rows);                                       \
     }
-#define PT_LPH(DV_)                                                                                                \
-    if (hdv == DV_)                                                                                                \
-        hipLaunchKernelGGL((dev::k_lp_scan_h<DV_, 4>), gh, bh, 0, st, us, pairs, uoff, uids + y0, p_norm, norm_flag, \
-                           global_E, ds, base, normal, rows);
 #define PT_LP(G_, V_, K_)                                                                                          \
     if (s.G == G_ && s.VEC == V_ && s.KCH == K_) {                                                               \
         for (int64_t y0 = 0; y0 < n_active; y0 += 65535) {                                                         \
@@ -1357,10 +1269,7 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
                     hipLaunchKernelGGL((dev::k_lp_bases<1, G_, V_, K_>), gb, block, 0, st, us, pairs, n_pairs,    \
                                        p_norm, norm_flag, ds, base, normal, tuple_min);                            \
             }                                                                                                      \
-            if (hdv) {                                                                                             \
-                const dim3 gh((unsigned)((max_ent + 255) / 256), gs.y), bh(256);                                   \
-                PT_LPH(8) PT_LPH(16) PT_LPH(20) PT_LPH(24) PT_LPH(32)                                              \
-            } else if (PT_LP_SCAN_T && lds_t <= (160 << 10)) {                                                  \
+if (PT_LP_SCAN_T && lds_t <= (160 << 10)) {                                                         \
                 const dim3 gt((unsigned)((max_ent + 63) / 64), gs.y), bt((unsigned)(64 * nw));                   \
                 PT_LPT(4) PT_LPT(8) PT_LPT(16)                                                                     \
             } else if (model == 0)                                                                                 \
@@ -1375,7 +1284,6 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
     PT_SHAPES(PT_LP)
 #undef PT_LP
 #undef PT_LPT
-#undef PT_LPH
     return hipErrorInvalidValue;
 }
 

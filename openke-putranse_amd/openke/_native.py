@@ -123,8 +123,6 @@ SIGNATURES = {
     "pt_universe_set_profiling": (ctypes.c_int, [c_vp, c_i32]),
     "pt_set_universe_team_width": (ctypes.c_int, [c_i32]),
     "pt_get_universe_team_width": (c_i32, []),
-    "pt_set_lp_scan_kernel": (ctypes.c_int, [c_i32]),
-    "pt_get_lp_scan_kernel": (c_i32, []),
     "pt_universe_set_teams": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "pt_universe_set_states": (ctypes.c_int, [c_vp, c_i64, c_vp]),
     "pt_universe_set_reset": (ctypes.c_int, [c_vp]),

@@ -80,46 +80,3 @@ def test_scan_paths_round_alike(D, p, nf):
     d = _diff(together, alone)
     assert d is None, "D %d p %d nf %d: %s" % (D, p, nf, d)
     assert torch.equal(t_tog.view(torch.int32), t_alone.view(torch.int32))
-
-
-@pytest.mark.parametrize("p,nf", [(1, 1), (2, 1), (1, 0), (2, 0)])
-def test_transh_scan_kernels_bit_identical(p, nf):
-    """TransH: k_lp_scan_h (the row in registers, D <= 32) against k_lp_scan_t, one call each over the same
-    universes: dims 5, 8, 20 and 24 take register tiers (20 and 24 in one launch: 20's dims past D are zeros), 36
-    takes k_lp_scan_t under both settings. Rows and null-vector tuple scores equal bit for bit."""
-    from openke import _native as n
-    L = n.lib()
-    g = torch.Generator().manual_seed(5 + p + 3 * nf)
-    rng = np.random.default_rng(17 + p + nf)
-    dev = torch.device("cuda")
-    E, n_keys = 3000, 41
-    unis, pairs = [], []
-    for k, D in enumerate([5, 8, 20, 24, 36]):
-        Eu, Ru = int(rng.integers(100, 700)), 6
-        unis.append({"ent": (torch.rand(Eu, D, generator=g) * 2 - 1).to(dev),
-                     "rel": (torch.rand(Ru, D, generator=g) * 2 - 1).to(dev),
-                     "nv": (torch.rand(Ru, D, generator=g) * 2 - 1).to(dev),
-                     "remap": torch.from_numpy(np.sort(rng.choice(E, Eu, replace=False)).astype(np.int64)).to(dev)})
-        for key in range(n_keys):
-            if rng.random() < 0.7:
-                pairs.append((key, k, int(rng.integers(Eu)), int(rng.integers(Ru)), key % 2))
-    old = L.pt_get_lp_scan_kernel()
-    try:
-        n.check(L.pt_set_lp_scan_kernel(1))
-        r1, t1 = _rows(n, unis, pairs, p, nf, E, n_keys, model=1)
-        n.check(L.pt_set_lp_scan_kernel(0))
-        r0, t0 = _rows(n, unis, pairs, p, nf, E, n_keys, model=1)
-    finally:
-        n.check(L.pt_set_lp_scan_kernel(old))
-    assert torch.isfinite(r0).any()
-    d = _diff(r0, r1)
-    assert d is None, "p %d nf %d: %s" % (p, nf, d)
-    assert torch.equal(t0.view(torch.int32), t1.view(torch.int32))
-
-
-def test_scan_kernel_switch_validates():
-    from openke import _native as n
-    L = n.lib()
-    assert L.pt_get_lp_scan_kernel() == 0   # the register-row TransH scan is the default
-    assert L.pt_set_lp_scan_kernel(2) != 0
-    assert L.pt_get_lp_scan_kernel() == 0
