@@ -895,15 +895,6 @@ __device__ __forceinline__ void sum8xn(int D, F f, float (&r)[NP]) {
         r[q] = ((a[q][0] + a[q][1]) + (a[q][2] + a[q][3])) + ((a[q][4] + a[q][5]) + (a[q][6] + a[q][7]));
 }
 
-// sum over d < D of fa(d) * fb(d) in the sum8 form, each term fused into its partial: a[d mod 8] = fma(fa(d), fb(d),
-// a[d mod 8]) in increasing d, then sum8's tree (the TransH scans' explicit dot products)
-template <typename FA, typename FB>
-__device__ __forceinline__ float sum8_fma(int D, FA fa, FB fb) {
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int d = 0; d < D; ++d) a[d & 7] = __builtin_fmaf(fa(d), fb(d), a[d & 7]);
-    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-}
-
 #ifndef PT_LP_PAIRS
 #ifndef PT_LP_PAIRS
 #define PT_LP_PAIRS 2   // (measured r05, C4 k_lp_scan_t total: 1 pair 137.9 ms, 2 pairs 99.4, 4 pairs 105.3, 8 pairs 128.5)
@@ -999,22 +990,21 @@ __global__ __launch_bounds__(64 * NW) void k_lp_scan_t(const LpUniverseDev *__re
                     sum8xn<1, 2>(D, [&](int, int d) { return __builtin_fmaf(sg, xr[d] * inv, b[d]); }, a1);
                 acc = a1[0];
             } else {
-                // TransH (_transfer, TransH.py:52-58, then F.normalize), every rounding explicit:
-                // xd = x . w; t = fma(-xd, w, x); sc = 1 / max(|t|, eps); y = fma(sg, t * sc, b)
                 const float *nw = normal + pi * ds;
-                const float xd = sum8_fma(D, [&](int d) { return xr[d]; }, [&](int d) { return nw[d]; });
-                auto tproj = [&](int d) { return __builtin_fmaf(-xd, nw[d], xr[d]); };
+                const float xd = sum8(D, [&](int d) { return xr[d] * nw[d]; });
                 float sc = 1.f;
                 if (norm_flag) {
-                    const float n = sqrtf(sum8_fma(D, tproj, tproj));
+                    const float n = sqrtf(sum8(D, [&](int d) {
+                        const float t = xr[d] - xd * nw[d];
+                        return t * t;
+                    }));
                     sc = 1.0f / (n > kEps ? n : kEps);
                 }
-                float a1[1];
-                if (p_norm == 1)
-                    sum8xn<1, 1>(D, [&](int, int d) { return __builtin_fmaf(sg, tproj(d) * sc, b[d]); }, a1);
-                else
-                    sum8xn<1, 2>(D, [&](int, int d) { return __builtin_fmaf(sg, tproj(d) * sc, b[d]); }, a1);
-                acc = a1[0];
+                acc = p_norm == 1 ? sum8(D, [&](int d) { return fabsf(sg * ((xr[d] - xd * nw[d]) * sc) + b[d]); })
+                                  : sum8(D, [&](int d) {
+                                        const float v = sg * ((xr[d] - xd * nw[d]) * sc) + b[d];
+                                        return v * v;
+                                    });
             }
             const float score = p_norm == 1 ? acc : sqrtf(acc);
             if (live) {
@@ -1269,7 +1259,7 @@ hipError_t launch_lp_min(const LpUniverseDev *us, const LpPair *pairs, int64_t n
                     hipLaunchKernelGGL((dev::k_lp_bases<1, G_, V_, K_>), gb, block, 0, st, us, pairs, n_pairs,    \
                                        p_norm, norm_flag, ds, base, normal, tuple_min);                            \
             }                                                                                                      \
-if (PT_LP_SCAN_T && lds_t <= (160 << 10)) {                                                         \
+            if (PT_LP_SCAN_T && lds_t <= (160 << 10)) {                                                         \
                 const dim3 gt((unsigned)((max_ent + 63) / 64), gs.y), bt((unsigned)(64 * nw));                   \
                 PT_LPT(4) PT_LPT(8) PT_LPT(16)                                                                     \
             } else if (model == 0)                                                                                 \

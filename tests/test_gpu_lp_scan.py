@@ -23,7 +23,7 @@ def _need_gpu():
     assert torch.cuda.is_available(), "GPU tests need a visible HIP device"
 
 
-def _rows(n, unis, pairs, p, nf, E, n_keys, model=0):
+def _rows(n, unis, pairs, p, nf, E, n_keys):
     L = n.lib()
     dev = torch.device("cuda")
     rows = torch.full((n_keys, E), float("inf"), device=dev)
@@ -31,16 +31,14 @@ def _rows(n, unis, pairs, p, nf, E, n_keys, model=0):
     lp_us = []
     for u in unis:
         U = n.LpUniverse()
-        U.ent, U.rel = u["ent"].data_ptr(), u["rel"].data_ptr()
-        U.normv = u["nv"].data_ptr() if u.get("nv") is not None else None
+        U.ent, U.rel, U.normv = u["ent"].data_ptr(), u["rel"].data_ptr(), None
         U.ent_total, U.rel_total, U.dim = u["ent"].shape[0], u["rel"].shape[0], u["ent"].shape[1]
         U.d_ent_remap = u["remap"].data_ptr()
         lp_us.append(U)
     arr_u = (n.LpUniverse * len(lp_us))(*lp_us)
     arr = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 5)
     arr_p = arr.ctypes.data_as(ctypes.POINTER(n.LpPair))
-    n.check(L.pt_lp_min_scores(arr_u, len(lp_us), model, p, nf, arr_p, len(arr), E, n.ptr(rows), n.ptr(tup),
-                               n.stream()))
+    n.check(L.pt_lp_min_scores(arr_u, len(lp_us), 0, p, nf, arr_p, len(arr), E, n.ptr(rows), n.ptr(tup), n.stream()))
     torch.cuda.synchronize()
     return rows.cpu(), tup.cpu()
 
